@@ -1,0 +1,203 @@
+/*
+ * sdrg.h — C ABI of the MI355X (gfx950) IQ-stream DSP engine.
+ *
+ * This is the drop-in boundary for the reference's per-frame hot path
+ * (alexandreGellibert/SDR-for-Android-lib, paths relative to the reference root):
+ *
+ *   FFTProcessor::configure / process / get*      src/dsp/fft_process.h:29-55, fft_process.cpp:20-379
+ *   processSSB_opt(iq, fs, upper, pcm, pulse, mode) src/ssb/ssb_demod_opt.h:64-65, ssb_demod_opt.cpp:221-296
+ *   SSBProcessor (queue + worker)                  src/ssb/ssb_processor.h:24-58
+ *   JNI applyConfig / read / set*                  src/sdr-bridge-java-soapy.cpp:625-764, 878-1141
+ *   SDRConfig fields                               java/fr/intuite/sdr/bridge/SDRBridge.kt:23-37
+ *
+ * The reference runs one receiver ("stream") per process and processes one frame of
+ * samplesPerReading complex samples per call.  The engine generalises that to B independent
+ * streams processed one frame each per call ("B streams x 1 frame per launch"): every piece of
+ * per-stream state the reference keeps in FFTProcessor members or in processSSB_opt's
+ * function statics is kept per stream in HBM, so stream s of a batch behaves exactly like a
+ * reference process that was fed stream s's frames in order.
+ *
+ * Conventions: plain pointers and sizes, no exceptions across the boundary, every entry point
+ * returns an sdrg_status (0 = OK).  A handle is not safe for concurrent calls from several
+ * threads; configuration changes are applied at the next process call (frame boundary), which
+ * replaces the reference's racy configure()-while-process() pattern (sdr-bridge-java-soapy.cpp:878-913).
+ */
+#ifndef SDRG_H
+#define SDRG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDRG_ABI_VERSION 1
+
+/* Status codes.  The reference's JNI layer reports failure as false/nullptr/0 plus a log line
+ * (e.g. applyConfig returns false when a device call throws, sdr-bridge-java-soapy.cpp:1115-1118). */
+typedef enum sdrg_status {
+    SDRG_OK = 0,
+    SDRG_E_INVALID = -1,      /* bad argument (null pointer, non-positive size, ...) */
+    SDRG_E_UNSUPPORTED = -2,  /* e.g. samples_per_reading not a power of two in [64, 65536] */
+    SDRG_E_NOMEM = -3,        /* device allocation failed */
+    SDRG_E_HIP = -4,          /* a HIP runtime call failed (message via sdrg_last_error) */
+    SDRG_E_NODEVICE = -5      /* no gfx950 device / HIP runtime not usable */
+} sdrg_status;
+
+/* Raw IQ sample formats.  The reference stream is always CF32 (sdr-bridge-java-soapy.cpp:263);
+ * the device drivers convert their native CU8 / CS8 / CS16 to CF32 before the hot path.  The
+ * engine fuses that conversion into its kernels with the convention
+ *   CS8: v/128      CU8: (v - 127.4f) * (1/128)  (the in-tree convertIQ, ssb_demod_opt.cpp:33-44)
+ *   CS16: v/32768   CF32: as is.  Samples are interleaved I,Q. */
+typedef enum sdrg_iq_format {
+    SDRG_IQ_CF32 = 0,
+    SDRG_IQ_CS8 = 1,
+    SDRG_IQ_CU8 = 2,
+    SDRG_IQ_CS16 = 3
+} sdrg_iq_format;
+
+/* Which stages a process call runs (bitmask). */
+enum {
+    SDRG_STAGE_SPECTRUM = 1,  /* FFT -> |X|^2 -> fftshift (fft_process.cpp:42-97) */
+    SDRG_STAGE_STATS = 2,     /* evaluateSignalStrength (fft_process.cpp:122-379); needs SPECTRUM */
+    SDRG_STAGE_SSB = 4,       /* processSSB_opt (ssb_demod_opt.cpp:221-296) */
+    SDRG_STAGE_ALL = 7
+};
+
+/* Mirror of Kotlin SDRConfig (SDRBridge.kt:23-37) / the 9 JNI applyConfig arguments
+ * (sdr-bridge-java-soapy.cpp:1073-1085).  gain and refresh_* are carried for API parity only:
+ * gain is a device setting and the refresh periods are stored but never read by the reference. */
+typedef struct sdrg_config {
+    int64_t center_frequency;          /* Hz; the reference stores it as uint32 (bridge-config.h:18) */
+    int64_t sample_rate;               /* Hz; uint32 in the reference */
+    int32_t samples_per_reading;       /* frame size N */
+    int32_t freq_focus_range_khz;      /* focus half-width X in kHz */
+    int32_t gain;
+    int32_t sound_mode;                /* 0,1,2 (SDRBridge.kt:35-36); other values keep the last mode */
+    int64_t refresh_fft_ms;
+    int64_t refresh_peak_ms;
+    int64_t refresh_signal_strength_ms;
+} sdrg_config;
+
+/* Per-frame, per-stream outputs: exactly what soapyCallback reads through the FFTProcessor getters
+ * (sdr-bridge-java-soapy.cpp:446-455, fft_process.h:38-55), plus a few diagnostics for parity. */
+typedef struct sdrg_frame_record {
+    int64_t tracking_frequency;        /* getTrackingFrequency(): lround-ish of the float latch */
+    float mean_snr_db;                 /* getMeanSnrDb */
+    float mean_snr_sigma;              /* getMeanSnrSigma */
+    float peak_above_noise_mean_db;    /* getPeakAboveNoiseMeanDb */
+    float max_bin_snr_db;              /* getMaxBinSnrDb */
+    float max_bin_snr_sigma;           /* getMaxBinSnrSigma */
+    float best1khz_snr_db;             /* getBest1kHzSnrDb */
+    float best1khz_snr_sigma;          /* getBest1kHzSnrSigma */
+    float best1khz_center_freq_hz;     /* getBest1kHzCenterFreqHz */
+    float per_bin_mean;                /* getPerBinMean (noiseLevel callback) */
+    int32_t detection_flag;            /* getDetectionFlag: 0 or 3 */
+    /* diagnostics (not reference getters) */
+    int32_t peak_bin;                  /* focusLo + peakBinInFocus of this frame (-1 if no focus window) */
+    float abs_peak_db;                 /* in-focus peak, 10*log10f(P+1e-20) */
+    float signal_power_db;             /* focus-window mean power, dB */
+    int32_t valid;                     /* nRef >= 2 (fft_process.cpp:218-225) */
+    int32_t n_ref_windows;             /* reference windows collected */
+} sdrg_frame_record;
+
+/* Callback table mirroring the JNI read() callbacks (SDRBridge.kt:141-154,
+ * sdr-bridge-java-soapy.cpp:625-693).  Any entry may be NULL.  `stream` is the stream index in the
+ * batch.  The order of invocation per frame is soapyCallback's (sdr-bridge-java-soapy.cpp:458-475):
+ * fft, detection_flag, mean_snr, mean_snr_sigma, peak_frequency, peak_above_noise_mean, max_bin,
+ * best1khz, noise_level; pcm comes from the SSB worker (ssb_processor.cpp:103-113) and is invoked
+ * after them, only when the frame produced samples.  The audio-pulse and spectral-pulse callbacks
+ * belong to the pulse detectors, which are outside this engine. */
+typedef struct sdrg_callbacks {
+    void *user;
+    void (*fft)(void *user, int32_t stream, const float *power_shifted, int32_t n);        /* ([F)V  */
+    void (*detection_flag)(void *user, int32_t stream, int32_t flag);                     /* (I)V   */
+    void (*mean_snr)(void *user, int32_t stream, float mean_snr_db);                      /* (F)V   */
+    void (*mean_snr_sigma)(void *user, int32_t stream, float mean_snr_sigma);             /* (F)V   */
+    void (*peak_frequency)(void *user, int32_t stream, int64_t hz);                       /* (J)V   */
+    void (*pcm)(void *user, int32_t stream, const int16_t *pcm, int32_t n);               /* ([S)V  */
+    void (*peak_above_noise_mean)(void *user, int32_t stream, float db);                  /* (F)V   */
+    void (*max_bin)(void *user, int32_t stream, float snr_db, float snr_sigma);           /* (FF)V  */
+    void (*best1khz)(void *user, int32_t stream, float snr_db, float snr_sigma);          /* (FF)V  */
+    void (*noise_level)(void *user, int32_t stream, float per_bin_mean);                  /* (F)V   */
+} sdrg_callbacks;
+
+/* Per-kernel device times of the last process call, from hipEvents recorded on the stream each
+ * kernel was launched on (only filled while profiling is enabled). */
+typedef struct sdrg_timings {
+    float spectrum_ms;   /* unpack + FFT + |X|^2 + fftshift kernel */
+    float stats_ms;      /* signal-strength kernel */
+    float ssb_ms;        /* whole SSB chain (all its kernels) */
+    float total_ms;      /* first launch start -> last kernel end, across both streams */
+} sdrg_timings;
+
+typedef struct sdrg_engine sdrg_engine;
+
+/* Library identity. */
+int32_t sdrg_abi_version(void);
+const char *sdrg_last_error(void);      /* thread-local message for the last failing call */
+
+/* Geometry helpers (host-only, no device needed). */
+/* Frame size the SSB chain emits for a frame of n samples at sample_rate (0 if none):
+ * (n - taps)/decim + 1 with taps = 255 (or n|1 when n < 255), decim = max(1, int(fs/48000.0f))
+ * (ssb_demod_opt.cpp:121-143, :273). */
+int32_t sdrg_ssb_pcm_len(int32_t n, int64_t sample_rate);
+
+/* Create an engine for n_streams independent receivers on HIP device `device`.
+ * Replaces FFTProcessor() + configure() (fft_process.cpp:8-39) and BridgeConfig::initialize
+ * (bridge-config.h:17-38) for each stream. */
+int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t device, sdrg_engine **out);
+int32_t sdrg_engine_destroy(sdrg_engine *eng);
+
+/* JNI applyConfig (sdr-bridge-java-soapy.cpp:1073-1141): BridgeConfig::initialize + FFTProcessor::configure.
+ * Per-stream tracking/detection/SSB state is kept, exactly as the reference keeps its members and
+ * statics across applyConfig. */
+int32_t sdrg_engine_apply_config(sdrg_engine *eng, const sdrg_config *cfg);
+/* JNI setFrequency (:878-913): reconfigure + raise isCenterFrequencyChanged for every stream. */
+int32_t sdrg_engine_set_frequency(sdrg_engine *eng, int64_t center_frequency);
+/* JNI setFrequencyFocusRange (:1025-1040). */
+int32_t sdrg_engine_set_frequency_focus_range(sdrg_engine *eng, int32_t khz);
+/* JNI setSoundMode (:1066-1071). */
+int32_t sdrg_engine_set_sound_mode(sdrg_engine *eng, int32_t mode);
+/* Current configuration (BridgeConfig getters, bridge-config.h:41-51). */
+int32_t sdrg_engine_get_config(const sdrg_engine *eng, sdrg_config *out);
+int32_t sdrg_engine_n_streams(const sdrg_engine *eng);
+/* Samples per frame the SSB chain of every stream emits (constant for a configuration). */
+int32_t sdrg_engine_pcm_len(const sdrg_engine *eng);
+
+/* Reset every stream's cross-frame state (tracking latch, detection ring, SSB filter state) to the
+ * state of a freshly constructed reference process. */
+int32_t sdrg_engine_reset_state(sdrg_engine *eng);
+
+/* Process one frame of every stream, all buffers in device memory (HBM).
+ *   iq       : [n_streams][samples_per_reading] samples in `format`
+ *   spectra  : [n_streams][samples_per_reading] float, fftshifted linear power (fftCallback payload);
+ *              may be NULL when STATS is not requested (then an internal buffer is used)
+ *   records  : [n_streams] sdrg_frame_record (may be NULL if STATS not requested)
+ *   pcm      : [n_streams][pcm_len] int16 (may be NULL if SSB not requested)
+ *   now_ms   : monotonic clock in ms for the 300 ms frequency-tracking latch
+ *              (fft_process.cpp:333-361 uses steady_clock; injected here so results are reproducible)
+ * Work is enqueued on the engine's HIP streams and is complete when sdrg_engine_synchronize returns. */
+int32_t sdrg_engine_process_device(sdrg_engine *eng, const void *iq, int32_t format, int32_t stages,
+                                   float *spectra, sdrg_frame_record *records, int16_t *pcm,
+                                   int64_t now_ms);
+int32_t sdrg_engine_synchronize(sdrg_engine *eng);
+
+/* Same from host memory (PCIe-inclusive): copies iq in, runs, copies outputs back, synchronises,
+ * then invokes the registered callbacks per stream in soapyCallback order.  Any output may be NULL. */
+int32_t sdrg_engine_process_host(sdrg_engine *eng, const void *iq, int32_t format, int32_t stages,
+                                 float *spectra, sdrg_frame_record *records, int16_t *pcm,
+                                 int64_t now_ms);
+
+/* JNI read(): register the callback table (copied). NULL clears it. */
+int32_t sdrg_engine_set_callbacks(sdrg_engine *eng, const sdrg_callbacks *cbs);
+
+/* Profiling: when enabled, every process call records hipEvents around each kernel group. */
+int32_t sdrg_engine_set_profiling(sdrg_engine *eng, int32_t enabled);
+int32_t sdrg_engine_get_timings(const sdrg_engine *eng, sdrg_timings *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SDRG_H */
