@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""bench.py — IQ Msamples/s of the reference hot path on MI355X (BASELINE.json metric).
+
+A "step" is one pass of the hot path over one batch: every one of B = 4096 independent streams hands one
+16384-sample CS8 frame (2 Msps) to the engine, which runs IQ unpack -> 16384-pt FFT -> |X|^2 -> fftshift ->
+signal-strength statistics (FFTProcessor::process, src/dsp/fft_process.cpp:42-379) and the SSB chain ->
+int16 PCM (processSSB_opt, src/ssb/ssb_demod_opt.cpp:221-296; the reference's 255-tap FIR, decim 41).
+Inputs are synthetic CW tones + noise, resident in HBM before the timed region; every step does the full
+work (the per-stream filter state advances from step to step like a live receiver).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one process per GPU)
+
+With N > 1 every rank runs its own 4096 streams (weak scaling) and the per-frame records of each step are
+gathered to rank 0 over RCCL; value = all ranks' samples / max-over-ranks time.
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sdr-for-android-lib_amd"))
+
+import numpy as np  # noqa: E402
+
+N = 16384
+FS = 2_000_000
+CF = 100_000_000
+B = 4096
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+ALG_BYTES_PER_SAMPLE = {"spectrum": 6.0}  # CS8: 2 B in + 4 B fftshifted float32 power out
+
+
+def log(msg: str) -> None:
+    print(msg, file=sys.stderr, flush=True)
+
+
+def synth_device_frames(torch, dev, n_streams: int, seed: int):
+    """CS8 CW tone per stream (inside the 5 kHz focus) + Gaussian noise, generated on the GPU."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    tones = (torch.rand(n_streams, 1, device=dev, generator=g, dtype=torch.float64) * 9000.0 - 4500.0)
+    t = torch.arange(N, device=dev, dtype=torch.float64)[None, :]
+    ph = 2 * np.pi * tones * t / FS
+    i = torch.round(60 * torch.cos(ph) + 4 * torch.randn(n_streams, N, device=dev, generator=g, dtype=torch.float64))
+    q = torch.round(60 * torch.sin(ph) + 4 * torch.randn(n_streams, N, device=dev, generator=g, dtype=torch.float64))
+    iq = torch.stack([i, q], dim=2).clamp_(-128, 127).to(torch.int8).reshape(n_streams, 2 * N).contiguous()
+    return iq
+
+
+def cpu_baseline(threads: int, target_cpu_s: float = 15.0) -> dict:
+    """The oracle (our C restatement of the reference path: FFT + stats + SSB per frame), one fresh stream per
+    frame, timed on the host cores with `threads` worker threads (ctypes releases the GIL)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.lib()
+    frames = 64
+    raw = O.synth_frames(frames, N, O.CS8, tone_hz=1500.0, fs=FS)
+    # calibrate single-thread cost per frame
+    t0 = time.perf_counter()
+    O.run_streams(raw, O.CS8, N, 0, 8, FS, CF, 5)
+    per_frame = (time.perf_counter() - t0) / 8
+    per_thread = max(8, int(target_cpu_s / threads / per_frame))
+
+    def work():
+        done = 0
+        while done < per_thread:
+            k = min(frames, per_thread - done)
+            O.run_streams(raw, O.CS8, N, 0, k, FS, CF, 5)
+            done += k
+
+    ts = [threading.Thread(target=work) for _ in range(threads)]
+    t0 = time.perf_counter()
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join()
+    wall = time.perf_counter() - t0
+    total = per_thread * threads
+    return {"value": round(total * N / wall / 1e6, 3), "unit": "IQ Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{total} frames x {N} CS8 samples (FFT+stats+SSB per frame, fresh stream each), "
+                      f"{threads} threads, {wall:.2f} s wall, {per_frame * 1e3:.3f} ms/frame single-thread"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--streams", type=int, default=B)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import sdrg
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    streams = args.streams
+    cfg = sdrg.SDRConfig(centerFrequency=CF, samplesPerReading=N, sampleRate=FS, freqFocusRangeKhz=5, soundMode=1)
+    eng = sdrg.Engine(cfg, streams, device=local)
+    iq = synth_device_frames(torch, dev, streams, seed=0x5D12 + rank)
+    spec = torch.empty((streams, N), dtype=torch.float32, device=dev)
+    rec = torch.zeros((streams, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    plen = eng.pcm_len
+    pcm = torch.empty((streams, plen), dtype=torch.int16, device=dev)
+    gathered = [torch.empty_like(rec) for _ in range(world)] if (world > 1 and rank == 0) else None
+    torch.cuda.synchronize()
+
+    now = [1000]
+
+    def step():
+        eng.process_device(iq.data_ptr(), sdrg.CS8, sdrg.STAGE_ALL, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(),
+                           now[0])
+        now[0] += 8  # 16384 samples @ 2 Msps = 8.192 ms per frame
+        if world > 1:
+            eng.synchronize()
+            dist.gather(rec, gathered, dst=0)
+
+    eng.set_profiling(True)
+    for _ in range(args.warmup):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    eng.reset_timing_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ts = eng.timing_stats()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples = args.steps * streams * N * world
+    value = samples / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+    spec_ms = ts["spectrum_ms"]
+    alg_bytes = ALG_BYTES_PER_SAMPLE["spectrum"] * streams * N
+    achieved = alg_bytes / (spec_ms * 1e-3) / 1e9 if spec_ms > 0 else 0.0
+    out = {
+        "metric": "IQ Msamples/s (16384-pt FFT+SSB) at 1/2/4/8 GPUs; % HBM roofline",
+        "value": round(value, 2),
+        "unit": "IQ Msamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 (int8 CS8 in, int16 PCM out)",
+        "data": "synthetic CS8 CW tones + Gaussian noise, generated on device",
+        "config": {"workload": f"C3: {streams} streams x {N}-pt CS8 frames @2 Msps per GPU; FFT + |X|^2 + fftshift "
+                               "+ signal-strength stats + SSB (DC, LPF, AGC, 255-tap FIR decim 41, EQ, PCM)",
+                   "streams_per_gpu": streams, "samples_per_frame": N, "sample_rate": FS, "format": "CS8",
+                   "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (", RCCL gather of records"
+                                                                                         if world > 1 else "")},
+        "kernel_ms": {k: round(v, 4) for k, v in ts.items() if k != "count"},
+        "roofline": {"kernel": "spectrum (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "alg_bytes_per_launch": alg_bytes},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
+        except Exception as exc:  # the baseline is informative; never fail the bench line on it
+            out["cpu_baseline"] = {"error": repr(exc)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -143,6 +143,13 @@ const char *sdrg_last_error(void);      /* thread-local message for the last fai
  * (ssb_demod_opt.cpp:121-143, :273). */
 int32_t sdrg_ssb_pcm_len(int32_t n, int64_t sample_rate);
 
+/* The SSB filter design the engine uses for a configuration, from the reference's own expressions:
+ * rfFilter low-pass (iir2InitLowpass at (float)fs with the sound mode's fc/Q, ssb_demod_opt.cpp:60-73, :262),
+ * HP/BP biquads (:148-175, :278-279) and the FIR taps (:121-134).  lpf/hp/bp: {a0, a1, a2, b1, b2};
+ * taps must hold 255 floats; *n_taps receives the tap count.  Host-only. */
+int32_t sdrg_ssb_design(int32_t samp_count, int64_t sample_rate, int32_t sound_mode, float *lpf, float *hp,
+                        float *bp, float *taps, int32_t *n_taps);
+
 /* Create an engine for n_streams independent receivers on HIP device `device`.
  * Replaces FFTProcessor() + configure() (fft_process.cpp:8-39) and BridgeConfig::initialize
  * (bridge-config.h:17-38) for each stream. */
@@ -192,9 +199,14 @@ int32_t sdrg_engine_process_host(sdrg_engine *eng, const void *iq, int32_t forma
 /* JNI read(): register the callback table (copied). NULL clears it. */
 int32_t sdrg_engine_set_callbacks(sdrg_engine *eng, const sdrg_callbacks *cbs);
 
-/* Profiling: when enabled, every process call records hipEvents around each kernel group. */
+/* Profiling: when enabled, every process call records hipEvents around each kernel group (a ring of
+ * event sets, so back-to-back calls are timed without host synchronisation). */
 int32_t sdrg_engine_set_profiling(sdrg_engine *eng, int32_t enabled);
+/* Timings of the most recent profiled call (waits for it to finish). */
 int32_t sdrg_engine_get_timings(const sdrg_engine *eng, sdrg_timings *out);
+/* Mean timings over every profiled call since the last reset (waits for them); *count = calls averaged. */
+int32_t sdrg_engine_get_timing_stats(const sdrg_engine *eng, sdrg_timings *mean, int32_t *count);
+int32_t sdrg_engine_reset_timing_stats(sdrg_engine *eng);
 
 #ifdef __cplusplus
 }

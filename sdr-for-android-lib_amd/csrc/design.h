@@ -1,0 +1,19 @@
+// design.h — host-side filter design and window geometry (see design.cpp).
+#pragma once
+
+#include <stdint.h>
+
+#include "sdrg_types.h"
+
+namespace sdrg {
+
+void design_lowpass(float fs, float fc, float Q, float c[5]);
+void design_highpass(float fs, float f0, float Q, float c[5]);
+void design_bandpass(float fs, float f0, float Q, float c[5]);
+int design_fir(int64_t in_size, int decim, float cutoff_rel, float *h);
+int ssb_decim(uint32_t sample_rate);
+int ssb_taps_for(int64_t samp_count);
+int ssb_pcm_len(int64_t samp_count, uint32_t sample_rate);
+StatsGeometry stats_geometry(uint32_t sample_rate, uint32_t center_frequency, int n, int focus_khz);
+
+}  // namespace sdrg

@@ -1,0 +1,666 @@
+// engine.cpp — the C ABI (include/sdrg.h): configuration, per-stream state in HBM, kernel orchestration.
+//
+// Host-side equivalent of the reference's bridge + FFTProcessor + processSSB_opt control logic:
+//   BridgeConfig::initialize / setters     src/bridge-config.h:17-65
+//   FFTProcessor::configure                src/dsp/fft_process.cpp:20-39
+//   processSSB_opt's static initialisation src/ssb/ssb_demod_opt.cpp:223-282 (mode globals, rfInit, eqInit)
+//   soapyCallback's per-frame dispatch     src/sdr-bridge-java-soapy.cpp:424-493
+// Everything that runs per sample runs in the HIP kernels (spectrum.hip, stats.hip, ssb.hip).
+//
+// Work is enqueued on a main HIP stream (spectrum -> stats) and a forked SSB stream that joins back,
+// so the two independent halves of the hot path overlap on the GPU and a caller sees one stream.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "design.h"
+#include "sdrg_internal.h"
+
+using namespace sdrg;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int32_t fail(int32_t code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) return fail(SDRG_E_HIP, "%s: %s", #expr, hipGetErrorString(e_));    \
+    } while (0)
+
+bool is_pow2(int64_t n) { return n > 0 && (n & (n - 1)) == 0; }
+
+// processSSB_opt's statics that every stream of an engine shares (they only depend on the call sequence)
+struct SsbControl {
+    int64_t samp_count = 0;  // static size_t sampCount, frozen at the first call (:224)
+    float agc_target = 0.35f, agc_fast = 0.006f, agc_slow = 0.00035f, gain = 0.5f;  // :17-28
+    float lowpass_bd = 3200.0f, lowpass_q = 0.9f, transient_coeff = 0.55f;
+    bool rf_init = false;
+    float lpf[5] = {0, 0, 0, 0, 0};
+    bool eq_init = false;
+    float hp[5] = {0, 0, 0, 0, 0}, bp[5] = {0, 0, 0, 0, 0};
+    // FIR taps currently uploaded (depend on samp_count and decim)
+    int64_t taps_samp = -1;
+    int taps_decim = -1, n_taps = 0;
+};
+
+struct EvSet {
+    hipEvent_t t0 = nullptr, spec = nullptr, stats = nullptr, ssb0 = nullptr, ssb1 = nullptr, end = nullptr;
+    bool has_spec = false, has_stats = false, has_ssb = false, pending = false;
+};
+
+}  // namespace
+
+struct sdrg_engine {
+    sdrg_config cfg{};
+    int n_streams = 0;
+    int device = 0;
+    hipStream_t s_main = nullptr, s_ssb = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // profiling: a ring of event sets so consecutive calls are timed without host synchronisation
+    static constexpr int RING = 64;
+    EvSet ring[RING];
+    bool ring_created = false;
+    int ring_next = 0, ring_last = -1;
+    bool profiling = false;
+    sdrg_timings last_timings{};
+    double sum_spec = 0, sum_stats = 0, sum_ssb = 0, sum_total = 0;
+    int n_acc = 0;
+
+    // device state / buffers
+    StatsState *d_stats = nullptr;
+    SsbStreamState *d_ssb = nullptr;
+    float *d_twiddles = nullptr;
+    int tw_n = 0;
+    float *d_taps = nullptr;
+    float *d_ssb_scratch = nullptr;
+    size_t ssb_scratch_elems = 0;
+    float *d_spec_scratch = nullptr;
+    size_t spec_scratch_elems = 0;
+    sdrg_frame_record *d_rec_scratch = nullptr;
+    // host-path staging
+    void *d_iq_stage = nullptr;
+    size_t iq_stage_bytes = 0;
+    float *d_spec_stage = nullptr;
+    size_t spec_stage_elems = 0;
+    sdrg_frame_record *d_rec_stage = nullptr;
+    int16_t *d_pcm_stage = nullptr;
+    size_t pcm_stage_elems = 0;
+    std::vector<float> h_spec;
+    std::vector<sdrg_frame_record> h_rec;
+    std::vector<int16_t> h_pcm;
+
+    SsbControl ssb;
+    bool cf_changed_pending = false;
+    bool has_cbs = false;
+    sdrg_callbacks cbs{};
+};
+
+namespace {
+
+int32_t validate_config(const sdrg_config *cfg) {
+    if (!cfg) return fail(SDRG_E_INVALID, "null config");
+    if (cfg->samples_per_reading < 64 || cfg->samples_per_reading > 65536 || !is_pow2(cfg->samples_per_reading))
+        return fail(SDRG_E_UNSUPPORTED, "samples_per_reading %d: need a power of two in [64, 65536]",
+                    cfg->samples_per_reading);
+    if ((uint32_t)cfg->sample_rate == 0) return fail(SDRG_E_INVALID, "sample_rate must be > 0");
+    if (cfg->freq_focus_range_khz < 0) return fail(SDRG_E_INVALID, "freq_focus_range_khz must be >= 0");
+    return SDRG_OK;
+}
+
+template <typename T>
+int32_t ensure_device(T **p, size_t *have, size_t need) {
+    if (*have >= need && *p) return SDRG_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    if (need == 0) return SDRG_OK;
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(p), need * sizeof(T)));
+    *have = need;
+    return SDRG_OK;
+}
+
+int32_t upload_twiddles(sdrg_engine *e, int n) {
+    if (e->tw_n == n && e->d_twiddles) return SDRG_OK;
+    std::vector<float> tw(2 * (size_t)n);
+    for (int m = 0; m < n; m++) {
+        const double a = -2.0 * M_PI * (double)m / (double)n;
+        tw[2 * m] = (float)cos(a);
+        tw[2 * m + 1] = (float)sin(a);
+    }
+    if (e->d_twiddles) (void)hipFree(e->d_twiddles);
+    e->d_twiddles = nullptr;
+    e->tw_n = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_twiddles), tw.size() * sizeof(float)));
+    HIP_TRY(hipMemcpy(e->d_twiddles, tw.data(), tw.size() * sizeof(float), hipMemcpyHostToDevice));
+    e->tw_n = n;
+    return SDRG_OK;
+}
+
+int64_t ssb_frozen_or(const sdrg_engine *e) {
+    return e->ssb.samp_count ? e->ssb.samp_count : e->cfg.samples_per_reading;
+}
+
+// Resolve one ring slot's events into timings and add them to the running sums.
+int32_t fold_slot(sdrg_engine *e, int slot) {
+    EvSet &ev = e->ring[slot];
+    if (!ev.pending) return SDRG_OK;
+    HIP_TRY(hipEventSynchronize(ev.end));
+    sdrg_timings t{};
+    float ms = 0.0f;
+    if (ev.has_spec) {
+        HIP_TRY(hipEventElapsedTime(&ms, ev.t0, ev.spec));
+        t.spectrum_ms = ms;
+    }
+    if (ev.has_stats) {
+        HIP_TRY(hipEventElapsedTime(&ms, ev.has_spec ? ev.spec : ev.t0, ev.stats));
+        t.stats_ms = ms;
+    }
+    if (ev.has_ssb) {
+        HIP_TRY(hipEventElapsedTime(&ms, ev.ssb0, ev.ssb1));
+        t.ssb_ms = ms;
+    }
+    HIP_TRY(hipEventElapsedTime(&ms, ev.t0, ev.end));
+    t.total_ms = ms;
+    ev.pending = false;
+    if (slot == e->ring_last) e->last_timings = t;
+    e->sum_spec += t.spectrum_ms;
+    e->sum_stats += t.stats_ms;
+    e->sum_ssb += t.ssb_ms;
+    e->sum_total += t.total_ms;
+    e->n_acc++;
+    return SDRG_OK;
+}
+
+int32_t fold_all(sdrg_engine *e) {
+    // oldest first
+    for (int k = 0; k < sdrg_engine::RING; k++) {
+        int32_t rc = fold_slot(e, (e->ring_next + k) % sdrg_engine::RING);
+        if (rc) return rc;
+    }
+    return SDRG_OK;
+}
+
+// processSSB_opt's per-call control logic (:223-282) -> kernel parameters
+int32_t prepare_ssb(sdrg_engine *e, SsbParams *p) {
+    SsbControl &c = e->ssb;
+    const uint32_t fs = (uint32_t)e->cfg.sample_rate;
+    if (c.samp_count == 0) c.samp_count = e->cfg.samples_per_reading;  // static size_t sampCount = iq.size()
+    const int mode = e->cfg.sound_mode;
+    if (mode == 2) {
+        c.agc_target = 0.45f; c.agc_fast = 0.008f; c.gain = 4.5f;
+        c.lowpass_bd = 2200.0f; c.lowpass_q = 1.2f; c.transient_coeff = 0.7f;
+    } else if (mode == 0) {
+        c.agc_target = 0.45f; c.agc_fast = 0.008f; c.gain = 10.0f;
+        c.lowpass_bd = 2200.0f; c.lowpass_q = 1.2f; c.transient_coeff = 0.7f;
+    } else if (mode == 1) {
+        c.agc_target = 0.35f; c.agc_fast = 0.006f; c.agc_slow = 0.00035f; c.gain = 0.5f;
+        c.lowpass_bd = 3200.0f; c.lowpass_q = 0.9f; c.transient_coeff = 0.55f;
+    }
+    if (!c.rf_init) {
+        design_lowpass((float)fs, c.lowpass_bd, c.lowpass_q, c.lpf);
+        c.rf_init = true;
+    }
+    const int decim = ssb_decim(fs);
+    if (c.taps_samp != c.samp_count || c.taps_decim != decim || !e->d_taps) {
+        float h[256];
+        c.n_taps = design_fir(c.samp_count, decim, 0.45f, h);
+        if (!e->d_taps) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_taps), 256 * sizeof(float)));
+        HIP_TRY(hipMemcpy(e->d_taps, h, sizeof(float) * (size_t)c.n_taps, hipMemcpyHostToDevice));
+        c.taps_samp = c.samp_count;
+        c.taps_decim = decim;
+    }
+    if (!c.eq_init) {
+        design_highpass(48000.0f, 1200.0f, 0.7f, c.hp);
+        design_bandpass(48000.0f, 2400.0f, 0.6f, c.bp);
+        c.eq_init = true;
+    }
+    memset(p, 0, sizeof(*p));
+    p->samp_count = (int32_t)c.samp_count;
+    p->n_in = e->cfg.samples_per_reading;
+    p->upper = 1;  // SSBProcessor always asks for the upper sideband (ssb_processor.cpp:103)
+    p->decim = decim;
+    p->n_taps = c.n_taps;
+    p->pcm_len = ssb_pcm_len(c.samp_count, fs);
+    p->agc_target = c.agc_target;
+    p->agc_fast = c.agc_fast;
+    p->agc_slow = c.agc_slow;
+    p->gain = c.gain;
+    p->transient_coeff = c.transient_coeff;
+    memcpy(p->lpf, c.lpf, sizeof(p->lpf));
+    memcpy(p->hp, c.hp, sizeof(p->hp));
+    memcpy(p->bp, c.bp, sizeof(p->bp));
+    return SDRG_OK;
+}
+
+int32_t alloc_state(sdrg_engine *e) {
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_stats), sizeof(StatsState) * (size_t)e->n_streams));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_ssb), sizeof(SsbStreamState) * (size_t)e->n_streams));
+    HIP_TRY(hipMemset(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
+    HIP_TRY(hipMemset(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
+    return SDRG_OK;
+}
+
+// FFTProcessor::configure (fft_process.cpp:33-35): maxPeakAndFrequency = {-130, cf} on first configure.
+// The device state starts zeroed; max_peak_set = 0 makes the kernel seed it at the first frame with the
+// centre frequency of that frame's configuration, which is what configure() stored.
+int32_t bytes_per_sample(int fmt) {
+    switch (fmt) {
+    case SDRG_IQ_CF32: return 8;
+    case SDRG_IQ_CS16: return 4;
+    case SDRG_IQ_CS8:
+    case SDRG_IQ_CU8: return 2;
+    default: return 0;
+    }
+}
+
+int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, float *spectra,
+                sdrg_frame_record *records, int16_t *pcm, int64_t now_ms) {
+    const int n = e->cfg.samples_per_reading;
+    const int B = e->n_streams;
+    if (!iq) return fail(SDRG_E_INVALID, "null iq");
+    if (bytes_per_sample(fmt) == 0) return fail(SDRG_E_INVALID, "unknown iq format %d", fmt);
+    if (stages & ~SDRG_STAGE_ALL) return fail(SDRG_E_INVALID, "unknown stage bits 0x%x", stages);
+    if ((stages & SDRG_STAGE_STATS) && !(stages & SDRG_STAGE_SPECTRUM))
+        return fail(SDRG_E_INVALID, "STATS needs SPECTRUM");
+    const bool do_spec = stages & SDRG_STAGE_SPECTRUM, do_stats = stages & SDRG_STAGE_STATS,
+               do_ssb = stages & SDRG_STAGE_SSB;
+    if (do_spec && !spectrum_supported(n))
+        return fail(SDRG_E_UNSUPPORTED, "spectrum for N=%d not supported by this build", n);
+
+    float *spec = spectra;
+    if (do_spec && !spec) {
+        int32_t rc = ensure_device(&e->d_spec_scratch, &e->spec_scratch_elems, (size_t)B * n);
+        if (rc) return rc;
+        spec = e->d_spec_scratch;
+    }
+    sdrg_frame_record *recs = records;
+    if (do_stats && !recs) {
+        size_t have = e->d_rec_scratch ? (size_t)B : 0;
+        int32_t rc = ensure_device(&e->d_rec_scratch, &have, (size_t)B);
+        if (rc) return rc;
+        recs = e->d_rec_scratch;
+    }
+    SsbParams sp;
+    if (do_ssb) {
+        int32_t rc = prepare_ssb(e, &sp);
+        if (rc) return rc;
+        if (!pcm && sp.pcm_len > 0) return fail(SDRG_E_INVALID, "null pcm with SSB stage");
+        rc = ensure_device(&e->d_ssb_scratch, &e->ssb_scratch_elems,
+                           (size_t)B * ((size_t)sp.samp_count + (size_t)sp.pcm_len));
+        if (rc) return rc;
+    }
+    if (do_spec) {
+        int32_t rc = upload_twiddles(e, n);
+        if (rc) return rc;
+    }
+
+    StatsGeometry geo{};
+    if (do_stats) {
+        geo = stats_geometry((uint32_t)e->cfg.sample_rate, (uint32_t)e->cfg.center_frequency, n,
+                             e->cfg.freq_focus_range_khz);
+        geo.cf_changed = e->cf_changed_pending ? 1 : 0;
+        if (geo.max_pool > 16384) return fail(SDRG_E_UNSUPPORTED, "pooled noise bins %d > 16384", geo.max_pool);
+    }
+
+    const bool prof = e->profiling;
+    EvSet *ev = nullptr;
+    if (prof) {
+        const int slot = e->ring_next;
+        if (e->ring[slot].pending) {
+            int32_t rc = fold_slot(e, slot);
+            if (rc) return rc;
+        }
+        ev = &e->ring[slot];
+        ev->has_spec = do_spec;
+        ev->has_stats = do_stats;
+        ev->has_ssb = do_ssb;
+        HIP_TRY(hipEventRecord(ev->t0, e->s_main));
+    }
+    if (do_ssb) {  // fork
+        HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
+        HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
+        if (prof) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
+        HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_ssb, e->d_ssb_scratch, pcm, e->s_ssb));
+        if (prof) HIP_TRY(hipEventRecord(ev->ssb1, e->s_ssb));
+        HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
+    }
+    if (do_spec) {
+        HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->s_main));
+        if (prof) HIP_TRY(hipEventRecord(ev->spec, e->s_main));
+    }
+    if (do_stats) {
+        HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->s_main));
+        if (prof) HIP_TRY(hipEventRecord(ev->stats, e->s_main));
+        e->cf_changed_pending = false;
+    }
+    if (do_ssb) HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));  // join
+    if (prof) {
+        HIP_TRY(hipEventRecord(ev->end, e->s_main));
+        ev->pending = true;
+        e->ring_last = e->ring_next;
+        e->ring_next = (e->ring_next + 1) % sdrg_engine::RING;
+    }
+    return SDRG_OK;
+}
+
+void dispatch_callbacks(sdrg_engine *e, int32_t stages, int pcm_len) {
+    // soapyCallback order (sdr-bridge-java-soapy.cpp:458-475), then the SSB worker's pcm callback
+    const sdrg_callbacks &c = e->cbs;
+    const int n = e->cfg.samples_per_reading;
+    for (int s = 0; s < e->n_streams; s++) {
+        if (stages & SDRG_STAGE_STATS) {
+            const sdrg_frame_record &r = e->h_rec[s];
+            if (c.fft) c.fft(c.user, s, e->h_spec.data() + (size_t)s * n, n);
+            if (c.detection_flag) c.detection_flag(c.user, s, r.detection_flag);
+            if (c.mean_snr) c.mean_snr(c.user, s, r.mean_snr_db);
+            if (c.mean_snr_sigma) c.mean_snr_sigma(c.user, s, r.mean_snr_sigma);
+            if (c.peak_frequency) c.peak_frequency(c.user, s, r.tracking_frequency);
+            if (c.peak_above_noise_mean) c.peak_above_noise_mean(c.user, s, r.peak_above_noise_mean_db);
+            if (c.max_bin) c.max_bin(c.user, s, r.max_bin_snr_db, r.max_bin_snr_sigma);
+            if (c.best1khz) c.best1khz(c.user, s, r.best1khz_snr_db, r.best1khz_snr_sigma);
+            if (c.noise_level) c.noise_level(c.user, s, r.per_bin_mean);
+        }
+        if ((stages & SDRG_STAGE_SSB) && c.pcm && pcm_len > 0)
+            c.pcm(c.user, s, e->h_pcm.data() + (size_t)s * pcm_len, pcm_len);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t sdrg_abi_version(void) { return SDRG_ABI_VERSION; }
+
+const char *sdrg_last_error(void) { return g_last_error.c_str(); }
+
+int32_t sdrg_ssb_pcm_len(int32_t n, int64_t sample_rate) {
+    if (n <= 0) return 0;
+    return ssb_pcm_len(n, (uint32_t)sample_rate);
+}
+
+int32_t sdrg_ssb_design(int32_t samp_count, int64_t sample_rate, int32_t sound_mode, float *lpf, float *hp,
+                        float *bp, float *taps, int32_t *n_taps) {
+    if (samp_count <= 0 || (uint32_t)sample_rate == 0) return fail(SDRG_E_INVALID, "bad samp_count/sample_rate");
+    SsbControl c;
+    if (sound_mode == 2 || sound_mode == 0) {
+        c.lowpass_bd = 2200.0f;
+        c.lowpass_q = 1.2f;
+    }
+    const uint32_t fs = (uint32_t)sample_rate;
+    if (lpf) design_lowpass((float)fs, c.lowpass_bd, c.lowpass_q, lpf);
+    if (hp) design_highpass(48000.0f, 1200.0f, 0.7f, hp);
+    if (bp) design_bandpass(48000.0f, 2400.0f, 0.6f, bp);
+    if (taps) {
+        const int nt = design_fir(samp_count, ssb_decim(fs), 0.45f, taps);
+        if (n_taps) *n_taps = nt;
+    }
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t device, sdrg_engine **out) {
+    if (!out) return fail(SDRG_E_INVALID, "null out");
+    *out = nullptr;
+    int32_t rc = validate_config(cfg);
+    if (rc) return rc;
+    if (n_streams <= 0) return fail(SDRG_E_INVALID, "n_streams must be > 0");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(SDRG_E_NODEVICE, "no HIP device");
+    if (device < 0 || device >= count) return fail(SDRG_E_INVALID, "device %d out of range [0, %d)", device, count);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SDRG_E_NODEVICE, "device %d is %s, this build targets gfx950", device, prop.gcnArchName);
+    HIP_TRY(hipSetDevice(device));
+    sdrg_engine *e = new sdrg_engine();
+    e->cfg = *cfg;
+    e->n_streams = n_streams;
+    e->device = device;
+    auto cleanup = [&](int32_t code) {
+        sdrg_engine_destroy(e);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&e->s_main, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->s_ssb, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
+    hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join};
+    for (auto p : evs)
+        if (hipEventCreateWithFlags(p, hipEventDisableTiming) != hipSuccess)
+            return cleanup(fail(SDRG_E_HIP, "hipEventCreate failed"));
+    rc = alloc_state(e);
+    if (rc) return cleanup(rc);
+    *out = e;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_destroy(sdrg_engine *e) {
+    if (!e) return SDRG_OK;
+    (void)hipSetDevice(e->device);
+    if (e->s_main) (void)hipStreamSynchronize(e->s_main);
+    if (e->s_ssb) (void)hipStreamSynchronize(e->s_ssb);
+    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_ssb_scratch, e->d_spec_scratch,
+                    e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    hipEvent_t evs[] = {e->ev_fork, e->ev_join};
+    for (hipEvent_t ev : evs)
+        if (ev) (void)hipEventDestroy(ev);
+    for (auto &r : e->ring) {
+        hipEvent_t rev[] = {r.t0, r.spec, r.stats, r.ssb0, r.ssb1, r.end};
+        for (hipEvent_t ev : rev)
+            if (ev) (void)hipEventDestroy(ev);
+    }
+    if (e->s_main) (void)hipStreamDestroy(e->s_main);
+    if (e->s_ssb) (void)hipStreamDestroy(e->s_ssb);
+    delete e;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_apply_config(sdrg_engine *e, const sdrg_config *cfg) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    int32_t rc = validate_config(cfg);
+    if (rc) return rc;
+    e->cfg = *cfg;  // applied at the next process call (frame boundary)
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_frequency(sdrg_engine *e, int64_t center_frequency) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    e->cfg.center_frequency = center_frequency;
+    e->cf_changed_pending = true;  // :907 isCenterFrequencyChanged = true
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_frequency_focus_range(sdrg_engine *e, int32_t khz) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if (khz < 0) return fail(SDRG_E_INVALID, "focus range must be >= 0");
+    e->cfg.freq_focus_range_khz = khz;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_sound_mode(sdrg_engine *e, int32_t mode) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    e->cfg.sound_mode = mode;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_get_config(const sdrg_engine *e, sdrg_config *out) {
+    if (!e || !out) return fail(SDRG_E_INVALID, "null argument");
+    *out = e->cfg;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_n_streams(const sdrg_engine *e) { return e ? e->n_streams : 0; }
+
+int32_t sdrg_engine_pcm_len(const sdrg_engine *e) {
+    if (!e) return 0;
+    return ssb_pcm_len(ssb_frozen_or(e), (uint32_t)e->cfg.sample_rate);
+}
+
+int32_t sdrg_engine_reset_state(sdrg_engine *e) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->s_main));
+    HIP_TRY(hipStreamSynchronize(e->s_ssb));
+    HIP_TRY(hipMemset(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
+    HIP_TRY(hipMemset(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
+    e->ssb = SsbControl{};
+    e->cf_changed_pending = false;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_process_device(sdrg_engine *e, const void *iq, int32_t format, int32_t stages, float *spectra,
+                                   sdrg_frame_record *records, int16_t *pcm, int64_t now_ms) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    return enqueue(e, iq, format, stages, spectra, records, pcm, now_ms);
+}
+
+int32_t sdrg_engine_synchronize(sdrg_engine *e) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    HIP_TRY(hipStreamSynchronize(e->s_main));
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_process_host(sdrg_engine *e, const void *iq, int32_t format, int32_t stages, float *spectra,
+                                 sdrg_frame_record *records, int16_t *pcm, int64_t now_ms) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if (!iq) return fail(SDRG_E_INVALID, "null iq");
+    const int bps = bytes_per_sample(format);
+    if (!bps) return fail(SDRG_E_INVALID, "unknown iq format %d", format);
+    HIP_TRY(hipSetDevice(e->device));
+    const int n = e->cfg.samples_per_reading;
+    const int B = e->n_streams;
+    const size_t iq_bytes = (size_t)B * n * bps;
+    if (e->iq_stage_bytes < iq_bytes) {
+        size_t have = e->iq_stage_bytes;
+        char *p = static_cast<char *>(e->d_iq_stage);
+        int32_t rc = ensure_device(&p, &have, iq_bytes);
+        if (rc) return rc;
+        e->d_iq_stage = p;
+        e->iq_stage_bytes = have;
+    }
+    const bool want_cb = e->has_cbs;
+    const bool do_spec = stages & SDRG_STAGE_SPECTRUM, do_stats = stages & SDRG_STAGE_STATS,
+               do_ssb = stages & SDRG_STAGE_SSB;
+    if (do_spec) {
+        int32_t rc = ensure_device(&e->d_spec_stage, &e->spec_stage_elems, (size_t)B * n);
+        if (rc) return rc;
+    }
+    if (do_stats && !e->d_rec_stage)
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_rec_stage), sizeof(sdrg_frame_record) * (size_t)B));
+    int pcm_len = 0;
+    if (do_ssb) {
+        // pcm length is known before the call: frozen (or about-to-be frozen) size and current fs
+        pcm_len = ssb_pcm_len(ssb_frozen_or(e), (uint32_t)e->cfg.sample_rate);
+        int32_t rc = ensure_device(&e->d_pcm_stage, &e->pcm_stage_elems, (size_t)B * (pcm_len > 0 ? pcm_len : 1));
+        if (rc) return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(e->d_iq_stage, iq, iq_bytes, hipMemcpyHostToDevice, e->s_main));
+    int32_t rc = enqueue(e, e->d_iq_stage, format, stages, do_spec ? e->d_spec_stage : nullptr,
+                         do_stats ? e->d_rec_stage : nullptr, do_ssb ? e->d_pcm_stage : nullptr, now_ms);
+    if (rc) return rc;
+    float *h_spec = spectra;
+    sdrg_frame_record *h_rec = records;
+    int16_t *h_pcm = pcm;
+    if (want_cb) {
+        if (do_spec && !h_spec) { e->h_spec.resize((size_t)B * n); h_spec = e->h_spec.data(); }
+        if (do_stats && !h_rec) { e->h_rec.resize(B); h_rec = e->h_rec.data(); }
+        if (do_ssb && !h_pcm) { e->h_pcm.resize((size_t)B * std::max(pcm_len, 1)); h_pcm = e->h_pcm.data(); }
+    }
+    if (do_spec && h_spec)
+        HIP_TRY(hipMemcpyAsync(h_spec, e->d_spec_stage, sizeof(float) * (size_t)B * n, hipMemcpyDeviceToHost, e->s_main));
+    if (do_stats && h_rec)
+        HIP_TRY(hipMemcpyAsync(h_rec, e->d_rec_stage, sizeof(sdrg_frame_record) * (size_t)B, hipMemcpyDeviceToHost,
+                               e->s_main));
+    if (do_ssb && h_pcm && pcm_len > 0)
+        HIP_TRY(hipMemcpyAsync(h_pcm, e->d_pcm_stage, sizeof(int16_t) * (size_t)B * pcm_len, hipMemcpyDeviceToHost,
+                               e->s_main));
+    HIP_TRY(hipStreamSynchronize(e->s_main));
+    if (want_cb) {
+        // callbacks read the engine-owned host copies; make sure they hold this call's data
+        if (do_spec && h_spec != e->h_spec.data()) e->h_spec.assign(h_spec, h_spec + (size_t)B * n);
+        if (do_stats && h_rec != e->h_rec.data()) e->h_rec.assign(h_rec, h_rec + B);
+        if (do_ssb && h_pcm != e->h_pcm.data() && pcm_len > 0) e->h_pcm.assign(h_pcm, h_pcm + (size_t)B * pcm_len);
+        dispatch_callbacks(e, stages, pcm_len);
+    }
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_callbacks(sdrg_engine *e, const sdrg_callbacks *cbs) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if (cbs) {
+        e->cbs = *cbs;
+        e->has_cbs = true;
+    } else {
+        e->cbs = sdrg_callbacks{};
+        e->has_cbs = false;
+    }
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_profiling(sdrg_engine *e, int32_t enabled) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    if (enabled && !e->ring_created) {
+        for (auto &r : e->ring) {
+            hipEvent_t *rev[] = {&r.t0, &r.spec, &r.stats, &r.ssb0, &r.ssb1, &r.end};
+            for (hipEvent_t *p : rev) HIP_TRY(hipEventCreate(p));
+        }
+        e->ring_created = true;
+    }
+    e->profiling = enabled != 0;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_get_timings(const sdrg_engine *ce, sdrg_timings *out) {
+    if (!ce || !out) return fail(SDRG_E_INVALID, "null argument");
+    sdrg_engine *e = const_cast<sdrg_engine *>(ce);
+    if (e->ring_last < 0) return fail(SDRG_E_INVALID, "no profiled call yet");
+    int32_t rc = fold_slot(e, e->ring_last);
+    if (rc) return rc;
+    *out = e->last_timings;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_get_timing_stats(const sdrg_engine *ce, sdrg_timings *mean, int32_t *count) {
+    if (!ce || !mean) return fail(SDRG_E_INVALID, "null argument");
+    sdrg_engine *e = const_cast<sdrg_engine *>(ce);
+    int32_t rc = fold_all(e);
+    if (rc) return rc;
+    const double k = e->n_acc > 0 ? 1.0 / e->n_acc : 0.0;
+    mean->spectrum_ms = (float)(e->sum_spec * k);
+    mean->stats_ms = (float)(e->sum_stats * k);
+    mean->ssb_ms = (float)(e->sum_ssb * k);
+    mean->total_ms = (float)(e->sum_total * k);
+    if (count) *count = e->n_acc;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_reset_timing_stats(sdrg_engine *e) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    int32_t rc = fold_all(e);
+    if (rc) return rc;
+    e->sum_spec = e->sum_stats = e->sum_ssb = e->sum_total = 0;
+    e->n_acc = 0;
+    return SDRG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,28 @@
+// sdrg_internal.h — kernel launchers shared by the engine (host C++) and the HIP translation units.
+// Not part of the public ABI (include/sdrg.h is).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sdrg_types.h"
+
+namespace sdrg {
+
+// ------------------------------------------------------------------------------------------------
+// Launchers (defined in the .hip translation units).  All are asynchronous on `stream`.
+// ------------------------------------------------------------------------------------------------
+// Is N supported by the LDS-resident spectrum kernel?
+bool spectrum_supported(int n);
+// Twiddle table exp(-2 pi i m / N), m in [0, N), float2, computed in double on the host.
+hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles,
+                           float *spectra, hipStream_t stream);
+
+hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry &geo, int64_t now_ms,
+                        StatsState *state, sdrg_frame_record *records, hipStream_t stream);
+
+// scratch: [n_frames][samp_count] float (AGC output) ; taps: [n_taps] device floats
+hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
+                      SsbStreamState *state, float *scratch, int16_t *pcm, hipStream_t stream);
+
+}  // namespace sdrg

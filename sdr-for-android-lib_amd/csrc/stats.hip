@@ -1,0 +1,351 @@
+// stats.hip — per-frame signal-strength statistics, frequency tracking and detection flag.
+//
+// Replaces FFTProcessor::evaluateSignalStrength (src/dsp/fft_process.cpp:122-379) for a batch of frames,
+// one wavefront per frame, reading the fftshifted power spectrum the spectrum kernel wrote and updating
+// the stream's FFTProcessor state (StatsState) in HBM.
+//
+// The reference's float expressions are kept in their order, with FP contraction off, so the statistics
+// follow it to libm rounding: the sequential running sums (best1kHzMean, the best-start scan) are
+// replayed sequentially by one lane per window because their drift is part of the reference result
+// (fft_process.cpp:163-180, :313-319); the focus peak is the FIRST maximum of the dB values (strict >,
+// seeded at -130 dB), found by a wave reduction that prefers the lower index on ties; the MAD medians
+// are exact k-th-element radix selects instead of std::sort.  Only the trip-wise order-free parts
+// (dB conversions, the pooled-gap selection) run across lanes.
+#include "sdrg_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace sdrg {
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int MAX_POOL = 16384;  // pooled-bin bound: N/4 at N = 65536 (the widest nBottom case, see engine.cpp)
+
+__device__ __forceinline__ float db_of(float p) { return 10.0f * log10f(p / 1.0f + 1e-20f); }  // refPower = 1
+
+struct WinScan {
+    float sum;       // sequential sum over [lo, hi]
+    float best1k;    // best1kHzMean(lo, hi)
+    int best_start;  // first start maximising the raw running sum (focus scan, :311-320)
+};
+
+// One lane replays the reference's sequential loops over P[lo..hi].
+__device__ WinScan scan_window(const float *__restrict__ P, int lo, int hi, int w) {
+    WinScan r;
+    float s = 0.0f;
+    for (int i = lo; i <= hi; i++) s += P[i];
+    r.sum = s;
+    const int len = hi - lo + 1;
+    r.best_start = lo;
+    if (len <= 0) {
+        r.best1k = 0.0f;
+    } else if (len < w) {
+        r.best1k = s / len;
+    } else {
+        float rs = 0.0f;
+        for (int i = lo; i < lo + w; i++) rs += P[i];
+        float best = rs / w, bv = rs;
+        for (int st = lo + 1; st + w - 1 <= hi; st++) {
+            rs += P[st + w - 1] - P[st - 1];
+            const float m = rs / w;
+            if (m > best) best = m;
+            if (rs > bv) {
+                bv = rs;
+                r.best_start = st;
+            }
+        }
+        r.best1k = best;
+    }
+    return r;
+}
+
+__device__ __forceinline__ float fmax_ref(float a, float b) { return (a < b) ? b : a; }  // std::max
+
+// k-th smallest (0-based) of non-negative floats in lds_vals[0..cnt) by 4 x 8-bit radix select.
+__device__ float kth_smallest(const float *vals, int cnt, int k, int *hist, int *shared_prefix) {
+    const int lane = threadIdx.x;
+    uint32_t prefix = 0, mask = 0;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = lane; i < 256; i += WAVE) hist[i] = 0;
+        __syncthreads();
+        for (int q = lane; q < cnt; q += WAVE) {
+            const uint32_t b = __float_as_uint(vals[q]);
+            if ((b & mask) == prefix) atomicAdd(&hist[(b >> shift) & 0xff], 1);
+        }
+        __syncthreads();
+        if (lane == 0) {
+            int acc = 0, d = 0;
+            for (; d < 255; d++) {
+                if (acc + hist[d] > k) break;
+                acc += hist[d];
+            }
+            k -= acc;
+            shared_prefix[0] = (int)(prefix | ((uint32_t)d << shift));
+            shared_prefix[1] = k;
+        }
+        __syncthreads();
+        prefix = (uint32_t)shared_prefix[0];
+        k = shared_prefix[1];
+        mask |= 0xffu << shift;
+        __syncthreads();
+    }
+    return __uint_as_float(prefix);
+}
+
+__global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ spectra, StatsGeometry g,
+                                                     int64_t now_ms, StatsState *__restrict__ state,
+                                                     sdrg_frame_record *__restrict__ records) {
+    extern __shared__ __attribute__((aligned(16))) float pool[];  // [g.max_pool] pooled dB / gaps
+    __shared__ int hist[256];
+    __shared__ int sh_int[2];
+    __shared__ int sh_nbottom, sh_best_start;
+    __shared__ float w_mean_db[10], w_best1k_db[10];
+    __shared__ int w_lo[10], w_hi[10], order[10];
+    __shared__ float sh_f[4];
+
+    const int lane = threadIdx.x;
+    const size_t frame = blockIdx.x;
+    const float *P = spectra + frame * (size_t)g.n;
+    StatsState st = state[frame];
+    if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
+    sdrg_frame_record rec;
+    rec.peak_bin = -1;
+    rec.abs_peak_db = -130.0f;
+    rec.signal_power_db = 0.0f;
+    rec.valid = 0;
+    rec.n_ref_windows = 0;
+
+    if (g.focus_len > 0) {
+        // ---- 6.2 focus peak: first maximum of dB, seeded at -130 (fft_process.cpp:142-154) ----
+        float best = -130.0f;
+        int bidx = 0x7fffffff;
+        for (int i = g.focus_lo + lane; i <= g.focus_hi; i += WAVE) {
+            const float d = db_of(P[i]);
+            if (d > best) {
+                best = d;
+                bidx = i;
+            }
+        }
+        for (int off = WAVE / 2; off > 0; off >>= 1) {
+            const float ob = __shfl_xor(best, off);
+            const int oi = __shfl_xor(bidx, off);
+            if (ob > best || (ob == best && oi < bidx)) {
+                best = ob;
+                bidx = oi;
+            }
+        }
+        const float abs_peak_db = best;
+        const int peak_bin = (bidx == 0x7fffffff) ? g.focus_lo : bidx;
+
+        // ---- 6.2 focus sum + 6.3 reference windows: one lane per window (reference order), lane n_ref
+        //      takes the focus window; all of them run the same sequential scan in lockstep ----
+        const int w1k = g.win_bins_1k;
+        const int n_ref = g.n_ref;
+        if (lane <= n_ref) {
+            const bool is_focus = (lane == n_ref);
+            const int lo = is_focus ? g.focus_lo : g.win_lo[lane];
+            const int hi = is_focus ? g.focus_hi : g.win_hi[lane];
+            const WinScan ws = scan_window(P, lo, hi, w1k);
+            const int n = hi - lo + 1;
+            if (is_focus) {
+                sh_f[0] = db_of(ws.sum / n);  // signalPowerDb (:155)
+                sh_f[1] = ws.best1k;          // focusBest1kLinear (:302)
+                sh_best_start = ws.best_start;
+            } else {
+                w_mean_db[lane] = db_of(ws.sum / n);
+                w_best1k_db[lane] = db_of(ws.best1k);
+                w_lo[lane] = lo;
+                w_hi[lane] = hi;
+            }
+        }
+        __syncthreads();
+        const float signal_power_db = sh_f[0];
+        const int valid = (n_ref >= 2);
+        rec.peak_bin = peak_bin;
+        rec.abs_peak_db = abs_peak_db;
+        rec.signal_power_db = signal_power_db;
+        rec.valid = valid;
+        rec.n_ref_windows = n_ref;
+
+        if (!valid) {
+            st.mean_snr_db = st.mean_snr_sigma = 0.0f;
+            st.peak_above_noise_mean_db = st.max_bin_snr_db = st.max_bin_snr_sigma = 0.0f;
+            st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
+        } else {
+            int n_bottom = 1;
+            if (lane == 0) {
+                // std::sort of <= 16 elements in libstdc++ is a (stable) insertion sort
+                for (int i = 0; i < n_ref; i++) order[i] = i;
+                for (int i = 1; i < n_ref; i++) {
+                    const int v = order[i];
+                    int j = i;
+                    while (j > 0 && w_mean_db[v] < w_mean_db[order[j - 1]]) {
+                        order[j] = order[j - 1];
+                        j--;
+                    }
+                    order[j] = v;
+                }
+                const int nb0 = (int)(n_ref * 0.4f);
+                n_bottom = nb0 > 1 ? nb0 : 1;
+                // 6.4a (:235-247)
+                float mean = 0.0f;
+                for (int i = 0; i < n_bottom; i++) mean += w_mean_db[order[i]];
+                mean /= n_bottom;
+                float gaps[10];
+                for (int i = 0; i < n_bottom; i++) gaps[i] = fabsf(w_mean_db[order[i]] - mean);
+                for (int i = 1; i < n_bottom; i++) {
+                    const float v = gaps[i];
+                    int j = i;
+                    while (j > 0 && v < gaps[j - 1]) { gaps[j] = gaps[j - 1]; j--; }
+                    gaps[j] = v;
+                }
+                const float sigma = fmax_ref(1.4816f * gaps[n_bottom / 2], 0.5f);
+                const float snr_db = signal_power_db - mean;
+                st.mean_snr_db = snr_db;
+                st.mean_snr_sigma = snr_db / sigma;
+                sh_nbottom = n_bottom;
+            }
+            __syncthreads();
+            n_bottom = sh_nbottom;
+
+            // ---- 6.4b pooled per-bin dB of the bottom windows, sorted-window order (:252-269) ----
+            int cnt = 0;
+            for (int j = 0; j < n_bottom; j++) {
+                const int lo = w_lo[order[j]], hi = w_hi[order[j]];
+                for (int i = lo + lane; i <= hi; i += WAVE) {
+                    const int q = cnt + (i - lo);
+                    if (q < g.max_pool) pool[q] = db_of(P[i]);
+                }
+                cnt += hi - lo + 1;
+            }
+            if (cnt > g.max_pool) cnt = g.max_pool;  // host sizes max_pool from the geometry
+            __syncthreads();
+            if (lane == 0) {
+                float m = 0.0f;
+                for (int q = 0; q < cnt; q++) m += pool[q];
+                m /= (float)cnt;
+                sh_f[2] = m;
+            }
+            __syncthreads();
+            const float per_bin_mean = sh_f[2];
+            for (int q = lane; q < cnt; q += WAVE) pool[q] = fabsf(pool[q] - per_bin_mean);
+            __syncthreads();
+            const float med = kth_smallest(pool, cnt, cnt / 2, hist, sh_int);
+            const float sigma_bin = (cnt > 0) ? fmax_ref(1.4816f * med, 1.0f) : 1.0f;
+            if (cnt > 0) st.per_bin_mean = per_bin_mean;
+            const float pbm = (cnt > 0) ? per_bin_mean : 0.0f;
+
+            if (lane == 0) {
+                st.peak_above_noise_mean_db = abs_peak_db - pbm;  // :274
+                // 6.4c (:281-288)
+                const float logN = logf((float)g.focus_len);
+                const float sqrt2logN = sqrtf(2.0f * logN);
+                const float gumbel_loc = pbm + sigma_bin * sqrt2logN;
+                const float gumbel_sig = fmax_ref(sigma_bin * 3.14159f / (sqrtf(6.0f) * sqrt2logN), 0.5f);
+                st.max_bin_snr_db = abs_peak_db - gumbel_loc;
+                st.max_bin_snr_sigma = st.max_bin_snr_db / gumbel_sig;
+                // 6.4d (:292-327)
+                float mean1k = 0.0f;
+                for (int i = 0; i < n_bottom; i++) mean1k += w_best1k_db[order[i]];
+                mean1k /= n_bottom;
+                float g1k[10];
+                for (int i = 0; i < n_bottom; i++) g1k[i] = fabsf(w_best1k_db[order[i]] - mean1k);
+                for (int i = 1; i < n_bottom; i++) {
+                    const float v = g1k[i];
+                    int j = i;
+                    while (j > 0 && v < g1k[j - 1]) { g1k[j] = g1k[j - 1]; j--; }
+                    g1k[j] = v;
+                }
+                const float sigma_floor_1k = sigma_bin / sqrtf((float)w1k);
+                float sigma1k = 1.4816f * g1k[n_bottom / 2];
+                if (sigma1k < sigma_floor_1k) sigma1k = sigma_floor_1k;
+                if (sigma1k < 0.5f) sigma1k = 0.5f;
+                const float focus_best1k_linear = sh_f[1];
+                if (focus_best1k_linear > 0.0f) {
+                    const float focus_best1k_db = db_of(focus_best1k_linear);
+                    st.best1khz_snr_db = focus_best1k_db - mean1k;
+                    st.best1khz_snr_sigma = st.best1khz_snr_db / sigma1k;
+                    const int best_start = sh_best_start;
+                    st.best1khz_center_freq_hz = (best_start + w1k / 2) * g.freq_per_bin + g.cf_minus_nyq;
+                } else {
+                    st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
+                }
+            }
+        }
+
+        if (lane == 0) {
+            // ---- 6.5 frequency tracking (:333-361), clock injected ----
+            if (st.tracking_frequency == 0.0f) st.tracking_frequency = g.cf_float;
+            if (st.center_frequency_changed) {
+                st.tracking_frequency = g.cf_float;
+                st.center_frequency_changed = 0;
+            }
+            if (!st.max_peak_set) {
+                st.max_peak_db = -130.0f;
+                st.max_peak_freq = g.cf_float;
+                st.max_peak_set = 1;
+            }
+            if (valid && abs_peak_db > st.max_peak_db) {
+                st.max_peak_db = abs_peak_db;
+                st.max_peak_freq = peak_bin * g.freq_per_bin + g.cf_u32_minus_nyq;
+                st.time_last_max_peak_ms = now_ms;
+            }
+            const int64_t ms_since = now_ms - st.time_last_max_peak_ms;
+            if (st.time_last_update_ms < st.time_last_max_peak_ms && ms_since > 300) {
+                st.tracking_frequency = st.max_peak_freq;
+                st.time_last_update_ms = now_ms;
+                st.max_peak_db = -130.0f;
+            }
+            // ---- 6.6 detection (:365-378) ----
+            const bool above = valid && (st.mean_snr_sigma >= 4.0f);
+            if (above) {
+                if (st.peak_confirmed < 1) st.peak_confirmed++;
+            } else {
+                st.peak_confirmed = 0;
+            }
+            const int flag = (above && st.peak_confirmed >= 1) ? 3 : 0;
+            st.det_buf[st.det_idx] = flag;
+            st.det_idx = (st.det_idx + 1) % 3;
+            int m = st.det_buf[0];
+            if (st.det_buf[1] > m) m = st.det_buf[1];
+            if (st.det_buf[2] > m) m = st.det_buf[2];
+            st.detection_flag_sent = m;
+        }
+    }
+
+    if (lane == 0) {
+        rec.tracking_frequency = (int64_t)roundf(st.tracking_frequency);
+        rec.mean_snr_db = st.mean_snr_db;
+        rec.mean_snr_sigma = st.mean_snr_sigma;
+        rec.peak_above_noise_mean_db = st.peak_above_noise_mean_db;
+        rec.max_bin_snr_db = st.max_bin_snr_db;
+        rec.max_bin_snr_sigma = st.max_bin_snr_sigma;
+        rec.best1khz_snr_db = st.best1khz_snr_db;
+        rec.best1khz_snr_sigma = st.best1khz_snr_sigma;
+        rec.best1khz_center_freq_hz = st.best1khz_center_freq_hz;
+        rec.per_bin_mean = st.per_bin_mean;
+        rec.detection_flag = st.detection_flag_sent;
+        if (records) records[frame] = rec;
+        state[frame] = st;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry &geo, int64_t now_ms,
+                        StatsState *state, sdrg_frame_record *records, hipStream_t stream) {
+    if (n_frames <= 0) return hipSuccess;
+    if (geo.max_pool > MAX_POOL) return hipErrorInvalidValue;
+    const size_t lds = sizeof(float) * (size_t)(geo.max_pool > 0 ? geo.max_pool : 1);
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(stats_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, MAX_POOL * 4);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(stats_kernel, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms, state, records);
+    return hipGetLastError();
+}
+
+}  // namespace sdrg

@@ -1,0 +1,329 @@
+"""Python binding of libsdrg.so (include/sdrg.h) — host-side mirror of the reference's SDRBridge surface.
+
+The reference exposes the hot path to Kotlin through JNI (java/fr/intuite/sdr/bridge/SDRBridge.kt:23-154):
+`SDRConfig`, `applyConfig(...)`, `read(12 callbacks)` and per-field setters.  This module mirrors that
+surface over the engine's C ABI with the same names and argument meaning:
+
+    cfg = SDRConfig(centerFrequency=100_000_000, sampleRate=2_000_000, samplesPerReading=16384)
+    eng = Engine(cfg, n_streams=4096)          # one reference "process" per stream
+    eng.applyConfig(cfg); eng.setFrequency(...); eng.setFrequencyFocusRange(...); eng.setSoundMode(...)
+    eng.read(fftCallback=..., meanSnrCallback=..., pcmCallback=...)   # register callbacks (JNI read)
+    spectra, records, pcm = eng.process(iq_frames, fmt=CS8)           # one frame per stream
+
+Everything runs in the HIP kernels of libsdrg.so; there is no CPU fallback.  If the library is missing
+or no gfx950 device is present, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG, "lib", "libsdrg.so")
+
+# include/sdrg.h
+CF32, CS8, CU8, CS16 = 0, 1, 2, 3
+STAGE_SPECTRUM, STAGE_STATS, STAGE_SSB, STAGE_ALL = 1, 2, 4, 7
+STATUS = {0: "SDRG_OK", -1: "SDRG_E_INVALID", -2: "SDRG_E_UNSUPPORTED", -3: "SDRG_E_NOMEM", -4: "SDRG_E_HIP",
+          -5: "SDRG_E_NODEVICE"}
+BYTES_PER_SAMPLE = {CF32: 8, CS8: 2, CU8: 2, CS16: 4}
+NUMPY_DTYPE = {CF32: np.float32, CS8: np.int8, CU8: np.uint8, CS16: np.int16}
+
+RECORD_DTYPE = np.dtype(
+    [
+        ("tracking_frequency", "<i8"),
+        ("mean_snr_db", "<f4"),
+        ("mean_snr_sigma", "<f4"),
+        ("peak_above_noise_mean_db", "<f4"),
+        ("max_bin_snr_db", "<f4"),
+        ("max_bin_snr_sigma", "<f4"),
+        ("best1khz_snr_db", "<f4"),
+        ("best1khz_snr_sigma", "<f4"),
+        ("best1khz_center_freq_hz", "<f4"),
+        ("per_bin_mean", "<f4"),
+        ("detection_flag", "<i4"),
+        ("peak_bin", "<i4"),
+        ("abs_peak_db", "<f4"),
+        ("signal_power_db", "<f4"),
+        ("valid", "<i4"),
+        ("n_ref_windows", "<i4"),
+    ],
+    align=True,
+)
+
+# Every entry point include/sdrg.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "sdrg_abi_version", "sdrg_last_error", "sdrg_ssb_pcm_len", "sdrg_ssb_design", "sdrg_engine_create", "sdrg_engine_destroy",
+    "sdrg_engine_apply_config", "sdrg_engine_set_frequency", "sdrg_engine_set_frequency_focus_range",
+    "sdrg_engine_set_sound_mode", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
+    "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_process_host",
+    "sdrg_engine_set_callbacks", "sdrg_engine_set_profiling", "sdrg_engine_get_timings",
+    "sdrg_engine_get_timing_stats", "sdrg_engine_reset_timing_stats",
+]
+
+
+class SdrgError(RuntimeError):
+    pass
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [
+        ("center_frequency", ctypes.c_int64),
+        ("sample_rate", ctypes.c_int64),
+        ("samples_per_reading", ctypes.c_int32),
+        ("freq_focus_range_khz", ctypes.c_int32),
+        ("gain", ctypes.c_int32),
+        ("sound_mode", ctypes.c_int32),
+        ("refresh_fft_ms", ctypes.c_int64),
+        ("refresh_peak_ms", ctypes.c_int64),
+        ("refresh_signal_strength_ms", ctypes.c_int64),
+    ]
+
+
+class _Timings(ctypes.Structure):
+    _fields_ = [("spectrum_ms", ctypes.c_float), ("stats_ms", ctypes.c_float), ("ssb_ms", ctypes.c_float),
+                ("total_ms", ctypes.c_float)]
+
+
+_V = ctypes.c_void_p
+_I32, _I64, _F = ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+CB_FFT = ctypes.CFUNCTYPE(None, _V, _I32, ctypes.POINTER(ctypes.c_float), _I32)
+CB_I = ctypes.CFUNCTYPE(None, _V, _I32, _I32)
+CB_F = ctypes.CFUNCTYPE(None, _V, _I32, _F)
+CB_J = ctypes.CFUNCTYPE(None, _V, _I32, _I64)
+CB_PCM = ctypes.CFUNCTYPE(None, _V, _I32, ctypes.POINTER(ctypes.c_int16), _I32)
+CB_FF = ctypes.CFUNCTYPE(None, _V, _I32, _F, _F)
+
+
+class _Callbacks(ctypes.Structure):
+    _fields_ = [
+        ("user", _V),
+        ("fft", CB_FFT),
+        ("detection_flag", CB_I),
+        ("mean_snr", CB_F),
+        ("mean_snr_sigma", CB_F),
+        ("peak_frequency", CB_J),
+        ("pcm", CB_PCM),
+        ("peak_above_noise_mean", CB_F),
+        ("max_bin", CB_FF),
+        ("best1khz", CB_FF),
+        ("noise_level", CB_F),
+    ]
+
+
+_lib = None
+
+
+def lib_path() -> str:
+    return LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    """Load libsdrg.so; raise if it has not been built (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SdrgError(f"{LIB_PATH} not built: run `make -C sdr-for-android-lib_amd` "
+                        "(or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    sig = {
+        "sdrg_abi_version": (_I32, []),
+        "sdrg_last_error": (ctypes.c_char_p, []),
+        "sdrg_ssb_pcm_len": (_I32, [_I32, _I64]),
+        "sdrg_ssb_design": (_I32, [_I32, _I64, _I32, P, P, P, P, ctypes.POINTER(_I32)]),
+        "sdrg_engine_create": (_I32, [ctypes.POINTER(_Config), _I32, _I32, ctypes.POINTER(P)]),
+        "sdrg_engine_destroy": (_I32, [P]),
+        "sdrg_engine_apply_config": (_I32, [P, ctypes.POINTER(_Config)]),
+        "sdrg_engine_set_frequency": (_I32, [P, _I64]),
+        "sdrg_engine_set_frequency_focus_range": (_I32, [P, _I32]),
+        "sdrg_engine_set_sound_mode": (_I32, [P, _I32]),
+        "sdrg_engine_get_config": (_I32, [P, ctypes.POINTER(_Config)]),
+        "sdrg_engine_n_streams": (_I32, [P]),
+        "sdrg_engine_pcm_len": (_I32, [P]),
+        "sdrg_engine_reset_state": (_I32, [P]),
+        "sdrg_engine_process_device": (_I32, [P, P, _I32, _I32, P, P, P, _I64]),
+        "sdrg_engine_synchronize": (_I32, [P]),
+        "sdrg_engine_process_host": (_I32, [P, P, _I32, _I32, P, P, P, _I64]),
+        "sdrg_engine_set_callbacks": (_I32, [P, ctypes.POINTER(_Callbacks)]),
+        "sdrg_engine_set_profiling": (_I32, [P, _I32]),
+        "sdrg_engine_get_timings": (_I32, [P, ctypes.POINTER(_Timings)]),
+        "sdrg_engine_get_timing_stats": (_I32, [P, ctypes.POINTER(_Timings), ctypes.POINTER(_I32)]),
+        "sdrg_engine_reset_timing_stats": (_I32, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().sdrg_last_error()
+        raise SdrgError(f"{what}: {STATUS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+
+def ssb_pcm_len(n: int, sample_rate: int) -> int:
+    return int(load().sdrg_ssb_pcm_len(n, sample_rate))
+
+
+def ssb_design(samp_count: int, sample_rate: int, sound_mode: int = 1) -> dict:
+    """The engine's SSB filter design for a configuration (host-side, no device)."""
+    lpf, hp, bp = (np.zeros(5, np.float32) for _ in range(3))
+    taps = np.zeros(256, np.float32)
+    nt = ctypes.c_int32()
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    _check(load().sdrg_ssb_design(samp_count, sample_rate, sound_mode, p(lpf), p(hp), p(bp), p(taps),
+                                  ctypes.byref(nt)), "ssb_design")
+    return {"lpf": lpf, "hp": hp, "bp": bp, "taps": taps[: nt.value].copy()}
+
+
+@dataclass
+class SDRConfig:
+    """Kotlin SDRConfig (SDRBridge.kt:23-37): same field names and defaults."""
+    centerFrequency: int = 430_000_000
+    samplesPerReading: int = 16384
+    sampleRate: int = 2_500_000
+    gain: int = 10
+    freqFocusRangeKhz: int = 5
+    refreshFFTMs: int = 50
+    refreshPeakMs: int = 200
+    refreshSignalStrengthMs: int = 30
+    soundMode: int = 1
+
+    def _c(self) -> _Config:
+        return _Config(self.centerFrequency, self.sampleRate, self.samplesPerReading, self.freqFocusRangeKhz,
+                       self.gain, self.soundMode, self.refreshFFTMs, self.refreshPeakMs, self.refreshSignalStrengthMs)
+
+
+class Engine:
+    """n_streams independent receivers on one GPU; each process call consumes one frame per stream."""
+
+    def __init__(self, cfg: SDRConfig, n_streams: int, device: int = 0):
+        L = load()
+        h = ctypes.c_void_p()
+        c = cfg._c()
+        _check(L.sdrg_engine_create(ctypes.byref(c), n_streams, device, ctypes.byref(h)), "sdrg_engine_create")
+        self._h = h
+        self.n_streams = n_streams
+        self.cfg = cfg
+        self._cbs = None
+
+    # ---- SDRBridge surface -------------------------------------------------------------------------
+    def applyConfig(self, cfg: SDRConfig) -> bool:
+        c = cfg._c()
+        _check(load().sdrg_engine_apply_config(self._h, ctypes.byref(c)), "applyConfig")
+        self.cfg = cfg
+        return True
+
+    def setFrequency(self, frequency: int) -> None:
+        _check(load().sdrg_engine_set_frequency(self._h, frequency), "setFrequency")
+        self.cfg.centerFrequency = frequency
+
+    def setFrequencyFocusRange(self, khz: int) -> None:
+        _check(load().sdrg_engine_set_frequency_focus_range(self._h, khz), "setFrequencyFocusRange")
+        self.cfg.freqFocusRangeKhz = khz
+
+    def setSoundMode(self, mode: int) -> None:
+        _check(load().sdrg_engine_set_sound_mode(self._h, mode), "setSoundMode")
+        self.cfg.soundMode = mode
+
+    def read(self, fftCallback=None, detectionFlagCallback=None, meanSnrCallback=None, meanSnrSigmaCallback=None,
+             peakFrequencyCallback=None, pcmCallback=None, peakAboveNoiseMeanCallback=None, maxBinCallback=None,
+             best1kHzCallback=None, noiseLevelCallback=None) -> None:
+        """Register per-frame callbacks (JNI read(), SDRBridge.kt:141-154).  Each receives the stream index
+        first, then the reference callback's arguments; arrays arrive as numpy copies."""
+        def wrap(fn, ctype, conv):
+            if fn is None:
+                return ctype()
+            return ctype(lambda _u, s, *a: fn(s, *conv(*a)))
+
+        n_of = lambda p, n: (np.ctypeslib.as_array(p, shape=(n,)).copy(),)  # noqa: E731
+        ident = lambda *a: a  # noqa: E731
+        self._cbs = _Callbacks(
+            None,
+            wrap(fftCallback, CB_FFT, n_of),
+            wrap(detectionFlagCallback, CB_I, ident),
+            wrap(meanSnrCallback, CB_F, ident),
+            wrap(meanSnrSigmaCallback, CB_F, ident),
+            wrap(peakFrequencyCallback, CB_J, ident),
+            wrap(pcmCallback, CB_PCM, n_of),
+            wrap(peakAboveNoiseMeanCallback, CB_F, ident),
+            wrap(maxBinCallback, CB_FF, ident),
+            wrap(best1kHzCallback, CB_FF, ident),
+            wrap(noiseLevelCallback, CB_F, ident),
+        )
+        _check(load().sdrg_engine_set_callbacks(self._h, ctypes.byref(self._cbs)), "read")
+
+    def stopReading(self) -> None:
+        _check(load().sdrg_engine_set_callbacks(self._h, None), "stopReading")
+        self._cbs = None
+
+    # ---- engine ------------------------------------------------------------------------------------
+    @property
+    def pcm_len(self) -> int:
+        return int(load().sdrg_engine_pcm_len(self._h))
+
+    def reset_state(self) -> None:
+        _check(load().sdrg_engine_reset_state(self._h), "reset_state")
+
+    def process(self, iq: np.ndarray, fmt: int = CS8, stages: int = STAGE_ALL, now_ms: int = 0):
+        """Host path: iq is [n_streams][samplesPerReading * 2] raw samples. Returns (spectra, records, pcm)."""
+        n = self.cfg.samplesPerReading
+        iq = np.ascontiguousarray(iq, dtype=NUMPY_DTYPE[fmt])
+        if iq.size != self.n_streams * n * 2:
+            raise SdrgError(f"iq has {iq.size} values, expected {self.n_streams}x{n}x2")
+        spec = np.empty((self.n_streams, n), np.float32) if stages & STAGE_SPECTRUM else None
+        recs = np.zeros(self.n_streams, RECORD_DTYPE) if stages & STAGE_STATS else None
+        plen = self.pcm_len
+        pcm = np.empty((self.n_streams, max(plen, 0)), np.int16) if stages & STAGE_SSB else None
+        ptr = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        _check(load().sdrg_engine_process_host(self._h, ptr(iq), fmt, stages, ptr(spec), ptr(recs),
+                                               ptr(pcm) if (pcm is not None and plen > 0) else None, now_ms),
+               "process_host")
+        return spec, recs, pcm
+
+    def process_device(self, iq_ptr: int, fmt: int, stages: int, spectra_ptr: int | None, records_ptr: int | None,
+                       pcm_ptr: int | None, now_ms: int = 0) -> None:
+        """Device path: raw device pointers (e.g. torch tensor .data_ptr()); asynchronous."""
+        _check(load().sdrg_engine_process_device(self._h, iq_ptr, fmt, stages, spectra_ptr, records_ptr, pcm_ptr,
+                                                 now_ms), "process_device")
+
+    def synchronize(self) -> None:
+        _check(load().sdrg_engine_synchronize(self._h), "synchronize")
+
+    def set_profiling(self, on: bool) -> None:
+        _check(load().sdrg_engine_set_profiling(self._h, int(on)), "set_profiling")
+
+    def timings(self) -> dict:
+        t = _Timings()
+        _check(load().sdrg_engine_get_timings(self._h, ctypes.byref(t)), "get_timings")
+        return {"spectrum_ms": t.spectrum_ms, "stats_ms": t.stats_ms, "ssb_ms": t.ssb_ms, "total_ms": t.total_ms}
+
+    def timing_stats(self) -> dict:
+        t = _Timings()
+        c = ctypes.c_int32()
+        _check(load().sdrg_engine_get_timing_stats(self._h, ctypes.byref(t), ctypes.byref(c)), "get_timing_stats")
+        return {"spectrum_ms": t.spectrum_ms, "stats_ms": t.stats_ms, "ssb_ms": t.ssb_ms, "total_ms": t.total_ms,
+                "count": c.value}
+
+    def reset_timing_stats(self) -> None:
+        _check(load().sdrg_engine_reset_timing_stats(self._h), "reset_timing_stats")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            load().sdrg_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
