@@ -38,7 +38,7 @@ extern "C" {
 typedef enum sdrg_status {
     SDRG_OK = 0,
     SDRG_E_INVALID = -1,      /* bad argument (null pointer, non-positive size, ...) */
-    SDRG_E_UNSUPPORTED = -2,  /* e.g. samples_per_reading not a power of two in [64, 65536] */
+    SDRG_E_UNSUPPORTED = -2,  /* e.g. a spectrum of a size the FFT kernels do not cover */
     SDRG_E_NOMEM = -3,        /* device allocation failed */
     SDRG_E_HIP = -4,          /* a HIP runtime call failed (message via sdrg_last_error) */
     SDRG_E_NODEVICE = -5      /* no gfx950 device / HIP runtime not usable */
@@ -70,7 +70,8 @@ enum {
 typedef struct sdrg_config {
     int64_t center_frequency;          /* Hz; the reference stores it as uint32 (bridge-config.h:18) */
     int64_t sample_rate;               /* Hz; uint32 in the reference */
-    int32_t samples_per_reading;       /* frame size N */
+    int32_t samples_per_reading;       /* frame size N: any N in [1, 2^20] for SSB; the spectrum needs a
+                                          power of two in [64, 65536] (SDRBridge.kt:25 recommends multiples of 512) */
     int32_t freq_focus_range_khz;      /* focus half-width X in kHz */
     int32_t gain;
     int32_t sound_mode;                /* 0,1,2 (SDRBridge.kt:35-36); other values keep the last mode */
@@ -166,6 +167,9 @@ int32_t sdrg_engine_set_frequency(sdrg_engine *eng, int64_t center_frequency);
 int32_t sdrg_engine_set_frequency_focus_range(sdrg_engine *eng, int32_t khz);
 /* JNI setSoundMode (:1066-1071). */
 int32_t sdrg_engine_set_sound_mode(sdrg_engine *eng, int32_t mode);
+/* processSSB_opt's upperSideband argument (default 1, which is what SSBProcessor always passes,
+ * ssb_processor.cpp:103; 0 gives the reference's lower-sideband result, Re - Im of {y, y} = 0). */
+int32_t sdrg_engine_set_upper_sideband(sdrg_engine *eng, int32_t upper);
 /* Current configuration (BridgeConfig getters, bridge-config.h:41-51). */
 int32_t sdrg_engine_get_config(const sdrg_engine *eng, sdrg_config *out);
 int32_t sdrg_engine_n_streams(const sdrg_engine *eng);

@@ -1,0 +1,80 @@
+// sdrg_compat.hpp — source-compatible C++ drop-ins for the reference's internal DSP seams, implemented
+// over the C ABI (sdrg.h).  A bridge that was written against
+//
+//   class FFTProcessor                       src/dsp/fft_process.h:29-55
+//   void processSSB_opt(...)                  src/ssb/ssb_demod_opt.h:64-65
+//
+// compiles unchanged against these (include this header instead and `using namespace sdrg::compat;`),
+// and its per-frame work then runs on the MI355X.  Each object owns a one-stream engine; the batched
+// C ABI (sdrg_engine_process_device) is the high-throughput path for many receivers.
+#pragma once
+
+#include <complex>
+#include <cstdint>
+#include <vector>
+
+#include "sdrg.h"
+
+namespace sdrg {
+namespace compat {
+
+// FftProcessorConfig (fft_process.h:20-26)
+struct FftProcessorConfig {
+    uint32_t centerFrequency;
+    uint32_t sampleRate;
+    int samplesPerReading;
+    int freqFocusRangeKhz;
+};
+
+// FFTProcessor (fft_process.h:29-115): same public interface and getter semantics.  Frequency tracking
+// uses std::chrono::steady_clock like the reference (fft_process.cpp:349-352).
+class FFTProcessor {
+public:
+    FFTProcessor();
+    ~FFTProcessor();
+    FFTProcessor(const FFTProcessor &) = delete;
+    FFTProcessor &operator=(const FFTProcessor &) = delete;
+
+    void configure(const FftProcessorConfig &config);
+    void process(const std::complex<float> *input_buf, uint32_t input_len);
+    // setFrequency (sdr-bridge-java-soapy.cpp:907) raises isCenterFrequencyChanged; call this instead
+    void notifyCenterFrequencyChanged();
+
+    const std::vector<float> &getPowerSpectrum() const { return power_shifted_vec_; }
+    float getMeanSnrDb() const { return rec_.mean_snr_db; }
+    float getMeanSnrSigma() const { return rec_.mean_snr_sigma; }
+    long getTrackingFrequency() const { return static_cast<long>(rec_.tracking_frequency); }
+    int getDetectionFlag() const { return rec_.detection_flag; }
+    float getPeakAboveNoiseMeanDb() const { return rec_.peak_above_noise_mean_db; }
+    float getMaxBinSnrDb() const { return rec_.max_bin_snr_db; }
+    float getMaxBinSnrSigma() const { return rec_.max_bin_snr_sigma; }
+    float getBest1kHzSnrDb() const { return rec_.best1khz_snr_db; }
+    float getBest1kHzSnrSigma() const { return rec_.best1khz_snr_sigma; }
+    float getBest1kHzCenterFreqHz() const { return rec_.best1khz_center_freq_hz; }
+    float getPerBinMean() const { return rec_.per_bin_mean; }
+
+    // status of the last call (the reference never fails; the engine can, e.g. without a GPU)
+    int32_t lastStatus() const { return status_; }
+    // process with an explicit clock (ms) instead of steady_clock, for reproducible tests
+    void processAt(const std::complex<float> *input_buf, uint32_t input_len, int64_t now_ms);
+
+private:
+    sdrg_engine *eng_ = nullptr;
+    sdrg_config cfg_{};
+    bool configured_ = false;
+    bool cf_changed_ = false;
+    int32_t status_ = SDRG_OK;
+    std::vector<float> power_shifted_vec_;
+    sdrg_frame_record rec_{};
+};
+
+// processSSB_opt (ssb_demod_opt.h:64-65).  Like the reference, the chain's filter state is process-global
+// (one shared one-stream engine); `pulse` is left untouched as in the reference (its detector is a TO DO).
+void processSSB_opt(std::vector<std::complex<float>> iq, uint32_t sampleRate, bool upperSideband,
+                    std::vector<int16_t> &pcmOut, bool &pulse, int mode);
+
+// Status of the last processSSB_opt call.
+int32_t lastSsbStatus();
+
+}  // namespace compat
+}  // namespace sdrg

@@ -45,7 +45,6 @@ int32_t fail(int32_t code, const char *fmt, ...) {
         if (e_ != hipSuccess) return fail(SDRG_E_HIP, "%s: %s", #expr, hipGetErrorString(e_));    \
     } while (0)
 
-bool is_pow2(int64_t n) { return n > 0 && (n & (n - 1)) == 0; }
 
 // processSSB_opt's statics that every stream of an engine shares (they only depend on the call sequence)
 struct SsbControl {
@@ -94,6 +93,8 @@ struct sdrg_engine {
     size_t ssb_scratch_elems = 0;
     float *d_spec_scratch = nullptr;
     size_t spec_scratch_elems = 0;
+    float *d_fft_scratch = nullptr;   // four-step intermediate (N > 16384)
+    size_t fft_scratch_elems = 0;
     sdrg_frame_record *d_rec_scratch = nullptr;
     // host-path staging
     void *d_iq_stage = nullptr;
@@ -109,6 +110,7 @@ struct sdrg_engine {
 
     SsbControl ssb;
     bool cf_changed_pending = false;
+    int upper = 1;
     bool has_cbs = false;
     sdrg_callbacks cbs{};
 };
@@ -117,9 +119,8 @@ namespace {
 
 int32_t validate_config(const sdrg_config *cfg) {
     if (!cfg) return fail(SDRG_E_INVALID, "null config");
-    if (cfg->samples_per_reading < 64 || cfg->samples_per_reading > 65536 || !is_pow2(cfg->samples_per_reading))
-        return fail(SDRG_E_UNSUPPORTED, "samples_per_reading %d: need a power of two in [64, 65536]",
-                    cfg->samples_per_reading);
+    if (cfg->samples_per_reading < 1 || cfg->samples_per_reading > (1 << 20))
+        return fail(SDRG_E_UNSUPPORTED, "samples_per_reading %d outside [1, 2^20]", cfg->samples_per_reading);
     if ((uint32_t)cfg->sample_rate == 0) return fail(SDRG_E_INVALID, "sample_rate must be > 0");
     if (cfg->freq_focus_range_khz < 0) return fail(SDRG_E_INVALID, "freq_focus_range_khz must be >= 0");
     return SDRG_OK;
@@ -235,7 +236,7 @@ int32_t prepare_ssb(sdrg_engine *e, SsbParams *p) {
     memset(p, 0, sizeof(*p));
     p->samp_count = (int32_t)c.samp_count;
     p->n_in = e->cfg.samples_per_reading;
-    p->upper = 1;  // SSBProcessor always asks for the upper sideband (ssb_processor.cpp:103)
+    p->upper = e->upper;  // SSBProcessor always asks for the upper sideband (ssb_processor.cpp:103)
     p->decim = decim;
     p->n_taps = c.n_taps;
     p->pcm_len = ssb_pcm_len(c.samp_count, fs);
@@ -310,6 +311,8 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     if (do_spec) {
         int32_t rc = upload_twiddles(e, n);
         if (rc) return rc;
+        rc = ensure_device(&e->d_fft_scratch, &e->fft_scratch_elems, spectrum_scratch_floats(n, B));
+        if (rc) return rc;
     }
 
     StatsGeometry geo{};
@@ -343,7 +346,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
     }
     if (do_spec) {
-        HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->s_main));
+        HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, e->s_main));
         if (prof) HIP_TRY(hipEventRecord(ev->spec, e->s_main));
     }
     if (do_stats) {
@@ -455,7 +458,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     (void)hipSetDevice(e->device);
     if (e->s_main) (void)hipStreamSynchronize(e->s_main);
     if (e->s_ssb) (void)hipStreamSynchronize(e->s_ssb);
-    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_ssb_scratch, e->d_spec_scratch,
+    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch,
                     e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -498,6 +501,12 @@ int32_t sdrg_engine_set_frequency_focus_range(sdrg_engine *e, int32_t khz) {
 int32_t sdrg_engine_set_sound_mode(sdrg_engine *e, int32_t mode) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     e->cfg.sound_mode = mode;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_upper_sideband(sdrg_engine *e, int32_t upper) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    e->upper = upper ? 1 : 0;
     return SDRG_OK;
 }
 

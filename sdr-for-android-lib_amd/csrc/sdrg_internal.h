@@ -12,11 +12,14 @@ namespace sdrg {
 // ------------------------------------------------------------------------------------------------
 // Launchers (defined in the .hip translation units).  All are asynchronous on `stream`.
 // ------------------------------------------------------------------------------------------------
-// Is N supported by the LDS-resident spectrum kernel?
+// Spectrum kernels: N <= 16384 one LDS-resident workgroup per frame; N = 32768/65536 two-kernel four-step
+// in waves of SPECTRUM_WAVE_FRAMES frames (intermediate in `scratch`, spectrum_scratch_floats() floats).
+constexpr int SPECTRUM_WAVE_FRAMES = 128;
 bool spectrum_supported(int n);
-// Twiddle table exp(-2 pi i m / N), m in [0, N), float2, computed in double on the host.
+size_t spectrum_scratch_floats(int n, int n_frames);
+// twiddles: exp(-2 pi i m / N), m in [0, N), float2, computed in double on the host.
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles,
-                           float *spectra, hipStream_t stream);
+                           float *spectra, float *scratch, hipStream_t stream);
 
 hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry &geo, int64_t now_ms,
                         StatsState *state, sdrg_frame_record *records, hipStream_t stream);

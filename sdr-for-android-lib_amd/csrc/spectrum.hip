@@ -212,16 +212,163 @@ hipError_t launch_n(const void *iq, int fmt, int n_frames, const float *tw, floa
     }
 }
 
+// ================================================================================================
+// N = 32768 / 65536: the frame (256 / 512 KiB as complex float) does not fit in LDS (160 KiB), so the
+// transform is a two-kernel four-step FFT, N = N1 * N2 with n = N2 n1 + n2 and k = k1 + N1 k2:
+//   kernel A (column tiles): Y[k1][n2] = W_N^(n2 k1) * DFT_N1 over n1 of x[N2 n1 + n2]   (reads raw IQ)
+//   kernel B (row tiles)   : X[k1 + N1 k2] = DFT_N2 over n2 of Y[k1][n2]; writes |X|^2 fftshifted
+// Each tile runs a Stockham FFT in LDS with 16 values per thread.  Frames go through in waves whose
+// intermediate Y (8 B/sample) stays inside the 256 MiB Infinity Cache between the two kernels.
+// ================================================================================================
+constexpr int TILE_T = 256;  // threads per tile workgroup
+
+template <int L>
+struct TilePlan {
+    static constexpr int C = 16 * TILE_T / L;  // columns (rows) per tile so that C*L = 16*T
+    static constexpr int LP = L + 1;           // padded column length in LDS
+    static constexpr int RA = (L == 256) ? 16 : (L == 128) ? 8 : 0;
+    static constexpr int RB = 16;
+};
+
+// One Stockham pass over every column of an LDS tile [C][LP]; FIRST reads through load(c, e),
+// LAST writes through store(c, k, v).
+template <int N, int L, int R, int NS, bool FIRST, bool LAST, class Load, class Store>
+__device__ __forceinline__ void tile_pass(f2 *lds, const f2 *__restrict__ tw, Load load, Store store) {
+    using TP = TilePlan<L>;
+    constexpr int C = TP::C;
+    constexpr int NB = (C * L / R) / TILE_T;
+    static_assert(NB >= 1, "tile too small for radix");
+    const int c = threadIdx.x % C, jj = threadIdx.x / C;
+    f2 x[NB][R];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int j = jj + b * (TILE_T / C);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int e = j + r * (L / R);
+            if constexpr (FIRST)
+                x[b][r] = load(c, e);
+            else
+                x[b][r] = lds[c * TP::LP + e];
+        }
+    }
+    if constexpr (!FIRST) __syncthreads();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int j = jj + b * (TILE_T / C);
+        if constexpr (NS > 1) {
+            const int k = j & (NS - 1);
+#pragma unroll
+            for (int r = 1; r < R; ++r) x[b][r] = cmul(x[b][r], tw[(r * k) * (N / (NS * R))]);
+        }
+        dft<R>(x[b]);
+        if constexpr (LAST) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) store(c, j + r * (L / R), x[b][r]);
+        } else {
+            const int base = (j / NS) * NS * R + (j & (NS - 1));
+#pragma unroll
+            for (int r = 0; r < R; ++r) lds[c * TP::LP + base + r * NS] = x[b][r];
+        }
+    }
+    if constexpr (!LAST) __syncthreads();
+}
+
+template <int LOG2N1, int LOG2N2, int FMT>
+__global__ __launch_bounds__(TILE_T) void four_step_a(const void *__restrict__ iq, f2 *__restrict__ Y,
+                                                       const f2 *__restrict__ tw) {
+    constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
+    using TP = TilePlan<N1>;
+    __shared__ __attribute__((aligned(16))) f2 lds[TP::C * TP::LP];
+    const size_t frame = blockIdx.y;
+    const int c0 = blockIdx.x * TP::C;
+    const void *src = reinterpret_cast<const char *>(iq) + frame * (size_t)N * bytes_per_sample<FMT>();
+    f2 *y = Y + frame * (size_t)N;
+    auto load = [&](int c, int n1) { return load_sample<FMT>(src, N2 * n1 + c0 + c); };
+    auto none = [](int, int, f2) {};
+    auto store = [&](int c, int k1, f2 v) {
+        const int n2 = c0 + c;
+        y[k1 * N2 + n2] = cmul(v, tw[(n2 * k1) & (N - 1)]);
+    };
+    auto noload = [](int, int) { return f2{0.0f, 0.0f}; };
+    tile_pass<N, N1, TP::RA, 1, true, false>(lds, tw, load, none);
+    tile_pass<N, N1, TP::RB, TP::RA, false, true>(lds, tw, noload, store);
+}
+
+template <int LOG2N1, int LOG2N2>
+__global__ __launch_bounds__(TILE_T) void four_step_b(const f2 *__restrict__ Y, float *__restrict__ spectra,
+                                                       const f2 *__restrict__ tw) {
+    constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
+    using TP = TilePlan<N2>;
+    __shared__ __attribute__((aligned(16))) f2 lds[TP::C * TP::LP];
+    const size_t frame = blockIdx.y;
+    const int r0 = blockIdx.x * TP::C;
+    const f2 *y = Y + frame * (size_t)N + (size_t)r0 * N2;
+    float *out = spectra + frame * (size_t)N;
+    // stage the C rows coalesced
+#pragma unroll
+    for (int i = 0; i < TP::C * N2 / TILE_T; ++i) {
+        const int e = threadIdx.x + i * TILE_T;
+        lds[(e / N2) * TP::LP + (e % N2)] = y[e];
+    }
+    __syncthreads();
+    auto noload = [](int, int) { return f2{0.0f, 0.0f}; };
+    auto none = [](int, int, f2) {};
+    auto store = [&](int rho, int k2, f2 v) {
+        const int k = r0 + rho + N1 * k2;
+        out[(k + N / 2) & (N - 1)] = v.x * v.x + v.y * v.y;
+    };
+    tile_pass<N, N2, TP::RA, 1, false, false>(lds, tw, noload, none);
+    tile_pass<N, N2, TP::RB, TP::RA, false, true>(lds, tw, noload, store);
+}
+
+template <int LOG2N1, int LOG2N2, int FMT>
+hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, float *spectra, float *scratch,
+                            int wave, hipStream_t s) {
+    constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
+    const f2 *tw = reinterpret_cast<const f2 *>(twf);
+    f2 *Y = reinterpret_cast<f2 *>(scratch);
+    for (int f0 = 0; f0 < n_frames; f0 += wave) {
+        const int nf = (n_frames - f0) < wave ? (n_frames - f0) : wave;
+        const char *src = reinterpret_cast<const char *>(iq) + (size_t)f0 * N * bytes_per_sample<FMT>();
+        hipLaunchKernelGGL((four_step_a<LOG2N1, LOG2N2, FMT>), dim3(N2 / TilePlan<N1>::C, nf), dim3(TILE_T), 0, s,
+                           src, Y, tw);
+        hipLaunchKernelGGL((four_step_b<LOG2N1, LOG2N2>), dim3(N1 / TilePlan<N2>::C, nf), dim3(TILE_T), 0, s, Y,
+                           spectra + (size_t)f0 * N, tw);
+    }
+    return hipGetLastError();
+}
+
+template <int LOG2N1, int LOG2N2>
+hipError_t launch_four_step_fmt(const void *iq, int fmt, int n_frames, const float *tw, float *spectra,
+                                float *scratch, int wave, hipStream_t s) {
+    switch (fmt) {
+    case SDRG_IQ_CS8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS8>(iq, n_frames, tw, spectra, scratch, wave, s);
+    case SDRG_IQ_CU8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CU8>(iq, n_frames, tw, spectra, scratch, wave, s);
+    case SDRG_IQ_CS16: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS16>(iq, n_frames, tw, spectra, scratch, wave, s);
+    case SDRG_IQ_CF32: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CF32>(iq, n_frames, tw, spectra, scratch, wave, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
 }  // namespace
 
 bool spectrum_supported(int n) {
-    return n >= 64 && n <= 16384 && (n & (n - 1)) == 0;
+    return n >= 64 && n <= 65536 && (n & (n - 1)) == 0;
+}
+
+size_t spectrum_scratch_floats(int n, int n_frames) {
+    if (n <= 16384) return 0;
+    const int wave = n_frames < SPECTRUM_WAVE_FRAMES ? n_frames : SPECTRUM_WAVE_FRAMES;
+    return (size_t)wave * n * 2;
 }
 
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles, float *spectra,
-                           hipStream_t stream) {
+                           float *scratch, hipStream_t stream) {
     if (n_frames <= 0) return hipSuccess;
     switch (n) {
+    case 32768: return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
+    case 65536: return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
     case 64: return launch_n<6>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 128: return launch_n<7>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 256: return launch_n<8>(iq, fmt, n_frames, twiddles, spectra, stream);

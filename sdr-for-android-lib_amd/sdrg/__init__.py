@@ -59,7 +59,7 @@ RECORD_DTYPE = np.dtype(
 EXPORTS = [
     "sdrg_abi_version", "sdrg_last_error", "sdrg_ssb_pcm_len", "sdrg_ssb_design", "sdrg_engine_create", "sdrg_engine_destroy",
     "sdrg_engine_apply_config", "sdrg_engine_set_frequency", "sdrg_engine_set_frequency_focus_range",
-    "sdrg_engine_set_sound_mode", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
+    "sdrg_engine_set_sound_mode", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
     "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_process_host",
     "sdrg_engine_set_callbacks", "sdrg_engine_set_profiling", "sdrg_engine_get_timings",
     "sdrg_engine_get_timing_stats", "sdrg_engine_reset_timing_stats",
@@ -143,6 +143,7 @@ def load() -> ctypes.CDLL:
         "sdrg_engine_set_frequency": (_I32, [P, _I64]),
         "sdrg_engine_set_frequency_focus_range": (_I32, [P, _I32]),
         "sdrg_engine_set_sound_mode": (_I32, [P, _I32]),
+        "sdrg_engine_set_upper_sideband": (_I32, [P, _I32]),
         "sdrg_engine_get_config": (_I32, [P, ctypes.POINTER(_Config)]),
         "sdrg_engine_n_streams": (_I32, [P]),
         "sdrg_engine_pcm_len": (_I32, [P]),
@@ -234,6 +235,9 @@ class Engine:
     def setSoundMode(self, mode: int) -> None:
         _check(load().sdrg_engine_set_sound_mode(self._h, mode), "setSoundMode")
         self.cfg.soundMode = mode
+
+    def setUpperSideband(self, upper: bool) -> None:
+        _check(load().sdrg_engine_set_upper_sideband(self._h, int(upper)), "setUpperSideband")
 
     def read(self, fftCallback=None, detectionFlagCallback=None, meanSnrCallback=None, meanSnrSigmaCallback=None,
              peakFrequencyCallback=None, pcmCallback=None, peakAboveNoiseMeanCallback=None, maxBinCallback=None,

@@ -88,5 +88,5 @@ def test_engine_create_without_gpu_reports_status():
 
 def test_invalid_configs_rejected_before_device():
     with pytest.raises(sdrg.SdrgError) as ei:
-        sdrg.Engine(sdrg.SDRConfig(samplesPerReading=1000), 1)
+        sdrg.Engine(sdrg.SDRConfig(samplesPerReading=0), 1)
     assert "UNSUPPORTED" in str(ei.value)
