@@ -24,7 +24,10 @@ hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const f
 hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry &geo, int64_t now_ms,
                         StatsState *state, sdrg_frame_record *records, hipStream_t stream);
 
-// scratch: [n_frames][samp_count] float (AGC output) ; taps: [n_taps] device floats
+// SSB chain.  The pipelined kernel needs no scratch; the lane-per-stream reference kernels (used for
+// sample rates below ~0.9 MHz, or when SDRG_SSB_REFERENCE_KERNELS=1) need
+// scratch: [n_frames][samp_count + pcm_len] floats.  taps: [n_taps] device floats.
+bool ssb_force_reference_kernels();
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       SsbStreamState *state, float *scratch, int16_t *pcm, hipStream_t stream);
 

@@ -10,11 +10,14 @@
 // output is therefore bit-identical to the reference, and the parallelism comes from running many
 // streams at once (one lane per stream) and from the FIR, whose outputs are independent.
 //
-// Kernels:
+// Kernels (the pipelined ssb_pipe_kernel below is the production path; these three are the
+// straightforward lane-per-stream form, kept for configurations the pipeline does not cover):
 //   ssb_chain_kernel : lane = stream; DC -> LPF -> demod -> AGC over the frame; AGC output -> scratch
 //   ssb_fir_kernel   : block = 64 outputs of one stream; input window staged in LDS; each output is the
 //                      reference's sequential 255-term sum
 //   ssb_eq_kernel    : lane = stream; HP -> BP -> boost -> PCM over the decimated frame
+#include <stdlib.h>
+
 #include "sdrg_internal.h"
 
 #pragma clang fp contract(off)
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(WAVE) void ssb_chain_kernel(const char *__restrict_
 
     const int S = p.samp_count;
     const int live = p.n_in < S ? p.n_in : S;  // samples present; the rest is iq.resize() zero padding
-    const int n8 = live & ~7;
+    const int n8 = (reinterpret_cast<uintptr_t>(frame) & 15) == 0 ? (live & ~7) : 0;  // 16-B loads need alignment
     int n = 0;
     for (; n < n8; n += 8) {
         float x[8];
@@ -187,9 +190,282 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
     state[s] = st;
 }
 
+// ================================================================================================
+// Pipelined SSB engine (the production path).
+//
+// The chain has three sample-serial recurrences (DC tracker, 2nd-order low-pass, AGC gain) whose
+// per-sample latency, not the chip's throughput, bounds the frame time: a lone wave issues one VALU
+// instruction per ~4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so every
+// non-recurrent operation left in a serial wave lengthens the frame.  This kernel therefore gives each
+// recurrence its own wave (lane = stream), keeps ONLY the recurrence arithmetic in it, and moves every
+// order-free operation (unpack, the AGC's sqrt/div "desired" level, the clamp, the FIR) to helper waves.
+// The stages are pipelined over chunks of CH samples through LDS rings with one workgroup barrier per
+// chunk, so while the low-pass wave works on chunk c the DC wave is on c+1, the helpers on c-1 ... c-4:
+//
+//   it:   load c=it | DC c=it-1 | LPF c=it-2 | DESIRED c=it-3 | AGC c=it-4 | OUT c=it-5 | FIR c=it-6 | EQ c=it-7
+//
+// The FIR accumulates each output's 255 products as its samples arrive (k ascending, exactly the
+// reference's order), so no sample window is kept; completed outputs go to the EQ wave (HP, BP, boost,
+// PCM).  All arithmetic is the reference's, in its order, without contraction: bit-identical PCM.
+// Workgroup = 32 streams x 16 waves; waves 0-3 are the serial roles (one per SIMD), 4-15 helpers.
+// ================================================================================================
+constexpr int PG = 32;          // streams per workgroup
+constexpr int CH = 32;          // samples per chunk
+constexpr int ROW = CH + 4;     // padded LDS row (floats): conflict-free ds_read_b128 by stream lanes
+constexpr int BUFF = PG * ROW;  // floats per chunk buffer
+constexpr int PIPE_T = 1024;    // 16 waves
+constexpr int MAX_SLOTS = 16;   // concurrent FIR outputs per stream
+constexpr int MAX_DONE = 4;     // FIR outputs completed per stream per chunk
+
+struct PipeLds {
+    float re[2][BUFF];
+    float a[2][BUFF];
+    float y[4][BUFF];
+    float d[2][BUFF];
+    float g[2][BUFF];
+    float out[2][BUFF];
+    float facc[PG * MAX_SLOTS];
+    float fq[2][PG * MAX_DONE];
+    float taps[256];
+};
+
+__device__ __forceinline__ int ceil_div_i(int a, int b) {  // b > 0, any sign of a
+    return a >= 0 ? (a + b - 1) / b : -((-a) / b);
+}
+
+template <int FMT>
+__device__ __forceinline__ void load_i8_masked(const char *frame, int t, int n_in, float (&x)[8]) {
+    if (t + 8 <= n_in && (reinterpret_cast<uintptr_t>(frame) & 15) == 0) {
+        load_i8<FMT>(frame, t, x);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; q++) x[q] = (t + q < n_in) ? load_i1<FMT>(frame, t + q) : 0.0f;
+    }
+}
+
+template <int FMT>
+__global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
+                                                          int n_slots, const float *__restrict__ taps,
+                                                          SsbStreamState *__restrict__ state,
+                                                          int16_t *__restrict__ pcm) {
+    __shared__ PipeLds L;
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int s0 = blockIdx.x * PG;
+    const int S = p.samp_count;
+    const int nch = (S + CH - 1) / CH;
+    const int D = p.decim, NT = p.n_taps, PL = p.pcm_len;
+
+    for (int i = tid; i < NT; i += PIPE_T) L.taps[i] = taps[i];
+
+    // per-role persistent state (registers)
+    const int my_s = lane;  // serial roles: lane = stream within the group
+    const bool serial_live = (wave < 4) && (lane < PG) && (s0 + lane < n_frames);
+    float dc = 0.0f;                              // removeDC: reset per call (:50)
+    float z1 = 0.0f, z2 = 0.0f;                   // rfFilter state, carried across frames
+    float gain = 1.0f;                            // adaptiveAGC: reset per call (:102)
+    float h1 = 0.0f, h2 = 0.0f, q1 = 0.0f, q2 = 0.0f, prev = 0.0f;  // HP/BP state (carried), boost prev
+    if (serial_live) {
+        const SsbStreamState st = state[s0 + my_s];
+        z1 = st.lpf_z1; z2 = st.lpf_z2;
+        h1 = st.hp_z1; h2 = st.hp_z2; q1 = st.bp_z1; q2 = st.bp_z2;
+    }
+    if (wave < 3) __builtin_amdgcn_s_setprio(2);  // the recurrences own their SIMD's issue slots
+    const size_t bps = bytes_per_sample<FMT>();
+    __syncthreads();
+
+    for (int it = 0; it < nch + 8; ++it) {
+        if (wave == 0) {
+            // ---- removeDC (:49-55) + a0 * x of iir2Process, chunk it-1 ----
+            const int c = it - 1;
+            if (c >= 0 && c < nch && lane < PG) {
+                const float *re = &L.re[c & 1][my_s * ROW];
+                float *ao = &L.a[c & 1][my_s * ROW];
+                const int lim = min(CH, S - c * CH);
+                const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
+#pragma unroll 2
+                for (int i = 0; i < CH; i += 4) {
+                    const float4 r = *reinterpret_cast<const float4 *>(re + i);
+                    float v[4] = {r.x, r.y, r.z, r.w}, o[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (i + q < lim) {
+                            dc = alpha * dc + one_minus * v[q];
+                            o[q] = a0 * (v[q] - dc);
+                        } else {
+                            o[q] = 0.0f;
+                        }
+                    }
+                    *reinterpret_cast<float4 *>(ao + i) = make_float4(o[0], o[1], o[2], o[3]);
+                }
+            }
+        } else if (wave == 1) {
+            // ---- iir2Process recurrence (:75-84), chunk it-2 ----
+            const int c = it - 2;
+            if (c >= 0 && c < nch && lane < PG) {
+                const float *ai = &L.a[c & 1][my_s * ROW];
+                float *yo = &L.y[c & 3][my_s * ROW];
+                const int lim = min(CH, S - c * CH);
+                const float a1 = p.lpf[1], a2 = p.lpf[2], b1 = p.lpf[3], b2 = p.lpf[4];
+#pragma unroll 2
+                for (int i = 0; i < CH; i += 4) {
+                    const float4 r = *reinterpret_cast<const float4 *>(ai + i);
+                    float v[4] = {r.x, r.y, r.z, r.w}, o[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (i + q < lim) {
+                            const float y = v[q] + a1 * z1 + a2 * z2 - b1 * z1 - b2 * z2;
+                            z2 = z1;
+                            z1 = y;
+                            o[q] = y;
+                        } else {
+                            o[q] = 0.0f;
+                        }
+                    }
+                    *reinterpret_cast<float4 *>(yo + i) = make_float4(o[0], o[1], o[2], o[3]);
+                }
+            }
+        } else if (wave == 2) {
+            // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
+            const int c = it - 4;
+            if (c >= 0 && c < nch && lane < PG) {
+                const float *di = &L.d[c & 1][my_s * ROW];
+                float *go = &L.g[c & 1][my_s * ROW];
+                const int lim = min(CH, S - c * CH);
+                const float fast = p.agc_fast, slow = 0.00035f;
+                const float omf = 1.0f - fast, oms = 1.0f - slow;
+#pragma unroll 2
+                for (int i = 0; i < CH; i += 4) {
+                    const float4 r = *reinterpret_cast<const float4 *>(di + i);
+                    float v[4] = {r.x, r.y, r.z, r.w}, o[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (i + q < lim) {
+                            const float desired = v[q];
+                            const float gf = gain * omf + desired * fast;
+                            const float gs = gain * oms + desired * slow;
+                            gain = (desired < gain) ? gf : gs;
+                        }
+                        o[q] = gain;
+                    }
+                    *reinterpret_cast<float4 *>(go + i) = make_float4(o[0], o[1], o[2], o[3]);
+                }
+            }
+        } else if (wave == 3) {
+            // ---- HP -> BP -> transientBoost -> floatToPCM on outputs the FIR completed, chunk it-7 ----
+            const int c = it - 7;
+            if (c >= 0 && c < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
+                const int t0 = c * CH, t1 = min(t0 + CH, S);
+                const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
+                const int o_hi = min(PL - 1, (t1 - NT) >= 0 ? (t1 - NT) / D : -1);
+                for (int o = o_lo; o <= o_hi; o++) {
+                    const float in = L.fq[c & 1][my_s * MAX_DONE + (o % MAX_DONE)];
+                    const float yh = p.hp[0] * in + p.hp[1] * h1 + p.hp[2] * h2 - p.hp[3] * h1 - p.hp[4] * h2;
+                    h2 = h1;
+                    h1 = yh;
+                    const float yb = p.bp[0] * yh + p.bp[1] * q1 + p.bp[2] * q2 - p.bp[3] * q1 - p.bp[4] * q2;
+                    q2 = q1;
+                    q1 = yb;
+                    const float diff = yb - prev;
+                    prev = yb;
+                    const float boosted = yb + p.transient_coeff * diff;
+                    const float v = clamp_ref(boosted * p.gain, -1.0f, 1.0f);
+                    pcm[(size_t)(s0 + my_s) * PL + o] = (int16_t)(v * 32767.0f);
+                }
+            }
+        } else if (wave < 8) {
+            // ---- FIR accumulation (:136-141) for chunk it-6: lane = (stream, slot group) ----
+            const int c = it - 6;
+            const int hl = tid - 256;
+            const int fs_ = hl % PG, q0 = hl / PG;
+            if (c >= 0 && c < nch && PL > 0) {
+                const int t0 = c * CH, t1 = min(t0 + CH, S);
+                const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
+                const int o_hi = min(PL - 1, (t1 - 1) / D);
+                const float *oin = &L.out[c & 1][fs_ * ROW];
+                for (int slot = q0; slot < n_slots; slot += 8) {
+                    const int o = o_lo + ((slot - (o_lo % n_slots)) + n_slots) % n_slots;
+                    if (o > o_hi) continue;
+                    const int base = D * o;
+                    float acc = (base >= t0) ? 0.0f : L.facc[fs_ * MAX_SLOTS + slot];
+                    const int k0 = max(t0, base) - base, k1 = min(t1, base + NT) - base;
+                    for (int k = k0; k < k1; k++) acc += oin[base + k - t0] * L.taps[k];
+                    if (base + NT <= t1)
+                        L.fq[c & 1][fs_ * MAX_DONE + (o % MAX_DONE)] = acc;
+                    else
+                        L.facc[fs_ * MAX_SLOTS + slot] = acc;
+                }
+            }
+        } else {
+            const int ol = tid - 512;  // [0, 512)
+            // ---- load + unpack the I channel of chunk it ----
+            {
+                const int c = it;
+                if (c < nch && ol < PG * (CH / 8)) {
+                    const int sl = ol / (CH / 8), part = ol % (CH / 8);
+                    const int t = c * CH + part * 8;
+                    float x[8];
+                    if (s0 + sl < n_frames) {
+                        const char *frame = iq + (size_t)(s0 + sl) * p.n_in * bps;
+                        load_i8_masked<FMT>(frame, t, min(p.n_in, S), x);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 8; q++) x[q] = 0.0f;
+                    }
+                    float *dst = &L.re[c & 1][sl * ROW + part * 8];
+                    *reinterpret_cast<float4 *>(dst) = make_float4(x[0], x[1], x[2], x[3]);
+                    *reinterpret_cast<float4 *>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
+                }
+            }
+            // ---- AGC "desired" level (:104-107), chunk it-3 ----
+            {
+                const int c = it - 3;
+                if (c >= 0 && c < nch) {
+#pragma unroll
+                    for (int m = 0; m < 2; m++) {
+                        const int e = ol + 512 * m, sl = e / CH, i = e % CH;
+                        const float y = L.y[c & 3][sl * ROW + i];
+                        const float a = p.upper ? (y + y) : (y - y);  // demodSSB on {y, y}
+                        const float mag = fabsf(a) + 1e-8f;
+                        L.d[c & 1][sl * ROW + i] = p.agc_target / (sqrtf(mag) + 1e-6f);
+                    }
+                }
+            }
+            // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5 ----
+            {
+                const int c = it - 5;
+                if (c >= 0 && c < nch) {
+#pragma unroll
+                    for (int m = 0; m < 2; m++) {
+                        const int e = ol + 512 * m, sl = e / CH, i = e % CH;
+                        const float y = L.y[c & 3][sl * ROW + i];
+                        const float a = p.upper ? (y + y) : (y - y);
+                        L.out[c & 1][sl * ROW + i] = clamp_ref(a * L.g[c & 1][sl * ROW + i], -1.0f, 1.0f);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    if (wave < 3) __builtin_amdgcn_s_setprio(0);
+    if (serial_live) {
+        if (wave == 1) {
+            state[s0 + my_s].lpf_z1 = z1;
+            state[s0 + my_s].lpf_z2 = z2;
+        } else if (wave == 3) {
+            state[s0 + my_s].hp_z1 = h1;
+            state[s0 + my_s].hp_z2 = h2;
+            state[s0 + my_s].bp_z1 = q1;
+            state[s0 + my_s].bp_z2 = q2;
+        }
+    }
+}
+
 }  // namespace
 
-hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
+hipError_t launch_ssb_reference(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       SsbStreamState *state, float *scratch, int16_t *pcm, hipStream_t stream) {
     if (n_frames <= 0) return hipSuccess;
     const dim3 grid((n_frames + WAVE - 1) / WAVE);
@@ -213,6 +489,43 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
     }
     hipLaunchKernelGGL(ssb_eq_kernel, grid, dim3(WAVE), 0, stream, fir_out, n_frames, p, state, pcm);
     return hipGetLastError();
+}
+
+bool ssb_force_reference_kernels() {
+    static const bool force = [] {
+        const char *v = getenv("SDRG_SSB_REFERENCE_KERNELS");
+        return v && v[0] == '1';
+    }();
+    return force;
+}
+
+bool ssb_pipe_supported(const SsbParams &p, int *n_slots) {
+    if (p.pcm_len <= 0) {
+        *n_slots = 1;
+        return true;
+    }
+    const int ns = (CH + p.n_taps - 2) / p.decim + 1;  // outputs whose window can overlap one chunk
+    *n_slots = ns;
+    return ns <= MAX_SLOTS && (CH + p.decim - 1) / p.decim <= MAX_DONE && p.n_taps <= 256;
+}
+
+hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
+                      SsbStreamState *state, float *scratch, int16_t *pcm, hipStream_t stream) {
+    if (n_frames <= 0) return hipSuccess;
+    int n_slots = 1;
+    const char *src = reinterpret_cast<const char *>(iq);
+    if (ssb_pipe_supported(p, &n_slots) && !ssb_force_reference_kernels()) {
+        const dim3 grid((n_frames + PG - 1) / PG);
+        switch (fmt) {
+        case SDRG_IQ_CS8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS8>, grid, dim3(PIPE_T), 0, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
+        case SDRG_IQ_CU8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CU8>, grid, dim3(PIPE_T), 0, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
+        case SDRG_IQ_CS16: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS16>, grid, dim3(PIPE_T), 0, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
+        case SDRG_IQ_CF32: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CF32>, grid, dim3(PIPE_T), 0, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    return launch_ssb_reference(iq, fmt, n_frames, p, taps, state, scratch, pcm, stream);
 }
 
 }  // namespace sdrg

@@ -12,6 +12,15 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "sdr-for-androi
         sys.path.insert(0, p)
 
 
+# torch wheels bundle their own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Whichever loads first is the
+# one every library in the process uses, and torch only works on its own build, so torch is imported before
+# libsdrg.so is loaded; libsdrg.so then runs on that runtime (see DESIGN.md "HIP runtime").
+try:
+    import torch  # noqa: F401
+except Exception:  # the CPU suite does not need torch
+    torch = None
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) and the built HIP library")
 
