@@ -26,6 +26,7 @@ namespace sdrg {
 namespace {
 
 constexpr int WAVE = 64;
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float clamp_ref(float v, float lo, float hi) {  // std::clamp
     return (v < lo) ? lo : (hi < v) ? hi : v;
@@ -200,22 +201,28 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 // recurrence its own wave (lane = stream), keeps ONLY the recurrence arithmetic in it, and moves every
 // order-free operation (unpack, the AGC's sqrt/div "desired" level, the clamp, the FIR) to helper waves.
 // The stages are pipelined over chunks of CH samples through LDS rings with one workgroup barrier per
-// chunk, so while the low-pass wave works on chunk c the DC wave is on c+1, the helpers on c-1 ... c-4:
+// chunk, so while the low-pass wave works on chunk c the DC wave is on c+1 and the helpers on c-1 ... c-4:
 //
-//   it:   load c=it | DC c=it-1 | LPF c=it-2 | DESIRED c=it-3 | AGC c=it-4 | OUT c=it-5 | FIR c=it-6 | EQ c=it-7
+//   it:  load c=it | DC c=it-1 | LPF c=it-2 | DESIRED c=it-3 | AGC c=it-4 | OUT c=it-5 | FIR c=it-6 | EQ c=it-7
 //
 // The FIR accumulates each output's 255 products as its samples arrive (k ascending, exactly the
-// reference's order), so no sample window is kept; completed outputs go to the EQ wave (HP, BP, boost,
-// PCM).  All arithmetic is the reference's, in its order, without contraction: bit-identical PCM.
-// Workgroup = 32 streams x 16 waves; waves 0-3 are the serial roles (one per SIMD), 4-15 helpers.
+// reference's order) in per-(stream, slot) accumulators, so no sample window is kept; completed outputs
+// go to the EQ role (HP, BP, boost, PCM).  All arithmetic is the reference's, in its order, without
+// contraction: bit-identical PCM.
+//
+// Workgroup = 16 streams x 8 waves, one workgroup per CU (LDS padded past half the CU), so the four
+// serial waves (DC, LPF, AGC, EQ+load) own one SIMD each and the helper waves are paired with them by load:
+//   w0 DC  + w4 FIR slots 0-3 | w1 LPF + w5 desired/out | w2 AGC + w6 FIR slots 4-7 | w3 EQ+load + w7 desired/out
 // ================================================================================================
-constexpr int PG = 32;          // streams per workgroup
+constexpr int PG = 16;          // streams per workgroup
 constexpr int CH = 32;          // samples per chunk
-constexpr int ROW = CH + 4;     // padded LDS row (floats): conflict-free ds_read_b128 by stream lanes
-constexpr int BUFF = PG * ROW;  // floats per chunk buffer
-constexpr int PIPE_T = 1024;    // 16 waves
-constexpr int MAX_SLOTS = 16;   // concurrent FIR outputs per stream
+constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_read_b128 by stream lanes
+constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
+constexpr int OT = PG + 1;      // padded sample row of the transposed [sample][stream] FIR input
+constexpr int PIPE_T = 512;     // 8 waves
+constexpr int MAX_SLOTS = 16;   // concurrent FIR outputs per stream (2 per FIR lane)
 constexpr int MAX_DONE = 4;     // FIR outputs completed per stream per chunk
+constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
 
 struct PipeLds {
     float re[2][BUFF];
@@ -223,8 +230,7 @@ struct PipeLds {
     float y[4][BUFF];
     float d[2][BUFF];
     float g[2][BUFF];
-    float out[2][BUFF];
-    float facc[PG * MAX_SLOTS];
+    float outT[2][CH * OT];
     float fq[2][PG * MAX_DONE];
     float taps[256];
 };
@@ -243,6 +249,35 @@ __device__ __forceinline__ void load_i8_masked(const char *frame, int t, int n_i
     }
 }
 
+__device__ __forceinline__ void read_row(const float *row, float (&v)[CH]) {
+#pragma unroll
+    for (int i = 0; i < CH; i += 4) {
+        const float4 r = *reinterpret_cast<const float4 *>(row + i);
+        v[i] = r.x; v[i + 1] = r.y; v[i + 2] = r.z; v[i + 3] = r.w;
+    }
+}
+
+__device__ __forceinline__ void write_row(float *row, const float (&v)[CH]) {
+#pragma unroll
+    for (int i = 0; i < CH; i += 4) *reinterpret_cast<float4 *>(row + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+}
+
+// One FIR slot of one stream over one chunk: the output o of this slot active in [t0, t1), if any.
+__device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int t1, int slot, int n_slots, int sl, int D,
+                                         int NT, int PL, float &acc) {
+    const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
+    const int o_hi = min(PL - 1, (t1 - 1) / D);
+    if (slot >= n_slots) return;
+    const int o = o_lo + ((slot - (o_lo % n_slots)) + n_slots) % n_slots;
+    if (o > o_hi) return;
+    const int base = D * o;
+    if (base >= t0) acc = 0.0f;
+    const int lo = max(t0, base), hi = min(t1, base + NT);
+    const float *in = &L.outT[c & 1][sl];
+    for (int t = lo; t < hi; t++) acc += in[(t - t0) * OT] * L.taps[t - base];
+    if (base + NT <= t1) L.fq[c & 1][sl * MAX_DONE + (o % MAX_DONE)] = acc;
+}
+
 template <int FMT>
 __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
                                                           int n_slots, const float *__restrict__ taps,
@@ -259,13 +294,13 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
 
     for (int i = tid; i < NT; i += PIPE_T) L.taps[i] = taps[i];
 
-    // per-role persistent state (registers)
     const int my_s = lane;  // serial roles: lane = stream within the group
     const bool serial_live = (wave < 4) && (lane < PG) && (s0 + lane < n_frames);
     float dc = 0.0f;                              // removeDC: reset per call (:50)
     float z1 = 0.0f, z2 = 0.0f;                   // rfFilter state, carried across frames
     float gain = 1.0f;                            // adaptiveAGC: reset per call (:102)
     float h1 = 0.0f, h2 = 0.0f, q1 = 0.0f, q2 = 0.0f, prev = 0.0f;  // HP/BP state (carried), boost prev
+    float acc0 = 0.0f, acc1 = 0.0f;               // FIR accumulators (two slots per FIR lane)
     if (serial_live) {
         const SsbStreamState st = state[s0 + my_s];
         z1 = st.lpf_z1; z2 = st.lpf_z2;
@@ -273,87 +308,112 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
     }
     if (wave < 3) __builtin_amdgcn_s_setprio(2);  // the recurrences own their SIMD's issue slots
     const size_t bps = bytes_per_sample<FMT>();
+    const int n_live = min(p.n_in, S);
     __syncthreads();
 
     for (int it = 0; it < nch + 8; ++it) {
         if (wave == 0) {
-            // ---- removeDC (:49-55) + a0 * x of iir2Process, chunk it-1 ----
+            // ---- removeDC (:49-55) and the a0*x term of iir2Process, chunk it-1 ----
             const int c = it - 1;
             if (c >= 0 && c < nch && lane < PG) {
-                const float *re = &L.re[c & 1][my_s * ROW];
-                float *ao = &L.a[c & 1][my_s * ROW];
+                float v[CH];
+                read_row(&L.re[c & 1][my_s * ROW], v);
                 const int lim = min(CH, S - c * CH);
                 const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
-#pragma unroll 2
-                for (int i = 0; i < CH; i += 4) {
-                    const float4 r = *reinterpret_cast<const float4 *>(re + i);
-                    float v[4] = {r.x, r.y, r.z, r.w}, o[4];
+                if (lim == CH) {
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        if (i + q < lim) {
-                            dc = alpha * dc + one_minus * v[q];
-                            o[q] = a0 * (v[q] - dc);
-                        } else {
-                            o[q] = 0.0f;
-                        }
+                    for (int q = 0; q < CH; q++) {
+                        dc = alpha * dc + one_minus * v[q];
+                        v[q] = a0 * (v[q] - dc);
                     }
-                    *reinterpret_cast<float4 *>(ao + i) = make_float4(o[0], o[1], o[2], o[3]);
+                } else {
+                    for (int q = 0; q < lim; q++) {
+                        dc = alpha * dc + one_minus * v[q];
+                        v[q] = a0 * (v[q] - dc);
+                    }
                 }
+                write_row(&L.a[c & 1][my_s * ROW], v);
             }
         } else if (wave == 1) {
             // ---- iir2Process recurrence (:75-84), chunk it-2 ----
             const int c = it - 2;
             if (c >= 0 && c < nch && lane < PG) {
-                const float *ai = &L.a[c & 1][my_s * ROW];
-                float *yo = &L.y[c & 3][my_s * ROW];
+                float v[CH];
+                read_row(&L.a[c & 1][my_s * ROW], v);
                 const int lim = min(CH, S - c * CH);
-                const float a1 = p.lpf[1], a2 = p.lpf[2], b1 = p.lpf[3], b2 = p.lpf[4];
-#pragma unroll 2
-                for (int i = 0; i < CH; i += 4) {
-                    const float4 r = *reinterpret_cast<const float4 *>(ai + i);
-                    float v[4] = {r.x, r.y, r.z, r.w}, o[4];
+                // y = ((((a0 x + a1 z1) + a2 z2) - b1 z1) - b2 z2): the four products as two packed
+                // multiplies (each lane of v_pk_mul_f32 rounds like v_mul_f32), the adds in order
+                const f2v c1 = {p.lpf[1], p.lpf[3]}, c2 = {p.lpf[2], p.lpf[4]};
+                if (lim == CH) {
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        if (i + q < lim) {
-                            const float y = v[q] + a1 * z1 + a2 * z2 - b1 * z1 - b2 * z2;
-                            z2 = z1;
-                            z1 = y;
-                            o[q] = y;
-                        } else {
-                            o[q] = 0.0f;
-                        }
+                    for (int q = 0; q < CH; q++) {
+                        const f2v p1 = c1 * z1, p2 = c2 * z2;
+                        const float y = (((v[q] + p1.x) + p2.x) - p1.y) - p2.y;
+                        z2 = z1;
+                        z1 = y;
+                        v[q] = y;
                     }
-                    *reinterpret_cast<float4 *>(yo + i) = make_float4(o[0], o[1], o[2], o[3]);
+                } else {
+                    for (int q = 0; q < lim; q++) {
+                        const f2v p1 = c1 * z1, p2 = c2 * z2;
+                        const float y = (((v[q] + p1.x) + p2.x) - p1.y) - p2.y;
+                        z2 = z1;
+                        z1 = y;
+                        v[q] = y;
+                    }
                 }
+                write_row(&L.y[c & 3][my_s * ROW], v);
             }
         } else if (wave == 2) {
             // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
             const int c = it - 4;
             if (c >= 0 && c < nch && lane < PG) {
-                const float *di = &L.d[c & 1][my_s * ROW];
-                float *go = &L.g[c & 1][my_s * ROW];
+                float v[CH];
+                read_row(&L.d[c & 1][my_s * ROW], v);
                 const int lim = min(CH, S - c * CH);
-                const float fast = p.agc_fast, slow = 0.00035f;
-                const float omf = 1.0f - fast, oms = 1.0f - slow;
-#pragma unroll 2
-                for (int i = 0; i < CH; i += 4) {
-                    const float4 r = *reinterpret_cast<const float4 *>(di + i);
-                    float v[4] = {r.x, r.y, r.z, r.w}, o[4];
+                // gain = gain*(1-rate) + desired*rate, rate = desired < gain ? fast : slow: both candidates
+                // (fast, slow) in one packed lane pair, then the select
+                const f2v rates = {p.agc_fast, 0.00035f};
+                const f2v keep = {1.0f - p.agc_fast, 1.0f - 0.00035f};
+                if (lim == CH) {
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        if (i + q < lim) {
-                            const float desired = v[q];
-                            const float gf = gain * omf + desired * fast;
-                            const float gs = gain * oms + desired * slow;
-                            gain = (desired < gain) ? gf : gs;
-                        }
-                        o[q] = gain;
+                    for (int q = 0; q < CH; q++) {
+                        const float desired = v[q];
+                        const f2v cand = gain * keep + desired * rates;
+                        gain = (desired < gain) ? cand.x : cand.y;
+                        v[q] = gain;
                     }
-                    *reinterpret_cast<float4 *>(go + i) = make_float4(o[0], o[1], o[2], o[3]);
+                } else {
+                    for (int q = 0; q < lim; q++) {
+                        const float desired = v[q];
+                        const f2v cand = gain * keep + desired * rates;
+                        gain = (desired < gain) ? cand.x : cand.y;
+                        v[q] = gain;
+                    }
                 }
+                write_row(&L.g[c & 1][my_s * ROW], v);
             }
         } else if (wave == 3) {
-            // ---- HP -> BP -> transientBoost -> floatToPCM on outputs the FIR completed, chunk it-7 ----
+            // ---- load + unpack the I channel of chunk it (lane = 4 x stream + part of 8 samples) ----
+            {
+                const int c = it;
+                if (c < nch) {
+                    const int sl = lane >> 2, part = lane & 3;
+                    const int t = c * CH + part * 8;
+                    float x[8];
+                    if (s0 + sl < n_frames) {
+                        const char *frame = iq + (size_t)(s0 + sl) * p.n_in * bps;
+                        load_i8_masked<FMT>(frame, t, n_live, x);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 8; q++) x[q] = 0.0f;
+                    }
+                    float *dst = &L.re[c & 1][sl * ROW + part * 8];
+                    *reinterpret_cast<float4 *>(dst) = make_float4(x[0], x[1], x[2], x[3]);
+                    *reinterpret_cast<float4 *>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
+                }
+            }
+            // ---- HP -> BP -> transientBoost -> floatToPCM on the outputs the FIR completed, chunk it-7 ----
             const int c = it - 7;
             if (c >= 0 && c < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
                 const int t0 = c * CH, t1 = min(t0 + CH, S);
@@ -374,57 +434,26 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                     pcm[(size_t)(s0 + my_s) * PL + o] = (int16_t)(v * 32767.0f);
                 }
             }
-        } else if (wave < 8) {
-            // ---- FIR accumulation (:136-141) for chunk it-6: lane = (stream, slot group) ----
+        } else if (wave == 4 || wave == 6) {
+            // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot, stream) ----
             const int c = it - 6;
-            const int hl = tid - 256;
-            const int fs_ = hl % PG, q0 = hl / PG;
             if (c >= 0 && c < nch && PL > 0) {
                 const int t0 = c * CH, t1 = min(t0 + CH, S);
-                const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
-                const int o_hi = min(PL - 1, (t1 - 1) / D);
-                const float *oin = &L.out[c & 1][fs_ * ROW];
-                for (int slot = q0; slot < n_slots; slot += 8) {
-                    const int o = o_lo + ((slot - (o_lo % n_slots)) + n_slots) % n_slots;
-                    if (o > o_hi) continue;
-                    const int base = D * o;
-                    float acc = (base >= t0) ? 0.0f : L.facc[fs_ * MAX_SLOTS + slot];
-                    const int k0 = max(t0, base) - base, k1 = min(t1, base + NT) - base;
-                    for (int k = k0; k < k1; k++) acc += oin[base + k - t0] * L.taps[k];
-                    if (base + NT <= t1)
-                        L.fq[c & 1][fs_ * MAX_DONE + (o % MAX_DONE)] = acc;
-                    else
-                        L.facc[fs_ * MAX_SLOTS + slot] = acc;
-                }
+                const int sl = lane % PG;
+                const int slot = (wave == 4 ? 0 : 4) + lane / PG;  // 0-3 or 4-7
+                fir_slot(L, c, t0, t1, slot, n_slots, sl, D, NT, PL, acc0);
+                fir_slot(L, c, t0, t1, slot + 8, n_slots, sl, D, NT, PL, acc1);
             }
         } else {
-            const int ol = tid - 512;  // [0, 512)
-            // ---- load + unpack the I channel of chunk it ----
-            {
-                const int c = it;
-                if (c < nch && ol < PG * (CH / 8)) {
-                    const int sl = ol / (CH / 8), part = ol % (CH / 8);
-                    const int t = c * CH + part * 8;
-                    float x[8];
-                    if (s0 + sl < n_frames) {
-                        const char *frame = iq + (size_t)(s0 + sl) * p.n_in * bps;
-                        load_i8_masked<FMT>(frame, t, min(p.n_in, S), x);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 8; q++) x[q] = 0.0f;
-                    }
-                    float *dst = &L.re[c & 1][sl * ROW + part * 8];
-                    *reinterpret_cast<float4 *>(dst) = make_float4(x[0], x[1], x[2], x[3]);
-                    *reinterpret_cast<float4 *>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
-                }
-            }
+            // waves 5 and 7: 128 lanes, 4 elements each of the 16 x 32 chunk
+            const int hl = (wave == 5 ? 0 : 64) + lane;
             // ---- AGC "desired" level (:104-107), chunk it-3 ----
             {
                 const int c = it - 3;
                 if (c >= 0 && c < nch) {
 #pragma unroll
-                    for (int m = 0; m < 2; m++) {
-                        const int e = ol + 512 * m, sl = e / CH, i = e % CH;
+                    for (int m = 0; m < 4; m++) {
+                        const int e = hl + 128 * m, sl = e / CH, i = e % CH;
                         const float y = L.y[c & 3][sl * ROW + i];
                         const float a = p.upper ? (y + y) : (y - y);  // demodSSB on {y, y}
                         const float mag = fabsf(a) + 1e-8f;
@@ -432,16 +461,16 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                     }
                 }
             }
-            // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5 ----
+            // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5, stored [sample][stream] ----
             {
                 const int c = it - 5;
                 if (c >= 0 && c < nch) {
 #pragma unroll
-                    for (int m = 0; m < 2; m++) {
-                        const int e = ol + 512 * m, sl = e / CH, i = e % CH;
+                    for (int m = 0; m < 4; m++) {
+                        const int e = hl + 128 * m, sl = e / CH, i = e % CH;
                         const float y = L.y[c & 3][sl * ROW + i];
                         const float a = p.upper ? (y + y) : (y - y);
-                        L.out[c & 1][sl * ROW + i] = clamp_ref(a * L.g[c & 1][sl * ROW + i], -1.0f, 1.0f);
+                        L.outT[c & 1][i * OT + sl] = clamp_ref(a * L.g[c & 1][sl * ROW + i], -1.0f, 1.0f);
                     }
                 }
             }
@@ -516,11 +545,12 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
     const char *src = reinterpret_cast<const char *>(iq);
     if (ssb_pipe_supported(p, &n_slots) && !ssb_force_reference_kernels()) {
         const dim3 grid((n_frames + PG - 1) / PG);
+        const size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
         switch (fmt) {
-        case SDRG_IQ_CS8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS8>, grid, dim3(PIPE_T), 0, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
-        case SDRG_IQ_CU8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CU8>, grid, dim3(PIPE_T), 0, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
-        case SDRG_IQ_CS16: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS16>, grid, dim3(PIPE_T), 0, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
-        case SDRG_IQ_CF32: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CF32>, grid, dim3(PIPE_T), 0, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
+        case SDRG_IQ_CS8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS8>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
+        case SDRG_IQ_CU8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CU8>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
+        case SDRG_IQ_CS16: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS16>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
+        case SDRG_IQ_CF32: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CF32>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
