@@ -155,6 +155,13 @@ StatsGeometry stats_geometry(uint32_t sample_rate, uint32_t center_frequency, in
     int pool = 0;
     for (int i = 0; i < n_bottom && i < nr; i++) pool += lens[i];
     g.max_pool = pool;
+    int slo = g.focus_lo, shi = g.focus_hi;
+    for (int i = 0; i < nr; i++) {
+        slo = g.win_lo[i] < slo ? g.win_lo[i] : slo;
+        shi = g.win_hi[i] > shi ? g.win_hi[i] : shi;
+    }
+    g.span_lo = slo;
+    g.span_len = g.focus_len > 0 ? shi - slo + 1 : 0;
     g.freq_per_bin = freq_per_bin;
     g.nyquist = nyquist;
     g.cf_float = static_cast<float>(center_frequency);

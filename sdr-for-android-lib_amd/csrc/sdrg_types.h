@@ -38,6 +38,7 @@ struct StatsGeometry {
     int32_t n_ref;             // reference windows collected (<= 10)
     int32_t win_lo[10], win_hi[10];
     int32_t max_pool;          // upper bound of pooled bins (sizes the LDS pool)
+    int32_t span_lo, span_len; // bins [span_lo, span_lo + span_len) cover the focus and every window
     float freq_per_bin, nyquist;
     float cf_minus_nyq;        // static_cast<float>(centerFrequency) - nyquist   (:327)
     float cf_u32_minus_nyq;    // (centerFrequency - nyquist), uint32 promoted to float (:350)

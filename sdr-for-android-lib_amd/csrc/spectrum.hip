@@ -4,11 +4,13 @@
 // fftwf_plan_dft_1d(N, FORWARD, ESTIMATE) + execute (unnormalised, no window), power = re^2 + im^2,
 // fftshift.  The unused 10-frame ring buffer (:62-73) has no observable output and is not kept.
 //
-// Design (gfx950): Stockham autosort FFT with radix-32 register butterflies, the frame resident in LDS
-// between passes (N = 16384: 3 passes = 32 * 32 * 16, two LDS exchanges).  Each thread owns E = 32
-// complex values (T = N/32 threads, 512 at N = 16384).  Pass 0 reads the raw int8/uint8/int16/float
-// samples straight from HBM (coalesced across lanes) and converts them in registers; the last pass
-// writes |X|^2 straight to HBM at the fftshifted index (coalesced).  Complex arithmetic is written on
+// Design (gfx950): Stockham autosort FFT with radix-32 register butterflies (N = 16384: 3 passes =
+// 32 * 32 * 16, two exchanges).  Each thread owns E = 32 complex values (T = N/32 threads, 512 at
+// N = 16384).  Between passes the values move through an LDS buffer of HALF the frame (66 KiB) in two
+// phases, so two frames' workgroups fit a CU beside the SSB pipeline's workgroup.  Pass 0 reads the raw
+// int8/uint8/int16/float samples straight from HBM (coalesced across lanes) and converts them in
+// registers; the last pass writes |X|^2 straight to HBM at the fftshifted index (coalesced).  Twiddles
+// come from two small factored tables (L1-resident).  Complex arithmetic is written on
 // 2-wide float vectors so it maps onto v_pk_{add,mul,fma}_f32.  HBM traffic = bytes in + 4 B out per
 // sample (6 B/sample for CS8), the algorithmic minimum.
 #include "sdrg_internal.h"
@@ -104,85 +106,131 @@ constexpr int bytes_per_sample() {
     return FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2;
 }
 
-// One Stockham pass: radix R, Ns = product of the previous radices.
-//   j in [0, N/R): k = j mod Ns; x[r] = A[j + r N/R] * w^(r k), w = exp(-2 pi i/(Ns R)); X = DFT_R(x);
-//   B[(j/Ns) Ns R + k + r Ns] = X[r]
-template <int LOG2N, int R, int NS, bool FIRST, bool LAST, int FMT>
-__device__ __forceinline__ void stockham_pass(f2 *lds, const void *frame, float *out, const f2 *__restrict__ tw) {
-    constexpr int N = 1 << LOG2N;
-    constexpr int T = N / E;
-    constexpr int NB = E / R;  // butterflies per thread in this pass
-    const int t = threadIdx.x;
-    f2 x[NB][R];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int j = t + b * T;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int e = j + r * (N / R);
-            if constexpr (FIRST)
-                x[b][r] = load_sample<FMT>(frame, e);
-            else
-                x[b][r] = lds[lds_idx(e)];
-        }
-    }
-    if constexpr (!FIRST) __syncthreads();  // every read of this pass done before anyone overwrites
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int j = t + b * T;
-        if constexpr (NS > 1) {
-            const int k = j & (NS - 1);
-#pragma unroll
-            for (int r = 1; r < R; ++r) x[b][r] = cmul(x[b][r], tw[(r * k) * (N / (NS * R))]);
-        }
-        dft<R>(x[b]);
-        if constexpr (LAST) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int o = j + r * (N / R);
-                const f2 v = x[b][r];
-                out[(o + N / 2) & (N - 1)] = v.x * v.x + v.y * v.y;
-            }
-        } else {
-            const int base = (j / NS) * NS * R + (j & (NS - 1));
-#pragma unroll
-            for (int r = 0; r < R; ++r) lds[lds_idx(base + r * NS)] = x[b][r];
-        }
-    }
-    if constexpr (!LAST) __syncthreads();
+// Twiddle W_N^m from the compact factored tables: W_N^m = W_N^(64 (m >> 6)) * W_N^(m & 63).
+// hi: N/64 entries W_N^(64 i); lo: 64 entries W_N^i.  Both stay in L1 (2.5 KB at N = 16384).
+__device__ __forceinline__ f2 twiddle_n(const f2 *__restrict__ hi, const f2 *__restrict__ lo, int m) {
+    return cmul(hi[m >> 6], lo[m & 63]);
 }
 
 template <int LOG2N>
 struct Plan {
     static constexpr int N = 1 << LOG2N;
     static constexpr int T = N / E;
-    static constexpr int NP = (LOG2N + 4) / 5;                   // passes
+    static constexpr int NP = (LOG2N + 4) / 5;  // passes: radix 32 ..., last = remainder
     static constexpr int RLAST = (LOG2N % 5 == 0) ? 32 : (1 << (LOG2N % 5));
-    static constexpr int LDS_BYTES = (N + N / 32) * 8;
+    static constexpr int HALF = N / 2;
+    static constexpr int LDS_BYTES = (HALF + HALF / 32) * 8;  // half the frame + pad (66 KiB at 16384)
+    template <int P>
+    static constexpr int radix() { return P == NP - 1 ? RLAST : 32; }
 };
 
-template <int LOG2N, int P, int NS, int FMT>
-__device__ __forceinline__ void run_passes(f2 *lds, const void *frame, float *out, const f2 *tw) {
+// Stockham pass P (radix R, NS = product of the previous radices) on the E values a thread holds as
+// v[b*R + r] for butterflies j = t + b*T:
+//   x[r] = A[j + r N/R] * w^(r k), k = j mod NS, w = exp(-2 pi i/(NS R));  X = DFT_R(x);
+//   B[(j/NS) NS R + k + r NS] = X[r]
+template <int LOG2N, int R, int NS>
+__device__ __forceinline__ void pass_compute(f2 (&v)[E], const f2 *__restrict__ thi, const f2 *__restrict__ tlo) {
+    constexpr int N = 1 << LOG2N;
+    constexpr int T = N / E;
+    constexpr int NB = E / R;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int j = threadIdx.x + b * T;
+        f2 x[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = v[b * R + r];
+        if constexpr (NS > 1) {
+            const int k = j & (NS - 1);
+#pragma unroll
+            for (int r = 1; r < R; ++r) x[r] = cmul(x[r], twiddle_n(thi, tlo, (r * k) * (N / (NS * R))));
+        }
+        dft<R>(x);
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[b * R + r] = x[r];
+    }
+}
+
+// Exchange pass P's outputs (radix R, NS) into pass P+1's inputs (radix R2) through an LDS buffer that
+// holds HALF the frame: phase h moves the outputs whose position lies in half h.  A reader's element
+// e = j' + r' N/R2 is in half 0 iff r' < R2/2 (compile-time), so every phase reads exactly half of each
+// thread's next inputs; a writer's outputs all fall in one half when NB = 1, so in phase 0 the waves of
+// the lower half of the threads empty their registers while the upper half still hold theirs (48 live
+// complex values at most).
+template <int LOG2N, int R, int NS, int R2>
+__device__ __forceinline__ void exchange(f2 *lds, f2 (&v)[E]) {
+    constexpr int N = 1 << LOG2N;
+    constexpr int T = N / E;
+    constexpr int NB = E / R, NB2 = E / R2;
+    constexpr int HALF = N / 2;
+    f2 nxt[E];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int j = threadIdx.x + b * T;
+            const int base = (j / NS) * NS * R + (j & (NS - 1));
+            if ((base >= HALF) == (h == 1)) {  // all R outputs of a butterfly share the half (NS R <= HALF)
+#pragma unroll
+                for (int r = 0; r < R; ++r) lds[lds_idx(base + r * NS - h * HALF)] = v[b * R + r];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int b = 0; b < NB2; ++b) {
+            const int j = threadIdx.x + b * T;
+#pragma unroll
+            for (int r = h * (R2 / 2); r < (h + 1) * (R2 / 2); ++r) nxt[b * R2 + r] = lds[lds_idx(j + r * (N / R2) - h * HALF)];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = nxt[i];
+}
+
+template <int LOG2N, int P, int NS>
+__device__ __forceinline__ void run_passes(f2 *lds, f2 (&v)[E], float *out, const f2 *thi, const f2 *tlo) {
     using PL = Plan<LOG2N>;
-    if constexpr (P < PL::NP) {
-        constexpr bool LAST = (P == PL::NP - 1);
-        constexpr int R = LAST ? PL::RLAST : 32;
-        stockham_pass<LOG2N, R, NS, P == 0, LAST, FMT>(lds, frame, out, tw);
-        run_passes<LOG2N, P + 1, NS * R, FMT>(lds, frame, out, tw);
+    constexpr int N = 1 << LOG2N;
+    constexpr int R = PL::template radix<P>();
+    pass_compute<LOG2N, R, NS>(v, thi, tlo);
+    if constexpr (P == PL::NP - 1) {
+        // last pass: output positions j + r N/R; |X|^2 at the fftshifted index (fft_process.cpp:83-97)
+        constexpr int T = N / E, NB = E / R;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int j = threadIdx.x + b * T;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const f2 x = v[b * R + r];
+                out[(j + r * (N / R) + N / 2) & (N - 1)] = x.x * x.x + x.y * x.y;
+            }
+        }
+    } else {
+        constexpr int R2 = PL::template radix<P + 1>();
+        exchange<LOG2N, R, NS, R2>(lds, v);
+        run_passes<LOG2N, P + 1, NS * R>(lds, v, out, thi, tlo);
     }
 }
 
 template <int LOG2N, int FMT>
-__global__ __launch_bounds__(Plan<LOG2N>::T) void spectrum_kernel(const void *__restrict__ iq,
-                                                                  float *__restrict__ spectra,
-                                                                  const f2 *__restrict__ tw) {
+__global__ __launch_bounds__(Plan<LOG2N>::T, 2) void spectrum_kernel(const void *__restrict__ iq,
+                                                                     float *__restrict__ spectra,
+                                                                     const f2 *__restrict__ thi,
+                                                                     const f2 *__restrict__ tlo) {
     using PL = Plan<LOG2N>;
+    constexpr int N = PL::N, T = PL::T, R0 = PL::template radix<0>(), NB0 = E / R0;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     f2 *lds = reinterpret_cast<f2 *>(smem);
     const size_t frame = blockIdx.x;
-    const void *src = reinterpret_cast<const char *>(iq) + frame * (size_t)PL::N * bytes_per_sample<FMT>();
-    float *dst = spectra + frame * (size_t)PL::N;
-    run_passes<LOG2N, 0, 1, FMT>(lds, src, dst, tw);
+    const void *src = reinterpret_cast<const char *>(iq) + frame * (size_t)N * bytes_per_sample<FMT>();
+    f2 v[E];
+#pragma unroll
+    for (int b = 0; b < NB0; ++b) {
+        const int j = threadIdx.x + b * T;
+#pragma unroll
+        for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_sample<FMT>(src, j + r * (N / R0));
+    }
+    run_passes<LOG2N, 0, 1>(lds, v, spectra + frame * (size_t)N, thi, tlo);
 }
 
 template <int LOG2N, int FMT>
@@ -196,8 +244,10 @@ hipError_t launch_t(const void *iq, int n_frames, const float *tw, float *spectr
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(k, dim3(n_frames), dim3(PL::T), PL::LDS_BYTES, s, iq, spectra,
-                       reinterpret_cast<const f2 *>(tw));
+    const f2 *base = reinterpret_cast<const f2 *>(tw);
+    const f2 *thi = base + PL::N;                 // compact tables follow the full table (engine layout)
+    const f2 *tlo = thi + PL::N / 64;
+    hipLaunchKernelGGL(k, dim3(n_frames), dim3(PL::T), PL::LDS_BYTES, s, iq, spectra, thi, tlo);
     return hipGetLastError();
 }
 

@@ -66,6 +66,37 @@ __device__ __forceinline__ void load_i8(const char *frame, int n, float (&x)[8])
     }
 }
 
+// I parts of 8 consecutive samples held in raw form in u[] (1, 2 or 4 uint4 by format).
+template <int FMT>
+__device__ __forceinline__ void unpack_i8(const uint4 *u, float (&x)[8]) {
+    if constexpr (FMT == SDRG_IQ_CS8 || FMT == SDRG_IQ_CU8) {
+        const uint32_t w[4] = {u[0].x, u[0].y, u[0].z, u[0].w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if constexpr (FMT == SDRG_IQ_CS8) {
+                x[2 * q] = (float)(int8_t)(w[q] & 0xff) * (1.0f / 128.0f);
+                x[2 * q + 1] = (float)(int8_t)((w[q] >> 16) & 0xff) * (1.0f / 128.0f);
+            } else {
+                x[2 * q] = ((float)(w[q] & 0xff) - 127.4f) * (1.0f / 128.0f);
+                x[2 * q + 1] = ((float)((w[q] >> 16) & 0xff) - 127.4f) * (1.0f / 128.0f);
+            }
+        }
+    } else if constexpr (FMT == SDRG_IQ_CS16) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t w[4] = {u[h].x, u[h].y, u[h].z, u[h].w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) x[4 * h + q] = (float)(int16_t)(w[q] & 0xffff) * (1.0f / 32768.0f);
+        }
+    } else {
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            x[2 * h] = __uint_as_float(u[h].x);
+            x[2 * h + 1] = __uint_as_float(u[h].z);
+        }
+    }
+}
+
 template <int FMT>
 __device__ __forceinline__ float load_i1(const char *frame, int n) {
     if constexpr (FMT == SDRG_IQ_CS8) return (float)(int8_t)frame[2 * (size_t)n] * (1.0f / 128.0f);
@@ -224,7 +255,15 @@ constexpr int MAX_SLOTS = 16;   // concurrent FIR outputs per stream (2 per FIR 
 constexpr int MAX_DONE = 4;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
 
+constexpr int RAW_U4 = PG * 32;  // one prefetch batch: 512 B per stream = 32 uint4
+
+template <int FMT>
+constexpr int batch_chunks() {  // chunks per 512-B-per-stream prefetch batch
+    return FMT == SDRG_IQ_CF32 ? 2 : FMT == SDRG_IQ_CS16 ? 4 : 8;
+}
+
 struct PipeLds {
+    uint4 raw[2][RAW_U4];  // raw IQ bytes of two prefetch batches, [stream][512 B]
     float re[2][BUFF];
     float a[2][BUFF];
     float y[4][BUFF];
@@ -263,19 +302,36 @@ __device__ __forceinline__ void write_row(float *row, const float (&v)[CH]) {
 }
 
 // One FIR slot of one stream over one chunk: the output o of this slot active in [t0, t1), if any.
+// Every lane runs the same fully unrolled 32-step body (all LDS reads issued first), the steps outside
+// its window [lo, hi) being masked by a select, so the four slots a wave holds do not diverge.
 __device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int t1, int slot, int n_slots, int sl, int D,
                                          int NT, int PL, float &acc) {
     const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
     const int o_hi = min(PL - 1, (t1 - 1) / D);
-    if (slot >= n_slots) return;
     const int o = o_lo + ((slot - (o_lo % n_slots)) + n_slots) % n_slots;
-    if (o > o_hi) return;
+    const bool active = slot < n_slots && o <= o_hi;
     const int base = D * o;
-    if (base >= t0) acc = 0.0f;
-    const int lo = max(t0, base), hi = min(t1, base + NT);
+    if (active && base >= t0) acc = 0.0f;
+    const int lo = active ? max(t0, base) : t1, hi = active ? min(t1, base + NT) : t1;
     const float *in = &L.outT[c & 1][sl];
-    for (int t = lo; t < hi; t++) acc += in[(t - t0) * OT] * L.taps[t - base];
-    if (base + NT <= t1) L.fq[c & 1][sl * MAX_DONE + (o % MAX_DONE)] = acc;
+    constexpr int HB = CH / 2;  // two batches of 16 keep the register footprint of the reads small
+#pragma unroll
+    for (int h = 0; h < CH; h += HB) {
+        float xv[HB], hv[HB];
+#pragma unroll
+        for (int i = 0; i < HB; i++) {
+            const int k = min(max(t0 + h + i - base, 0), NT - 1);
+            xv[i] = in[(h + i) * OT];
+            hv[i] = L.taps[k];
+        }
+#pragma unroll
+        for (int i = 0; i < HB; i++) {
+            const float prod = xv[i] * hv[i];
+            const bool in_win = (unsigned)(t0 + h + i - lo) < (unsigned)(hi - lo);
+            acc = in_win ? acc + prod : acc;
+        }
+    }
+    if (active && base + NT <= t1) L.fq[c & 1][sl * MAX_DONE + (o % MAX_DONE)] = acc;
 }
 
 template <int FMT>
@@ -309,6 +365,40 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
     if (wave < 3) __builtin_amdgcn_s_setprio(2);  // the recurrences own their SIMD's issue slots
     const size_t bps = bytes_per_sample<FMT>();
     const int n_live = min(p.n_in, S);
+
+    // raw-IQ prefetch state of the loader wave (wave 3): lane = 4 x stream + quarter of the stream's 512 B
+    constexpr int BC = batch_chunks<FMT>();
+    constexpr int SPU = 16 / (int)bytes_per_sample<FMT>();  // samples per uint4
+    uint4 pf[8];
+    const int ld_s = lane >> 2, ld_q = lane & 3;
+    const char *ld_frame = iq + (size_t)(s0 + ld_s) * p.n_in * bps;
+    const bool ld_live = (s0 + ld_s < n_frames);
+    const bool ld_aligned = (reinterpret_cast<uintptr_t>(ld_frame) & 15) == 0;
+    auto issue_batch = [&](int kb) {
+        const int t_a = kb * BC * CH + ld_q * 8 * SPU;  // this lane's 128 B start at sample t_a
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int tq = t_a + q * SPU;
+            if (ld_live && ld_aligned && tq + SPU <= n_live) {
+                pf[q] = *reinterpret_cast<const uint4 *>(ld_frame + (size_t)tq * bps);
+            } else {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (int b = 0; b < 16; b++)
+                    if (ld_live && tq + b / (int)bps < n_live)
+                        w[b >> 2] |= (uint32_t)(uint8_t)ld_frame[(size_t)tq * bps + b] << (8 * (b & 3));
+                pf[q] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+    };
+    auto store_batch = [&](int kb) {
+        uint4 *dst = &L.raw[kb & 1][ld_s * 32 + ld_q * 8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) dst[q] = pf[q];
+    };
+    if (wave == 3) {
+        issue_batch(0);
+        store_batch(0);
+    }
     __syncthreads();
 
     for (int it = 0; it < nch + 8; ++it) {
@@ -394,20 +484,26 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                 write_row(&L.g[c & 1][my_s * ROW], v);
             }
         } else if (wave == 3) {
-            // ---- load + unpack the I channel of chunk it (lane = 4 x stream + part of 8 samples) ----
+            // ---- raw IQ prefetch: batch kb (chunks [kb*BC, kb*BC+BC)) is issued BC iterations before its
+            //      first chunk is converted and parked in LDS at the end of the previous batch ----
+            if (it % BC == 0 && (it / BC + 1) * BC < nch) issue_batch(it / BC + 1);
+            if (it % BC == BC - 1 && (it / BC + 1) * BC < nch) store_batch(it / BC + 1);
+            // ---- unpack the I channel of chunk it from the parked raw bytes (lane = 4 x stream + part) ----
             {
                 const int c = it;
                 if (c < nch) {
                     const int sl = lane >> 2, part = lane & 3;
                     const int t = c * CH + part * 8;
-                    float x[8];
-                    if (s0 + sl < n_frames) {
-                        const char *frame = iq + (size_t)(s0 + sl) * p.n_in * bps;
-                        load_i8_masked<FMT>(frame, t, n_live, x);
-                    } else {
+                    constexpr int U4 = 8 * (int)bytes_per_sample<FMT>() / 16;  // uint4 per 8 samples
+                    const uint4 *src = &L.raw[(c / BC) & 1][sl * 32 + ((c % BC) * CH + part * 8) * (int)bytes_per_sample<FMT>() / 16];
+                    uint4 u[U4];
 #pragma unroll
-                        for (int q = 0; q < 8; q++) x[q] = 0.0f;
-                    }
+                    for (int q = 0; q < U4; q++) u[q] = src[q];
+                    float x[8];
+                    unpack_i8<FMT>(u, x);
+#pragma unroll
+                    for (int q = 0; q < 8; q++)
+                        if (t + q >= n_live || s0 + sl >= n_frames) x[q] = 0.0f;  // iq.resize() zero padding
                     float *dst = &L.re[c & 1][sl * ROW + part * 8];
                     *reinterpret_cast<float4 *>(dst) = make_float4(x[0], x[1], x[2], x[3]);
                     *reinterpret_cast<float4 *>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);

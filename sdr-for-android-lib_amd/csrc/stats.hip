@@ -19,6 +19,7 @@ namespace sdrg {
 namespace {
 
 constexpr int WAVE = 64;
+constexpr int STAGE_MAX = 8192;  // bins staged into LDS for the window scans (32 KiB)
 constexpr int MAX_POOL = 16384;  // pooled-bin bound: N/4 at N = 65536 (the widest nBottom case, see engine.cpp)
 
 __device__ __forceinline__ float db_of(float p) { return 10.0f * log10f(p / 1.0f + 1e-20f); }  // refPower = 1
@@ -29,10 +30,11 @@ struct WinScan {
     int best_start;  // first start maximising the raw running sum (focus scan, :311-320)
 };
 
-// One lane replays the reference's sequential loops over P[lo..hi].
-__device__ WinScan scan_window(const float *__restrict__ P, int lo, int hi, int w) {
+// One lane replays the reference's sequential loops over P[lo..hi] (P: staged LDS copy or HBM).
+__device__ __forceinline__ WinScan scan_window(const float *__restrict__ P, int lo, int hi, int w) {
     WinScan r;
     float s = 0.0f;
+#pragma unroll 8
     for (int i = lo; i <= hi; i++) s += P[i];
     r.sum = s;
     const int len = hi - lo + 1;
@@ -43,8 +45,10 @@ __device__ WinScan scan_window(const float *__restrict__ P, int lo, int hi, int 
         r.best1k = s / len;
     } else {
         float rs = 0.0f;
+#pragma unroll 8
         for (int i = lo; i < lo + w; i++) rs += P[i];
         float best = rs / w, bv = rs;
+#pragma unroll 4
         for (int st = lo + 1; st + w - 1 <= hi; st++) {
             rs += P[st + w - 1] - P[st - 1];
             const float m = rs / w;
@@ -95,7 +99,9 @@ __device__ float kth_smallest(const float *vals, int cnt, int k, int *hist, int 
 __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ spectra, StatsGeometry g,
                                                      int64_t now_ms, StatsState *__restrict__ state,
                                                      sdrg_frame_record *__restrict__ records) {
-    extern __shared__ __attribute__((aligned(16))) float pool[];  // [g.max_pool] pooled dB / gaps
+    extern __shared__ __attribute__((aligned(16))) float dyn[];  // [max_pool] pooled dB / gaps, then [span] staged bins
+    float *pool = dyn;
+    float *stage = dyn + ((g.max_pool + 3) & ~3);
     __shared__ int hist[256];
     __shared__ int sh_int[2];
     __shared__ int sh_nbottom, sh_best_start;
@@ -141,11 +147,18 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
         //      takes the focus window; all of them run the same sequential scan in lockstep ----
         const int w1k = g.win_bins_1k;
         const int n_ref = g.n_ref;
+        // stage the bins every window touches into LDS (coalesced) when they fit, so the sequential
+        // per-lane scans below read LDS instead of waiting on HBM for every element
+        const bool staged = g.span_len > 0 && g.span_len <= STAGE_MAX;
+        if (staged) {
+            for (int i = lane; i < g.span_len; i += WAVE) stage[i] = P[g.span_lo + i];
+            __syncthreads();
+        }
         if (lane <= n_ref) {
             const bool is_focus = (lane == n_ref);
             const int lo = is_focus ? g.focus_lo : g.win_lo[lane];
             const int hi = is_focus ? g.focus_hi : g.win_hi[lane];
-            const WinScan ws = scan_window(P, lo, hi, w1k);
+            const WinScan ws = staged ? scan_window(stage - g.span_lo, lo, hi, w1k) : scan_window(P, lo, hi, w1k);
             const int n = hi - lo + 1;
             if (is_focus) {
                 sh_f[0] = db_of(ws.sum / n);  // signalPowerDb (:155)
@@ -336,11 +349,12 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
                         StatsState *state, sdrg_frame_record *records, hipStream_t stream) {
     if (n_frames <= 0) return hipSuccess;
     if (geo.max_pool > MAX_POOL) return hipErrorInvalidValue;
-    const size_t lds = sizeof(float) * (size_t)(geo.max_pool > 0 ? geo.max_pool : 1);
+    const int staged = (geo.span_len > 0 && geo.span_len <= STAGE_MAX) ? geo.span_len : 0;
+    const size_t lds = sizeof(float) * (size_t)(((geo.max_pool + 3) & ~3) + staged + 4);
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(stats_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, MAX_POOL * 4);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (MAX_POOL + STAGE_MAX + 8) * 4);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
