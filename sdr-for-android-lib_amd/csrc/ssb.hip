@@ -274,6 +274,14 @@ struct PipeLds {
     float taps[256];
 };
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup release/acquire, which makes
+// every wave drain ALL its outstanding memory operations (s_waitcnt vmcnt(0)) first - the loader's
+// raw-IQ prefetch would then complete every chunk instead of several chunks ahead, and the pipeline
+// would pay an HBM round trip per chunk.  Nothing global is exchanged between waves inside the loop.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ int ceil_div_i(int a, int b) {  // b > 0, any sign of a
     return a >= 0 ? (a + b - 1) / b : -((-a) / b);
 }
@@ -571,7 +579,7 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
 
     if (wave < 3) __builtin_amdgcn_s_setprio(0);

@@ -151,6 +151,7 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
         // per-lane scans below read LDS instead of waiting on HBM for every element
         const bool staged = g.span_len > 0 && g.span_len <= STAGE_MAX;
         if (staged) {
+#pragma unroll 16
             for (int i = lane; i < g.span_len; i += WAVE) stage[i] = P[g.span_lo + i];
             __syncthreads();
         }
