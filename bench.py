@@ -96,6 +96,8 @@ def main() -> int:
     ap.add_argument("--streams", type=int, default=B)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--stages", default="all", choices=["all", "spectrum", "spectrum+stats", "ssb"],
+                    help="ablation only: the metric is defined on 'all'")
     args = ap.parse_args()
 
     import torch
@@ -124,8 +126,11 @@ def main() -> int:
 
     now = [1000]
 
+    stages = {"all": sdrg.STAGE_ALL, "spectrum": sdrg.STAGE_SPECTRUM, "ssb": sdrg.STAGE_SSB,
+              "spectrum+stats": sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS}[args.stages]
+
     def step():
-        eng.process_device(iq.data_ptr(), sdrg.CS8, sdrg.STAGE_ALL, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(),
+        eng.process_device(iq.data_ptr(), sdrg.CS8, stages, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(),
                            now[0])
         now[0] += 8  # 16384 samples @ 2 Msps = 8.192 ms per frame
         if world > 1:
@@ -185,7 +190,9 @@ def main() -> int:
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "alg_bytes_per_launch": alg_bytes},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.stages != "all":
+        out["ablation_stages"] = args.stages
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.stages == "all":
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
         except Exception as exc:  # the baseline is informative; never fail the bench line on it

@@ -14,6 +14,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -551,6 +552,11 @@ int32_t sdrg_engine_process_device(sdrg_engine *e, const void *iq, int32_t forma
 int32_t sdrg_engine_synchronize(sdrg_engine *e) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     HIP_TRY(hipStreamSynchronize(e->s_main));
+    static const bool stamps = [] {
+        const char *v = getenv("SDRG_PIPE_STAMPS");
+        return v && v[0] == '1';
+    }();
+    if (stamps) ssb_report_stamps();
     return SDRG_OK;
 }
 

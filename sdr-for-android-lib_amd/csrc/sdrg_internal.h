@@ -28,6 +28,7 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
 // sample rates below ~0.9 MHz, or when SDRG_SSB_REFERENCE_KERNELS=1) need
 // scratch: [n_frames][samp_count + pcm_len] floats.  taps: [n_taps] device floats.
 bool ssb_force_reference_kernels();
+void ssb_report_stamps();  // diagnostic (SDRG_PIPE_STAMPS=1)
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       SsbStreamState *state, float *scratch, int16_t *pcm, hipStream_t stream);
 

@@ -16,7 +16,10 @@
 //   ssb_fir_kernel   : block = 64 outputs of one stream; input window staged in LDS; each output is the
 //                      reference's sequential 255-term sum
 //   ssb_eq_kernel    : lane = stream; HP -> BP -> boost -> PCM over the decimated frame
+#include <stdio.h>
 #include <stdlib.h>
+
+#include <vector>
 
 #include "sdrg_internal.h"
 
@@ -346,7 +349,8 @@ template <int FMT>
 __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
                                                           int n_slots, const float *__restrict__ taps,
                                                           SsbStreamState *__restrict__ state,
-                                                          int16_t *__restrict__ pcm) {
+                                                          int16_t *__restrict__ pcm,
+                                                          unsigned long long *__restrict__ stamps) {
     __shared__ PipeLds L;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -409,7 +413,9 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
     }
     __syncthreads();
 
+    unsigned long long st_work = 0, st_t0 = stamps ? __builtin_amdgcn_s_memtime() : 0, st_a = st_t0;
     for (int it = 0; it < nch + 8; ++it) {
+        if (stamps) st_a = __builtin_amdgcn_s_memtime();
         if (wave == 0) {
             // ---- removeDC (:49-55) and the a0*x term of iir2Process, chunk it-1 ----
             const int c = it - 1;
@@ -579,7 +585,15 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                 }
             }
         }
+        if (stamps) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            st_work += __builtin_amdgcn_s_memtime() - st_a;
+        }
         lds_barrier();
+    }
+    if (stamps && lane == 0) {  // diagnostic build only: per-wave work cycles and loop cycles
+        stamps[(blockIdx.x * 8 + wave) * 2] = st_work;
+        stamps[(blockIdx.x * 8 + wave) * 2 + 1] = __builtin_amdgcn_s_memtime() - st_t0;
     }
 
     if (wave < 3) __builtin_amdgcn_s_setprio(0);
@@ -632,6 +646,42 @@ bool ssb_force_reference_kernels() {
     return force;
 }
 
+// Diagnostic: SDRG_PIPE_STAMPS=1 makes the pipeline record per-wave work/loop cycles (s_memtime) and
+// ssb_report_stamps() print them per role.  Off by default (stamps == nullptr: no instruction executes).
+static unsigned long long *g_stamps = nullptr;
+static int g_stamps_groups = 0;
+unsigned long long *ssb_stamps_buffer(int n_frames) {
+    static const bool on = [] {
+        const char *v = getenv("SDRG_PIPE_STAMPS");
+        return v && v[0] == '1';
+    }();
+    if (!on) return nullptr;
+    const int groups = (n_frames + PG - 1) / PG;
+    if (groups > g_stamps_groups) {
+        if (g_stamps) (void)hipFree(g_stamps);
+        if (hipMalloc(reinterpret_cast<void **>(&g_stamps), sizeof(unsigned long long) * groups * 16) != hipSuccess)
+            return nullptr;
+        g_stamps_groups = groups;
+    }
+    return g_stamps;
+}
+
+void ssb_report_stamps() {
+    if (!g_stamps) return;
+    std::vector<unsigned long long> h((size_t)g_stamps_groups * 16);
+    if (hipMemcpy(h.data(), g_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    const char *names[8] = {"DC", "LPF", "AGC", "LOAD+EQ", "FIR-A", "DES/OUT-A", "FIR-B", "DES/OUT-B"};
+    for (int w = 0; w < 8; w++) {
+        double work = 0, loop = 0;
+        for (int g = 0; g < g_stamps_groups; g++) {
+            work += h[(g * 8 + w) * 2];
+            loop += h[(g * 8 + w) * 2 + 1];
+        }
+        fprintf(stderr, "[sdrg stamps] wave %d %-10s work %12.0f cyc  loop %12.0f cyc  (mean over %d groups)\n", w,
+                names[w], work / g_stamps_groups, loop / g_stamps_groups, g_stamps_groups);
+    }
+}
+
 bool ssb_pipe_supported(const SsbParams &p, int *n_slots) {
     if (p.pcm_len <= 0) {
         *n_slots = 1;
@@ -651,10 +701,10 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         const dim3 grid((n_frames + PG - 1) / PG);
         const size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
         switch (fmt) {
-        case SDRG_IQ_CS8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS8>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
-        case SDRG_IQ_CU8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CU8>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
-        case SDRG_IQ_CS16: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS16>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
-        case SDRG_IQ_CF32: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CF32>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm); break;
+        case SDRG_IQ_CS8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS8>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm, ssb_stamps_buffer(n_frames)); break;
+        case SDRG_IQ_CU8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CU8>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm, ssb_stamps_buffer(n_frames)); break;
+        case SDRG_IQ_CS16: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS16>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm, ssb_stamps_buffer(n_frames)); break;
+        case SDRG_IQ_CF32: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CF32>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm, ssb_stamps_buffer(n_frames)); break;
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
