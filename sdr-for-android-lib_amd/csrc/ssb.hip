@@ -245,8 +245,8 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 // contraction: bit-identical PCM.
 //
 // Workgroup = 16 streams x 8 waves, one workgroup per CU (LDS padded past half the CU), so the four
-// serial waves (DC, LPF, AGC, EQ+load) own one SIMD each and the helper waves are paired with them by load:
-//   w0 DC  + w4 FIR slots 0-3 | w1 LPF + w5 desired/out | w2 AGC + w6 FIR slots 4-7 | w3 EQ+load + w7 desired/out
+// serial waves (DC, LPF, AGC, EQ+load) own one SIMD each and the helper waves are paired with them:
+//   w0 DC + w4 FIR+EQ | w1 LPF + w5 desired/out | w2 AGC + w6 desired/out | w3 load (LDS-DMA) + w7 desired/out
 // ================================================================================================
 constexpr int PG = 16;          // streams per workgroup
 constexpr int CH = 32;          // samples per chunk
@@ -258,7 +258,7 @@ constexpr int MAX_SLOTS = 16;   // concurrent FIR outputs per stream (2 per FIR 
 constexpr int MAX_DONE = 4;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
 
-constexpr int RAW_U4 = PG * 32;  // one prefetch batch: 512 B per stream = 32 uint4
+constexpr int RAW_U4 = PG * 32;  // one prefetch batch: 512 B per stream = 32 uint4, as [piece 8][lane 64]
 
 template <int FMT>
 constexpr int batch_chunks() {  // chunks per 512-B-per-stream prefetch batch
@@ -266,7 +266,7 @@ constexpr int batch_chunks() {  // chunks per 512-B-per-stream prefetch batch
 }
 
 struct PipeLds {
-    uint4 raw[2][RAW_U4];  // raw IQ bytes of two prefetch batches, [stream][512 B]
+    uint4 raw[2][RAW_U4];  // raw IQ bytes of two prefetch batches (LDS-DMA), [piece][loader lane]
     float re[2][BUFF];
     float a[2][BUFF];
     float y[4][BUFF];
@@ -274,7 +274,7 @@ struct PipeLds {
     float g[2][BUFF];
     float outT[2][CH * OT];
     float fq[2][PG * MAX_DONE];
-    float taps[256];
+    float taps_pad[CH + 256 + CH];  // [CH zeros][taps][zeros]: out-of-window FIR steps multiply by 0
 };
 
 // Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup release/acquire, which makes
@@ -313,8 +313,10 @@ __device__ __forceinline__ void write_row(float *row, const float (&v)[CH]) {
 }
 
 // One FIR slot of one stream over one chunk: the output o of this slot active in [t0, t1), if any.
-// Every lane runs the same fully unrolled 32-step body (all LDS reads issued first), the steps outside
-// its window [lo, hi) being masked by a select, so the four slots a wave holds do not diverge.
+// Every lane runs the same fully unrolled 32-step body with all LDS reads issued first.  Steps outside the
+// output's window read a zero tap from the padding around the taps, and acc + (+-0) == acc exactly here:
+// acc starts at +0 and a round-to-nearest sum never produces -0 from +0, so the masked steps leave the
+// reference's sequential sum unchanged.
 __device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int t1, int slot, int n_slots, int sl, int D,
                                          int NT, int PL, float &acc) {
     const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
@@ -323,29 +325,26 @@ __device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int t1, int 
     const bool active = slot < n_slots && o <= o_hi;
     const int base = D * o;
     if (active && base >= t0) acc = 0.0f;
-    const int lo = active ? max(t0, base) : t1, hi = active ? min(t1, base + NT) : t1;
+    // tap index of step i: t0 + i - base, shifted into taps_pad; inactive lanes read the zero padding
+    const int k0 = active ? (t0 - base + CH) : 0;
+    const float *tp = &L.taps_pad[k0];
     const float *in = &L.outT[c & 1][sl];
-    constexpr int HB = CH / 2;  // two batches of 16 keep the register footprint of the reads small
+    const int lim = t1 - t0;  // < CH only in a partial last chunk
 #pragma unroll
-    for (int h = 0; h < CH; h += HB) {
-        float xv[HB], hv[HB];
+    for (int h = 0; h < CH; h += 16) {
+        float xv[16], hv[16];
 #pragma unroll
-        for (int i = 0; i < HB; i++) {
-            const int k = min(max(t0 + h + i - base, 0), NT - 1);
+        for (int i = 0; i < 16; i++) {
             xv[i] = in[(h + i) * OT];
-            hv[i] = L.taps[k];
+            hv[i] = (h + i < lim) ? tp[h + i] : 0.0f;
         }
 #pragma unroll
-        for (int i = 0; i < HB; i++) {
-            const float prod = xv[i] * hv[i];
-            const bool in_win = (unsigned)(t0 + h + i - lo) < (unsigned)(hi - lo);
-            acc = in_win ? acc + prod : acc;
-        }
+        for (int i = 0; i < 16; i++) acc += xv[i] * hv[i];
     }
     if (active && base + NT <= t1) L.fq[c & 1][sl * MAX_DONE + (o % MAX_DONE)] = acc;
 }
 
-template <int FMT>
+template <int FMT, bool DMA>
 __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
                                                           int n_slots, const float *__restrict__ taps,
                                                           SsbStreamState *__restrict__ state,
@@ -360,15 +359,18 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
     const int nch = (S + CH - 1) / CH;
     const int D = p.decim, NT = p.n_taps, PL = p.pcm_len;
 
-    for (int i = tid; i < NT; i += PIPE_T) L.taps[i] = taps[i];
+    for (int i = tid; i < CH + 256 + CH; i += PIPE_T) {
+        const int k = i - CH;
+        L.taps_pad[i] = (k >= 0 && k < NT) ? taps[k] : 0.0f;
+    }
 
     const int my_s = lane;  // serial roles: lane = stream within the group
-    const bool serial_live = (wave < 4) && (lane < PG) && (s0 + lane < n_frames);
+    const bool serial_live = (wave < 3 || wave == 4) && (lane < PG) && (s0 + lane < n_frames);
     float dc = 0.0f;                              // removeDC: reset per call (:50)
     float z1 = 0.0f, z2 = 0.0f;                   // rfFilter state, carried across frames
     float gain = 1.0f;                            // adaptiveAGC: reset per call (:102)
     float h1 = 0.0f, h2 = 0.0f, q1 = 0.0f, q2 = 0.0f, prev = 0.0f;  // HP/BP state (carried), boost prev
-    float acc0 = 0.0f, acc1 = 0.0f;               // FIR accumulators (two slots per FIR lane)
+    float facc[MAX_SLOTS / 4] = {0.0f, 0.0f, 0.0f, 0.0f};  // FIR accumulators (slots j*4 + lane/16)
     if (serial_live) {
         const SsbStreamState st = state[s0 + my_s];
         z1 = st.lpf_z1; z2 = st.lpf_z2;
@@ -378,38 +380,25 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
     const size_t bps = bytes_per_sample<FMT>();
     const int n_live = min(p.n_in, S);
 
-    // raw-IQ prefetch state of the loader wave (wave 3): lane = 4 x stream + quarter of the stream's 512 B
+    // raw-IQ prefetch of the loader wave (wave 3): batch kb = chunks [kb*BC, kb*BC+BC) = 512 B per stream,
+    // moved by LDS-DMA (global_load_lds, no registers) BC iterations before its first chunk is unpacked.
+    // Lane = 4 x stream + quarter of the stream's 512 B; 8 DMA pieces of 16 B per lane.
     constexpr int BC = batch_chunks<FMT>();
-    constexpr int SPU = 16 / (int)bytes_per_sample<FMT>();  // samples per uint4
-    uint4 pf[8];
+    constexpr int SPU = 16 / (int)bytes_per_sample<FMT>();  // samples per 16 B
     const int ld_s = lane >> 2, ld_q = lane & 3;
-    const char *ld_frame = iq + (size_t)(s0 + ld_s) * p.n_in * bps;
     const bool ld_live = (s0 + ld_s < n_frames);
-    const bool ld_aligned = (reinterpret_cast<uintptr_t>(ld_frame) & 15) == 0;
+    const char *ld_frame = iq + (size_t)(ld_live ? s0 + ld_s : s0) * p.n_in * bps;
+    const int n_batches = (n_live + BC * CH - 1) / (BC * CH);
     auto issue_batch = [&](int kb) {
-        const int t_a = kb * BC * CH + ld_q * 8 * SPU;  // this lane's 128 B start at sample t_a
+        const char *src = ld_frame + (size_t)(kb * BC * CH + ld_q * 8 * SPU) * bps;
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int tq = t_a + q * SPU;
-            if (ld_live && ld_aligned && tq + SPU <= n_live) {
-                pf[q] = *reinterpret_cast<const uint4 *>(ld_frame + (size_t)tq * bps);
-            } else {
-                uint32_t w[4] = {0, 0, 0, 0};
-                for (int b = 0; b < 16; b++)
-                    if (ld_live && tq + b / (int)bps < n_live)
-                        w[b >> 2] |= (uint32_t)(uint8_t)ld_frame[(size_t)tq * bps + b] << (8 * (b & 3));
-                pf[q] = make_uint4(w[0], w[1], w[2], w[3]);
-            }
-        }
+        for (int q = 0; q < 8; q++)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + 16 * q),
+                                             (__attribute__((address_space(3))) void *)&L.raw[kb & 1][q * 64], 16, 0, 0);
     };
-    auto store_batch = [&](int kb) {
-        uint4 *dst = &L.raw[kb & 1][ld_s * 32 + ld_q * 8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) dst[q] = pf[q];
-    };
-    if (wave == 3) {
-        issue_batch(0);
-        store_batch(0);
+    if constexpr (DMA) {
+        if (wave == 3 && n_batches > 0) issue_batch(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 
@@ -498,23 +487,33 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                 write_row(&L.g[c & 1][my_s * ROW], v);
             }
         } else if (wave == 3) {
-            // ---- raw IQ prefetch: batch kb (chunks [kb*BC, kb*BC+BC)) is issued BC iterations before its
-            //      first chunk is converted and parked in LDS at the end of the previous batch ----
-            if (it % BC == 0 && (it / BC + 1) * BC < nch) issue_batch(it / BC + 1);
-            if (it % BC == BC - 1 && (it / BC + 1) * BC < nch) store_batch(it / BC + 1);
-            // ---- unpack the I channel of chunk it from the parked raw bytes (lane = 4 x stream + part) ----
+            if constexpr (DMA) {
+                // batch it/BC + 1 starts moving now; it must have landed before the barrier that ends
+                // the batch's last-but-one iteration (only this wave's DMAs are counted by its vmcnt)
+                if (it % BC == 0 && it / BC + 1 < n_batches) issue_batch(it / BC + 1);
+                if (it % BC == BC - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            // ---- unpack the I channel of chunk it (lane = 4 x stream + part of 8 samples) ----
             {
                 const int c = it;
                 if (c < nch) {
                     const int sl = lane >> 2, part = lane & 3;
                     const int t = c * CH + part * 8;
-                    constexpr int U4 = 8 * (int)bytes_per_sample<FMT>() / 16;  // uint4 per 8 samples
-                    const uint4 *src = &L.raw[(c / BC) & 1][sl * 32 + ((c % BC) * CH + part * 8) * (int)bytes_per_sample<FMT>() / 16];
-                    uint4 u[U4];
-#pragma unroll
-                    for (int q = 0; q < U4; q++) u[q] = src[q];
                     float x[8];
-                    unpack_i8<FMT>(u, x);
+                    if constexpr (DMA) {
+                        constexpr int U4 = 8 * (int)bytes_per_sample<FMT>() / 16;  // 16-B pieces per 8 samples
+                        const int off = ((c % BC) * CH + part * 8) * (int)bytes_per_sample<FMT>();
+                        const int quarter = off >> 7, piece = (off & 127) >> 4;
+                        uint4 u[U4];
+#pragma unroll
+                        for (int q = 0; q < U4; q++) u[q] = L.raw[(c / BC) & 1][(piece + q) * 64 + sl * 4 + quarter];
+                        unpack_i8<FMT>(u, x);
+                    } else {
+                        if (s0 + sl < n_frames) {
+                            const char *frame = iq + (size_t)(s0 + sl) * p.n_in * bps;
+                            load_i8_masked<FMT>(frame, t, n_live, x);
+                        }
+                    }
 #pragma unroll
                     for (int q = 0; q < 8; q++)
                         if (t + q >= n_live || s0 + sl >= n_frames) x[q] = 0.0f;  // iq.resize() zero padding
@@ -523,9 +522,21 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                     *reinterpret_cast<float4 *>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
                 }
             }
+        } else if (wave == 4) {
+            // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot mod 4, stream), 4 slots per pass ----
+            const int c = it - 6;
+            if (c >= 0 && c < nch && PL > 0) {
+                const int t0 = c * CH, t1 = min(t0 + CH, S);
+                const int sl = lane % PG, sub = lane / PG;
+#pragma unroll
+                for (int j = 0; j < MAX_SLOTS / 4; j++) {
+                    if (j * 4 < n_slots) fir_slot(L, c, t0, t1, j * 4 + sub, n_slots, sl, D, NT, PL, facc[j]);
+                }
+            }
             // ---- HP -> BP -> transientBoost -> floatToPCM on the outputs the FIR completed, chunk it-7 ----
-            const int c = it - 7;
-            if (c >= 0 && c < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
+            const int ce = it - 7;
+            if (ce >= 0 && ce < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
+                const int c = ce;
                 const int t0 = c * CH, t1 = min(t0 + CH, S);
                 const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
                 const int o_hi = min(PL - 1, (t1 - NT) >= 0 ? (t1 - NT) / D : -1);
@@ -544,30 +555,22 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                     pcm[(size_t)(s0 + my_s) * PL + o] = (int16_t)(v * 32767.0f);
                 }
             }
-        } else if (wave == 4 || wave == 6) {
-            // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot, stream) ----
-            const int c = it - 6;
-            if (c >= 0 && c < nch && PL > 0) {
-                const int t0 = c * CH, t1 = min(t0 + CH, S);
-                const int sl = lane % PG;
-                const int slot = (wave == 4 ? 0 : 4) + lane / PG;  // 0-3 or 4-7
-                fir_slot(L, c, t0, t1, slot, n_slots, sl, D, NT, PL, acc0);
-                fir_slot(L, c, t0, t1, slot + 8, n_slots, sl, D, NT, PL, acc1);
-            }
         } else {
-            // waves 5 and 7: 128 lanes, 4 elements each of the 16 x 32 chunk
-            const int hl = (wave == 5 ? 0 : 64) + lane;
+            // waves 5-7: 192 lanes over the 16 x 32 chunk elements
+            const int hl = (wave - 5) * 64 + lane;
             // ---- AGC "desired" level (:104-107), chunk it-3 ----
             {
                 const int c = it - 3;
                 if (c >= 0 && c < nch) {
 #pragma unroll
-                    for (int m = 0; m < 4; m++) {
-                        const int e = hl + 128 * m, sl = e / CH, i = e % CH;
-                        const float y = L.y[c & 3][sl * ROW + i];
-                        const float a = p.upper ? (y + y) : (y - y);  // demodSSB on {y, y}
-                        const float mag = fabsf(a) + 1e-8f;
-                        L.d[c & 1][sl * ROW + i] = p.agc_target / (sqrtf(mag) + 1e-6f);
+                    for (int m = 0; m < 3; m++) {
+                        const int e = hl + 192 * m, sl = e / CH, i = e % CH;
+                        if (e < PG * CH) {
+                            const float y = L.y[c & 3][sl * ROW + i];
+                            const float a = p.upper ? (y + y) : (y - y);  // demodSSB on {y, y}
+                            const float mag = fabsf(a) + 1e-8f;
+                            L.d[c & 1][sl * ROW + i] = p.agc_target / (sqrtf(mag) + 1e-6f);
+                        }
                     }
                 }
             }
@@ -576,11 +579,13 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                 const int c = it - 5;
                 if (c >= 0 && c < nch) {
 #pragma unroll
-                    for (int m = 0; m < 4; m++) {
-                        const int e = hl + 128 * m, sl = e / CH, i = e % CH;
-                        const float y = L.y[c & 3][sl * ROW + i];
-                        const float a = p.upper ? (y + y) : (y - y);
-                        L.outT[c & 1][i * OT + sl] = clamp_ref(a * L.g[c & 1][sl * ROW + i], -1.0f, 1.0f);
+                    for (int m = 0; m < 3; m++) {
+                        const int e = hl + 192 * m, sl = e / CH, i = e % CH;
+                        if (e < PG * CH) {
+                            const float y = L.y[c & 3][sl * ROW + i];
+                            const float a = p.upper ? (y + y) : (y - y);
+                            L.outT[c & 1][i * OT + sl] = clamp_ref(a * L.g[c & 1][sl * ROW + i], -1.0f, 1.0f);
+                        }
                     }
                 }
             }
@@ -601,7 +606,7 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
         if (wave == 1) {
             state[s0 + my_s].lpf_z1 = z1;
             state[s0 + my_s].lpf_z2 = z2;
-        } else if (wave == 3) {
+        } else if (wave == 4) {
             state[s0 + my_s].hp_z1 = h1;
             state[s0 + my_s].hp_z2 = h2;
             state[s0 + my_s].bp_z1 = q1;
@@ -670,7 +675,7 @@ void ssb_report_stamps() {
     if (!g_stamps) return;
     std::vector<unsigned long long> h((size_t)g_stamps_groups * 16);
     if (hipMemcpy(h.data(), g_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const char *names[8] = {"DC", "LPF", "AGC", "LOAD+EQ", "FIR-A", "DES/OUT-A", "FIR-B", "DES/OUT-B"};
+    const char *names[8] = {"DC", "LPF", "AGC", "LOAD", "FIR+EQ", "DES/OUT-0", "DES/OUT-1", "DES/OUT-2"};
     for (int w = 0; w < 8; w++) {
         double work = 0, loop = 0;
         for (int g = 0; g < g_stamps_groups; g++) {
@@ -700,11 +705,26 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
     if (ssb_pipe_supported(p, &n_slots) && !ssb_force_reference_kernels()) {
         const dim3 grid((n_frames + PG - 1) / PG);
         const size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
+        const int bps = fmt == SDRG_IQ_CF32 ? 8 : fmt == SDRG_IQ_CS16 ? 4 : 2;
+        const int bc = fmt == SDRG_IQ_CF32 ? 2 : fmt == SDRG_IQ_CS16 ? 4 : 8;
+        const int n_live = p.n_in < p.samp_count ? p.n_in : p.samp_count;
+        // LDS-DMA batches need whole 16-B pieces inside every frame
+        const bool dma = (n_live % (bc * CH)) == 0 && ((size_t)p.n_in * bps) % 16 == 0 &&
+                         (reinterpret_cast<uintptr_t>(iq) & 15) == 0;
+        unsigned long long *stamps = ssb_stamps_buffer(n_frames);
+#define SDRG_PIPE_LAUNCH(F)                                                                                      \
+    if (dma)                                                                                                     \
+        hipLaunchKernelGGL((ssb_pipe_kernel<F, true>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, \
+                           taps, state, pcm, stamps);                                                           \
+    else                                                                                                         \
+        hipLaunchKernelGGL((ssb_pipe_kernel<F, false>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, \
+                           taps, state, pcm, stamps);
         switch (fmt) {
-        case SDRG_IQ_CS8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS8>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm, ssb_stamps_buffer(n_frames)); break;
-        case SDRG_IQ_CU8: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CU8>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm, ssb_stamps_buffer(n_frames)); break;
-        case SDRG_IQ_CS16: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CS16>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm, ssb_stamps_buffer(n_frames)); break;
-        case SDRG_IQ_CF32: hipLaunchKernelGGL(ssb_pipe_kernel<SDRG_IQ_CF32>, grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, taps, state, pcm, ssb_stamps_buffer(n_frames)); break;
+        case SDRG_IQ_CS8: SDRG_PIPE_LAUNCH(SDRG_IQ_CS8); break;
+        case SDRG_IQ_CU8: SDRG_PIPE_LAUNCH(SDRG_IQ_CU8); break;
+        case SDRG_IQ_CS16: SDRG_PIPE_LAUNCH(SDRG_IQ_CS16); break;
+        case SDRG_IQ_CF32: SDRG_PIPE_LAUNCH(SDRG_IQ_CF32); break;
+#undef SDRG_PIPE_LAUNCH
         default: return hipErrorInvalidValue;
         }
         return hipGetLastError();
