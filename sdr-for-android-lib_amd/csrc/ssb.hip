@@ -328,15 +328,14 @@ __device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int t1, int 
     // tap index of step i: t0 + i - base, shifted into taps_pad; inactive lanes read the zero padding
     const int k0 = active ? (t0 - base + CH) : 0;
     const float *tp = &L.taps_pad[k0];
-    const float *in = &L.outT[c & 1][sl];
-    const int lim = t1 - t0;  // < CH only in a partial last chunk
+    const float *in = &L.outT[c & 1][sl];  // zero beyond the frame end (written so by the OUT role)
 #pragma unroll
     for (int h = 0; h < CH; h += 16) {
         float xv[16], hv[16];
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
+        for (int i = 0; i < 16; i++) {  // unconditional reads: a per-element select would branch per read
             xv[i] = in[(h + i) * OT];
-            hv[i] = (h + i < lim) ? tp[h + i] : 0.0f;
+            hv[i] = tp[h + i];
         }
 #pragma unroll
         for (int i = 0; i < 16; i++) acc += xv[i] * hv[i];
@@ -584,7 +583,8 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                         if (e < PG * CH) {
                             const float y = L.y[c & 3][sl * ROW + i];
                             const float a = p.upper ? (y + y) : (y - y);
-                            L.outT[c & 1][i * OT + sl] = clamp_ref(a * L.g[c & 1][sl * ROW + i], -1.0f, 1.0f);
+                            const float o = clamp_ref(a * L.g[c & 1][sl * ROW + i], -1.0f, 1.0f);
+                            L.outT[c & 1][i * OT + sl] = (c * CH + i < S) ? o : 0.0f;  // FIR reads whole chunks
                         }
                     }
                 }
