@@ -246,18 +246,18 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 //
 // Workgroup = 16 streams x 8 waves, one workgroup per CU (LDS padded past half the CU), so the four
 // serial waves (DC, LPF, AGC, EQ+load) own one SIMD each and the helper waves are paired with them:
-//   w0 DC + w4 FIR+EQ | w1 LPF + w5 desired/out | w2 AGC + w6 desired/out | w3 load (LDS-DMA) + w7 desired/out
+//   w0 DC + w4 FIR | w1 LPF + w5 desired/out | w2 AGC + w6 desired/out | w3 load (LDS-DMA) + w7 EQ
 // ================================================================================================
 constexpr int PG = 16;          // streams per workgroup
 constexpr int CH = 32;          // samples per chunk
 constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_read_b128 by stream lanes
 constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
-constexpr int OT = PG + 1;      // padded sample row of the transposed [sample][stream] FIR input
 constexpr int PIPE_T = 512;     // 8 waves
 constexpr int MAX_SLOTS = 16;   // concurrent FIR outputs per stream (2 per FIR lane)
 constexpr int MAX_DONE = 4;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
 
+constexpr int TAPS_ROW = CH + 256 + CH + 4;
 constexpr int RAW_U4 = PG * 32;  // one prefetch batch: 512 B per stream = 32 uint4, as [piece 8][lane 64]
 
 template <int FMT>
@@ -272,9 +272,11 @@ struct PipeLds {
     float y[4][BUFF];
     float d[2][BUFF];
     float g[2][BUFF];
-    float outT[2][CH * OT];
+    float out[2][BUFF];
     float fq[2][PG * MAX_DONE];
-    float taps_pad[CH + 256 + CH];  // [CH zeros][taps][zeros]: out-of-window FIR steps multiply by 0
+    // taps with CH zeros on both sides (out-of-window FIR steps multiply by 0), in 4 copies shifted by
+    // 0..3 floats so that any 32-tap window is read with aligned ds_read_b128
+    float taps_sh[4][TAPS_ROW];
 };
 
 // Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup release/acquire, which makes
@@ -313,10 +315,10 @@ __device__ __forceinline__ void write_row(float *row, const float (&v)[CH]) {
 }
 
 // One FIR slot of one stream over one chunk: the output o of this slot active in [t0, t1), if any.
-// Every lane runs the same fully unrolled 32-step body with all LDS reads issued first.  Steps outside the
-// output's window read a zero tap from the padding around the taps, and acc + (+-0) == acc exactly here:
-// acc starts at +0 and a round-to-nearest sum never produces -0 from +0, so the masked steps leave the
-// reference's sequential sum unchanged.
+// The lane reads its stream's 32 chunk values and the 32 taps that meet them with 8 + 8 ds_read_b128,
+// then accumulates in the reference's k order.  Steps outside the output's window meet a zero tap from
+// the padding, and acc + (+-0) == acc exactly here: acc starts at +0 and a round-to-nearest sum never
+// produces -0 from +0, so the masked steps leave the reference's sequential sum unchanged.
 __device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int t1, int slot, int n_slots, int sl, int D,
                                          int NT, int PL, float &acc) {
     const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
@@ -325,20 +327,22 @@ __device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int t1, int 
     const bool active = slot < n_slots && o <= o_hi;
     const int base = D * o;
     if (active && base >= t0) acc = 0.0f;
-    // tap index of step i: t0 + i - base, shifted into taps_pad; inactive lanes read the zero padding
+    // taps_pad index of step 0: t0 - base + CH (inactive lanes read the zero padding at 0)
     const int k0 = active ? (t0 - base + CH) : 0;
-    const float *tp = &L.taps_pad[k0];
-    const float *in = &L.outT[c & 1][sl];  // zero beyond the frame end (written so by the OUT role)
+    const float4 *tp = reinterpret_cast<const float4 *>(&L.taps_sh[k0 & 3][k0 & ~3]);
+    const float4 *in = reinterpret_cast<const float4 *>(&L.out[c & 1][sl * ROW]);  // 0 beyond frame end
+    float4 xv[CH / 4], hv[CH / 4];
 #pragma unroll
-    for (int h = 0; h < CH; h += 16) {
-        float xv[16], hv[16];
+    for (int i = 0; i < CH / 4; i++) {
+        xv[i] = in[i];
+        hv[i] = tp[i];
+    }
 #pragma unroll
-        for (int i = 0; i < 16; i++) {  // unconditional reads: a per-element select would branch per read
-            xv[i] = in[(h + i) * OT];
-            hv[i] = tp[h + i];
-        }
-#pragma unroll
-        for (int i = 0; i < 16; i++) acc += xv[i] * hv[i];
+    for (int i = 0; i < CH / 4; i++) {
+        acc += xv[i].x * hv[i].x;
+        acc += xv[i].y * hv[i].y;
+        acc += xv[i].z * hv[i].z;
+        acc += xv[i].w * hv[i].w;
     }
     if (active && base + NT <= t1) L.fq[c & 1][sl * MAX_DONE + (o % MAX_DONE)] = acc;
 }
@@ -358,13 +362,14 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
     const int nch = (S + CH - 1) / CH;
     const int D = p.decim, NT = p.n_taps, PL = p.pcm_len;
 
-    for (int i = tid; i < CH + 256 + CH; i += PIPE_T) {
-        const int k = i - CH;
-        L.taps_pad[i] = (k >= 0 && k < NT) ? taps[k] : 0.0f;
+    for (int i = tid; i < 4 * TAPS_ROW; i += PIPE_T) {
+        const int sh = i / TAPS_ROW, j = i % TAPS_ROW;
+        const int k = j + sh - CH;  // copy sh holds taps_pad[j + sh] at index j
+        L.taps_sh[sh][j] = (k >= 0 && k < NT) ? taps[k] : 0.0f;
     }
 
     const int my_s = lane;  // serial roles: lane = stream within the group
-    const bool serial_live = (wave < 3 || wave == 4) && (lane < PG) && (s0 + lane < n_frames);
+    const bool serial_live = (wave < 3 || wave == 7) && (lane < PG) && (s0 + lane < n_frames);
     float dc = 0.0f;                              // removeDC: reset per call (:50)
     float z1 = 0.0f, z2 = 0.0f;                   // rfFilter state, carried across frames
     float gain = 1.0f;                            // adaptiveAGC: reset per call (:102)
@@ -532,6 +537,7 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                     if (j * 4 < n_slots) fir_slot(L, c, t0, t1, j * 4 + sub, n_slots, sl, D, NT, PL, facc[j]);
                 }
             }
+        } else if (wave == 7) {
             // ---- HP -> BP -> transientBoost -> floatToPCM on the outputs the FIR completed, chunk it-7 ----
             const int ce = it - 7;
             if (ce >= 0 && ce < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
@@ -555,38 +561,40 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                 }
             }
         } else {
-            // waves 5-7: 192 lanes over the 16 x 32 chunk elements
+            // waves 5 and 6: lane = 4 consecutive samples of one stream (128 lanes x 4 = the 16 x 32 chunk)
             const int hl = (wave - 5) * 64 + lane;
+            const int sl = hl / (CH / 4), i4 = (hl % (CH / 4)) * 4;
             // ---- AGC "desired" level (:104-107), chunk it-3 ----
             {
                 const int c = it - 3;
                 if (c >= 0 && c < nch) {
+                    const float4 y4 = *reinterpret_cast<const float4 *>(&L.y[c & 3][sl * ROW + i4]);
+                    const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
+                    float dv[4];
 #pragma unroll
-                    for (int m = 0; m < 3; m++) {
-                        const int e = hl + 192 * m, sl = e / CH, i = e % CH;
-                        if (e < PG * CH) {
-                            const float y = L.y[c & 3][sl * ROW + i];
-                            const float a = p.upper ? (y + y) : (y - y);  // demodSSB on {y, y}
-                            const float mag = fabsf(a) + 1e-8f;
-                            L.d[c & 1][sl * ROW + i] = p.agc_target / (sqrtf(mag) + 1e-6f);
-                        }
+                    for (int q = 0; q < 4; q++) {
+                        const float a = p.upper ? (yv[q] + yv[q]) : (yv[q] - yv[q]);  // demodSSB on {y, y}
+                        const float mag = fabsf(a) + 1e-8f;
+                        dv[q] = p.agc_target / (sqrtf(mag) + 1e-6f);
                     }
+                    *reinterpret_cast<float4 *>(&L.d[c & 1][sl * ROW + i4]) = make_float4(dv[0], dv[1], dv[2], dv[3]);
                 }
             }
-            // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5, stored [sample][stream] ----
+            // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5; zero beyond the frame end ----
             {
                 const int c = it - 5;
                 if (c >= 0 && c < nch) {
+                    const float4 y4 = *reinterpret_cast<const float4 *>(&L.y[c & 3][sl * ROW + i4]);
+                    const float4 g4 = *reinterpret_cast<const float4 *>(&L.g[c & 1][sl * ROW + i4]);
+                    const float yv[4] = {y4.x, y4.y, y4.z, y4.w}, gv[4] = {g4.x, g4.y, g4.z, g4.w};
+                    float ov[4];
 #pragma unroll
-                    for (int m = 0; m < 3; m++) {
-                        const int e = hl + 192 * m, sl = e / CH, i = e % CH;
-                        if (e < PG * CH) {
-                            const float y = L.y[c & 3][sl * ROW + i];
-                            const float a = p.upper ? (y + y) : (y - y);
-                            const float o = clamp_ref(a * L.g[c & 1][sl * ROW + i], -1.0f, 1.0f);
-                            L.outT[c & 1][i * OT + sl] = (c * CH + i < S) ? o : 0.0f;  // FIR reads whole chunks
-                        }
+                    for (int q = 0; q < 4; q++) {
+                        const float a = p.upper ? (yv[q] + yv[q]) : (yv[q] - yv[q]);
+                        const float o = clamp_ref(a * gv[q], -1.0f, 1.0f);
+                        ov[q] = (c * CH + i4 + q < S) ? o : 0.0f;  // the FIR reads whole chunks
                     }
+                    *reinterpret_cast<float4 *>(&L.out[c & 1][sl * ROW + i4]) = make_float4(ov[0], ov[1], ov[2], ov[3]);
                 }
             }
         }
@@ -606,7 +614,7 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
         if (wave == 1) {
             state[s0 + my_s].lpf_z1 = z1;
             state[s0 + my_s].lpf_z2 = z2;
-        } else if (wave == 4) {
+        } else if (wave == 7) {
             state[s0 + my_s].hp_z1 = h1;
             state[s0 + my_s].hp_z2 = h2;
             state[s0 + my_s].bp_z1 = q1;
@@ -675,7 +683,7 @@ void ssb_report_stamps() {
     if (!g_stamps) return;
     std::vector<unsigned long long> h((size_t)g_stamps_groups * 16);
     if (hipMemcpy(h.data(), g_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const char *names[8] = {"DC", "LPF", "AGC", "LOAD", "FIR+EQ", "DES/OUT-0", "DES/OUT-1", "DES/OUT-2"};
+    const char *names[8] = {"DC", "LPF", "AGC", "LOAD", "FIR", "DES/OUT-0", "DES/OUT-1", "EQ"};
     for (int w = 0; w < 8; w++) {
         double work = 0, loop = 0;
         for (int g = 0; g < g_stamps_groups; g++) {
