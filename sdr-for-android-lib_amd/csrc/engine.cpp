@@ -90,6 +90,8 @@ struct sdrg_engine {
     float *d_twiddles = nullptr;
     int tw_n = 0;
     float *d_taps = nullptr;
+    int *d_chunk_table = nullptr;     // per SSB pipeline chunk: FIR outputs overlapping / completed
+    size_t chunk_table_elems = 0;
     float *d_ssb_scratch = nullptr;
     size_t ssb_scratch_elems = 0;
     float *d_spec_scratch = nullptr;
@@ -234,6 +236,27 @@ int32_t prepare_ssb(sdrg_engine *e, SsbParams *p) {
         HIP_TRY(hipMemcpy(e->d_taps, h, sizeof(float) * (size_t)c.n_taps, hipMemcpyHostToDevice));
         c.taps_samp = c.samp_count;
         c.taps_decim = decim;
+        // FIR output ranges per pipeline chunk (the kernel then needs no integer division):
+        // overlapping: D*o <= t1-1 and D*o + NT - 1 >= t0 ; completed: t0 <= D*o + NT - 1 < t1
+        const int CH = ssb_pipe_chunk(), D = decim, NT = c.n_taps;
+        const int S = (int)c.samp_count, PL = ssb_pcm_len(c.samp_count, fs);
+        const int nch = (S + CH - 1) / CH;
+        std::vector<int> tab(4 * (size_t)nch);
+        int ov_lo = 0, ov_hi = -1, dn_lo = 0, dn_hi = -1;
+        for (int ch = 0; ch < nch; ch++) {
+            const int t0 = ch * CH, t1 = std::min(t0 + CH, S);
+            while (ov_lo < PL && D * ov_lo + NT - 1 < t0) ov_lo++;
+            while (ov_hi + 1 < PL && D * (ov_hi + 1) <= t1 - 1) ov_hi++;
+            dn_lo = dn_hi + 1;
+            while (dn_hi + 1 < PL && D * (dn_hi + 1) + NT - 1 < t1) dn_hi++;
+            tab[4 * ch] = ov_lo;
+            tab[4 * ch + 1] = ov_hi;
+            tab[4 * ch + 2] = dn_lo;
+            tab[4 * ch + 3] = dn_hi;
+        }
+        int32_t rc = ensure_device(&e->d_chunk_table, &e->chunk_table_elems, tab.size());
+        if (rc) return rc;
+        HIP_TRY(hipMemcpy(e->d_chunk_table, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice));
     }
     if (!c.eq_init) {
         design_highpass(48000.0f, 1200.0f, 0.7f, c.hp);
@@ -348,7 +371,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
         HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
         if (prof) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
-        HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_ssb, e->d_ssb_scratch, pcm, e->s_ssb));
+        HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_chunk_table, e->d_ssb, e->d_ssb_scratch, pcm, e->s_ssb));
         if (prof) HIP_TRY(hipEventRecord(ev->ssb1, e->s_ssb));
         HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
     }
@@ -465,7 +488,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     (void)hipSetDevice(e->device);
     if (e->s_main) (void)hipStreamSynchronize(e->s_main);
     if (e->s_ssb) (void)hipStreamSynchronize(e->s_ssb);
-    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch,
+    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch,
                     e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
         if (b) (void)hipFree(b);

@@ -29,7 +29,11 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
 // scratch: [n_frames][samp_count + pcm_len] floats.  taps: [n_taps] device floats.
 bool ssb_force_reference_kernels();
 void ssb_report_stamps();  // diagnostic (SDRG_PIPE_STAMPS=1)
+// chunk_table: per chunk of ssb_pipe_chunk() samples {first, last output overlapping it, first, last output
+// completed in it} (host-computed, see engine.cpp); may be null (reference kernels).
+int ssb_pipe_chunk(void);
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
-                      SsbStreamState *state, float *scratch, int16_t *pcm, hipStream_t stream);
+                      const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,
+                      hipStream_t stream);
 
 }  // namespace sdrg

@@ -319,13 +319,12 @@ __device__ __forceinline__ void write_row(float *row, const float (&v)[CH]) {
 // then accumulates in the reference's k order.  Steps outside the output's window meet a zero tap from
 // the padding, and acc + (+-0) == acc exactly here: acc starts at +0 and a round-to-nearest sum never
 // produces -0 from +0, so the masked steps leave the reference's sequential sum unchanged.
-__device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int t1, int slot, int n_slots, int sl, int D,
-                                         int NT, int PL, float &acc) {
-    const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
-    const int o_hi = min(PL - 1, (t1 - 1) / D);
-    const int o = o_lo + ((slot - (o_lo % n_slots)) + n_slots) % n_slots;
-    const bool active = slot < n_slots && o <= o_hi;
+__device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int o_lo, int o_hi, int slot, int nsl_mask,
+                                         int sl, int D, int NT, float &acc) {
+    const int o = o_lo + ((slot - o_lo) & nsl_mask);  // the output this slot holds (o == slot mod NSL)
+    const bool active = o <= o_hi;
     const int base = D * o;
+    const int t1 = t0 + CH;
     if (active && base >= t0) acc = 0.0f;
     // taps_pad index of step 0: t0 - base + CH (inactive lanes read the zero padding at 0)
     const int k0 = active ? (t0 - base + CH) : 0;
@@ -344,12 +343,13 @@ __device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int t1, int 
         acc += xv[i].z * hv[i].z;
         acc += xv[i].w * hv[i].w;
     }
-    if (active && base + NT <= t1) L.fq[c & 1][sl * MAX_DONE + (o % MAX_DONE)] = acc;
+    if (active && base + NT <= t1) L.fq[c & 1][sl * MAX_DONE + (o & (MAX_DONE - 1))] = acc;
 }
 
 template <int FMT, bool DMA>
 __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
-                                                          int n_slots, const float *__restrict__ taps,
+                                                          int nsl_mask, const int4 *__restrict__ chunk_out,
+                                                          const float *__restrict__ taps,
                                                           SsbStreamState *__restrict__ state,
                                                           int16_t *__restrict__ pcm,
                                                           unsigned long long *__restrict__ stamps) {
@@ -530,11 +530,11 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
             // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot mod 4, stream), 4 slots per pass ----
             const int c = it - 6;
             if (c >= 0 && c < nch && PL > 0) {
-                const int t0 = c * CH, t1 = min(t0 + CH, S);
+                const int4 r = chunk_out[c];  // outputs overlapping chunk c: [r.x, r.y] (host table, no division)
                 const int sl = lane % PG, sub = lane / PG;
 #pragma unroll
                 for (int j = 0; j < MAX_SLOTS / 4; j++) {
-                    if (j * 4 < n_slots) fir_slot(L, c, t0, t1, j * 4 + sub, n_slots, sl, D, NT, PL, facc[j]);
+                    if (j * 4 <= nsl_mask) fir_slot(L, c, c * CH, r.x, r.y, j * 4 + sub, nsl_mask, sl, D, NT, facc[j]);
                 }
             }
         } else if (wave == 7) {
@@ -542,11 +542,9 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
             const int ce = it - 7;
             if (ce >= 0 && ce < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
                 const int c = ce;
-                const int t0 = c * CH, t1 = min(t0 + CH, S);
-                const int o_lo = max(0, ceil_div_i(t0 - NT + 1, D));
-                const int o_hi = min(PL - 1, (t1 - NT) >= 0 ? (t1 - NT) / D : -1);
-                for (int o = o_lo; o <= o_hi; o++) {
-                    const float in = L.fq[c & 1][my_s * MAX_DONE + (o % MAX_DONE)];
+                const int4 r = chunk_out[c];  // outputs completed in chunk c: [r.z, r.w]
+                for (int o = r.z; o <= r.w; o++) {
+                    const float in = L.fq[c & 1][my_s * MAX_DONE + (o & (MAX_DONE - 1))];
                     const float yh = p.hp[0] * in + p.hp[1] * h1 + p.hp[2] * h2 - p.hp[3] * h1 - p.hp[4] * h2;
                     h2 = h1;
                     h1 = yh;
@@ -695,22 +693,30 @@ void ssb_report_stamps() {
     }
 }
 
-bool ssb_pipe_supported(const SsbParams &p, int *n_slots) {
+// Outputs whose window can overlap one chunk: floor((CH + NT - 2) / D) + 1; the FIR keeps one accumulator
+// per output modulo NSL (a power of two >= that count, at most MAX_SLOTS).
+bool ssb_pipe_supported(const SsbParams &p, int *nsl_mask) {
     if (p.pcm_len <= 0) {
-        *n_slots = 1;
+        *nsl_mask = 3;
         return true;
     }
-    const int ns = (CH + p.n_taps - 2) / p.decim + 1;  // outputs whose window can overlap one chunk
-    *n_slots = ns;
-    return ns <= MAX_SLOTS && (CH + p.decim - 1) / p.decim <= MAX_DONE && p.n_taps <= 256;
+    const int ns = (CH + p.n_taps - 2) / p.decim + 1;
+    int nsl = 4;
+    while (nsl < ns) nsl *= 2;
+    *nsl_mask = nsl - 1;
+    return nsl <= MAX_SLOTS && (CH + p.decim - 1) / p.decim <= MAX_DONE && p.n_taps <= 256;
 }
 
+int ssb_pipe_chunk(void) { return CH; }
+
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
-                      SsbStreamState *state, float *scratch, int16_t *pcm, hipStream_t stream) {
+                      const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,
+                      hipStream_t stream) {
     if (n_frames <= 0) return hipSuccess;
-    int n_slots = 1;
+    int nsl_mask = 3;
     const char *src = reinterpret_cast<const char *>(iq);
-    if (ssb_pipe_supported(p, &n_slots) && !ssb_force_reference_kernels()) {
+    const int4 *chunk_out = reinterpret_cast<const int4 *>(chunk_table);
+    if (chunk_out && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels()) {
         const dim3 grid((n_frames + PG - 1) / PG);
         const size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
         const int bps = fmt == SDRG_IQ_CF32 ? 8 : fmt == SDRG_IQ_CS16 ? 4 : 2;
@@ -722,11 +728,11 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         unsigned long long *stamps = ssb_stamps_buffer(n_frames);
 #define SDRG_PIPE_LAUNCH(F)                                                                                      \
     if (dma)                                                                                                     \
-        hipLaunchKernelGGL((ssb_pipe_kernel<F, true>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, \
-                           taps, state, pcm, stamps);                                                           \
+        hipLaunchKernelGGL((ssb_pipe_kernel<F, true>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
+                           chunk_out, taps, state, pcm, stamps);                                                           \
     else                                                                                                         \
-        hipLaunchKernelGGL((ssb_pipe_kernel<F, false>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, n_slots, \
-                           taps, state, pcm, stamps);
+        hipLaunchKernelGGL((ssb_pipe_kernel<F, false>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
+                           chunk_out, taps, state, pcm, stamps);
         switch (fmt) {
         case SDRG_IQ_CS8: SDRG_PIPE_LAUNCH(SDRG_IQ_CS8); break;
         case SDRG_IQ_CU8: SDRG_PIPE_LAUNCH(SDRG_IQ_CU8); break;
