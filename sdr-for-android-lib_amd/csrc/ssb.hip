@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "sdrg_internal.h"
+#include "ssb_math.h"
 
 #pragma clang fp contract(off)
 
@@ -29,7 +30,6 @@ namespace sdrg {
 namespace {
 
 constexpr int WAVE = 64;
-typedef float f2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float clamp_ref(float v, float lo, float hi) {  // std::clamp
     return (v < lo) ? lo : (hi < v) ? hi : v;
@@ -244,15 +244,28 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 // go to the EQ role (HP, BP, boost, PCM).  All arithmetic is the reference's, in its order, without
 // contraction: bit-identical PCM.
 //
-// Workgroup = 16 streams x 8 waves, one workgroup per CU (LDS padded past half the CU), so the four
-// serial waves (DC, LPF, AGC, EQ+load) own one SIMD each and the helper waves are paired with them:
-//   w0 DC + w4 FIR | w1 LPF + w5 desired/out | w2 AGC + w6 desired/out | w3 load (LDS-DMA) + w7 EQ
+// Workgroup = 16 streams x 12 waves, one workgroup per CU (LDS padded past half the CU).  A wave issues
+// at most about one VALU instruction per ~10 cycles however idle its SIMD is, while a SIMD serves several
+// waves at that rate (tools/microbench/valu2.hip), so the order-free work is spread over as many waves as
+// keep the heaviest helper's instruction count below the low-pass wave's.  The roles are dealt to the
+// SIMDs (hardware wave w runs on SIMD w % 4) by measurement (tools/gpu_map.sh): a serial wave slows the
+// helpers that share its SIMD about twofold, so the FIR waves, the heaviest helpers, share the loader's:
+//   SIMD0: DC,   AGC output clamp,  desired (1/4)
+//   SIMD1: LPF,  EQ,                desired (1/4)
+//   SIMD2: AGC,  desired (1/4),     desired (1/4)
+//   SIMD3: load, FIR (slot group 0), FIR (slot group 1)
 // ================================================================================================
 constexpr int PG = 16;          // streams per workgroup
 constexpr int CH = 32;          // samples per chunk
 constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_read_b128 by stream lanes
 constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
-constexpr int PIPE_T = 512;     // 8 waves
+constexpr int PIPE_WAVES = 12;
+constexpr int PIPE_T = PIPE_WAVES * 64;
+enum PipeWave : int { W_DC = 0, W_LPF = 1, W_AGC = 2, W_LOAD = 3, W_FIR0 = 4, W_OUT = 5, W_EQ = 6, W_FIR1 = 7,
+                      W_DES0 = 8, W_DES1 = 9, W_DES2 = 10, W_DES3 = 11 };
+// role of hardware wave w = nibble w: w0 DC, w1 LPF, w2 AGC, w3 load, w4 OUT, w5 EQ, w6 DES2, w7 FIR0,
+// w8 DES0, w9 DES1, w10 DES3, w11 FIR1
+constexpr unsigned long long DEFAULT_ROLE_MAP = 0x7B984A653210ull;
 constexpr int MAX_SLOTS = 16;   // concurrent FIR outputs per stream (2 per FIR lane)
 constexpr int MAX_DONE = 4;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
@@ -314,36 +327,54 @@ __device__ __forceinline__ void write_row(float *row, const float (&v)[CH]) {
     for (int i = 0; i < CH; i += 4) *reinterpret_cast<float4 *>(row + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
 }
 
-// One FIR slot of one stream over one chunk: the output o of this slot active in [t0, t1), if any.
-// The lane reads its stream's 32 chunk values and the 32 taps that meet them with 8 + 8 ds_read_b128,
-// then accumulates in the reference's k order.  Steps outside the output's window meet a zero tap from
+// The FIR slots of one stream over one chunk: lane = (stream, sub); slot 4j+sub holds the output o active
+// in [t0, t1), if any.  The lane reads its stream's 32 chunk values once (8 ds_read_b128) and, per slot,
+// the 32 taps that meet them (8 ds_read_b128), forms the products two per packed multiply, and
+// accumulates each slot in the reference's k order; the NP slot chains interleave.  Steps outside the output's window meet a zero tap from
 // the padding, and acc + (+-0) == acc exactly here: acc starts at +0 and a round-to-nearest sum never
 // produces -0 from +0, so the masked steps leave the reference's sequential sum unchanged.
-__device__ __forceinline__ void fir_slot(PipeLds &L, int c, int t0, int o_lo, int o_hi, int slot, int nsl_mask,
-                                         int sl, int D, int NT, float &acc) {
-    const int o = o_lo + ((slot - o_lo) & nsl_mask);  // the output this slot holds (o == slot mod NSL)
-    const bool active = o <= o_hi;
-    const int base = D * o;
+template <int NP, int J0 = 0>
+__device__ __forceinline__ void fir_chunk(PipeLds &L, int c, int t0, int o_lo, int o_hi, int sub, int nsl_mask,
+                                          int sl, int D, int NT, float (&acc)[MAX_SLOTS / 4]) {
     const int t1 = t0 + CH;
-    if (active && base >= t0) acc = 0.0f;
-    // taps_pad index of step 0: t0 - base + CH (inactive lanes read the zero padding at 0)
-    const int k0 = active ? (t0 - base + CH) : 0;
-    const float4 *tp = reinterpret_cast<const float4 *>(&L.taps_sh[k0 & 3][k0 & ~3]);
+    int k0[NP];
+    bool active[NP], done[NP];
+    int slot_o[NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+        const int slot = 4 * (J0 + j) + sub;
+        const int o = o_lo + ((slot - o_lo) & nsl_mask);  // the output this slot holds (o == slot mod NSL)
+        const int base = D * o;
+        active[j] = o <= o_hi;
+        done[j] = active[j] && base + NT <= t1;
+        slot_o[j] = o;
+        if (active[j] && base >= t0) acc[J0 + j] = 0.0f;
+        k0[j] = active[j] ? (t0 - base + CH) : 0;  // taps_pad index of step 0 (inactive: the zero padding)
+    }
     const float4 *in = reinterpret_cast<const float4 *>(&L.out[c & 1][sl * ROW]);  // 0 beyond frame end
-    float4 xv[CH / 4], hv[CH / 4];
 #pragma unroll
     for (int i = 0; i < CH / 4; i++) {
-        xv[i] = in[i];
-        hv[i] = tp[i];
+        const float4 x = in[i];
+        f2v lo[NP], hi[NP];
+#pragma unroll
+        for (int j = 0; j < NP; j++) {
+            const float4 h = reinterpret_cast<const float4 *>(&L.taps_sh[k0[j] & 3][k0[j] & ~3])[i];
+            lo[j] = f2v{x.x, x.y} * f2v{h.x, h.y};  // products are order-free: two per packed op
+            hi[j] = f2v{x.z, x.w} * f2v{h.z, h.w};
+        }
+        // the sums keep the reference's tap order; the NP slot chains are independent and interleave
+#pragma unroll
+        for (int j = 0; j < NP; j++) acc[J0 + j] += lo[j].x;
+#pragma unroll
+        for (int j = 0; j < NP; j++) acc[J0 + j] += lo[j].y;
+#pragma unroll
+        for (int j = 0; j < NP; j++) acc[J0 + j] += hi[j].x;
+#pragma unroll
+        for (int j = 0; j < NP; j++) acc[J0 + j] += hi[j].y;
     }
 #pragma unroll
-    for (int i = 0; i < CH / 4; i++) {
-        acc += xv[i].x * hv[i].x;
-        acc += xv[i].y * hv[i].y;
-        acc += xv[i].z * hv[i].z;
-        acc += xv[i].w * hv[i].w;
-    }
-    if (active && base + NT <= t1) L.fq[c & 1][sl * MAX_DONE + (o & (MAX_DONE - 1))] = acc;
+    for (int j = 0; j < NP; j++)
+        if (done[j]) L.fq[c & 1][sl * MAX_DONE + (slot_o[j] & (MAX_DONE - 1))] = acc[J0 + j];
 }
 
 template <int FMT, bool DMA>
@@ -352,10 +383,12 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                                                           const float *__restrict__ taps,
                                                           SsbStreamState *__restrict__ state,
                                                           int16_t *__restrict__ pcm,
-                                                          unsigned long long *__restrict__ stamps) {
+                                                          unsigned long long *__restrict__ stamps, int prio_mask,
+                                                          int skip_mask, unsigned long long role_map) {
     __shared__ PipeLds L;
     const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hw_wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // runs on SIMD hw_wave % 4
+    const int wave = (int)((role_map >> (4 * hw_wave)) & 15);     // the role it plays (PipeWave)
     const int lane = tid & 63;
     const int s0 = blockIdx.x * PG;
     const int S = p.samp_count;
@@ -369,18 +402,10 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
     }
 
     const int my_s = lane;  // serial roles: lane = stream within the group
-    const bool serial_live = (wave < 3 || wave == 7) && (lane < PG) && (s0 + lane < n_frames);
-    float dc = 0.0f;                              // removeDC: reset per call (:50)
-    float z1 = 0.0f, z2 = 0.0f;                   // rfFilter state, carried across frames
-    float gain = 1.0f;                            // adaptiveAGC: reset per call (:102)
-    float h1 = 0.0f, h2 = 0.0f, q1 = 0.0f, q2 = 0.0f, prev = 0.0f;  // HP/BP state (carried), boost prev
-    float facc[MAX_SLOTS / 4] = {0.0f, 0.0f, 0.0f, 0.0f};  // FIR accumulators (slots j*4 + lane/16)
-    if (serial_live) {
-        const SsbStreamState st = state[s0 + my_s];
-        z1 = st.lpf_z1; z2 = st.lpf_z2;
-        h1 = st.hp_z1; h2 = st.hp_z2; q1 = st.bp_z1; q2 = st.bp_z2;
-    }
-    if (wave < 3) __builtin_amdgcn_s_setprio(2);  // the recurrences own their SIMD's issue slots
+    const float demod_k = p.upper ? 2.0f : 0.0f;  // demodSSB(y, y) = y + y or y - y (:89-94) as y * k
+    const bool serial_live = (wave < 3 || wave == W_EQ) && (lane < PG) && (s0 + lane < n_frames);
+    const bool high = (prio_mask >> wave) & 1;  // masks are per role  // default: the recurrences (waves 0-2) own their SIMD's issue slots
+    if (high) __builtin_amdgcn_s_setprio(2);
     const size_t bps = bytes_per_sample<FMT>();
     const int n_live = min(p.n_in, S);
 
@@ -401,15 +426,31 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                                              (__attribute__((address_space(3))) void *)&L.raw[kb & 1][q * 64], 16, 0, 0);
     };
     if constexpr (DMA) {
-        if (wave == 3 && n_batches > 0) issue_batch(0);
+        if (wave == W_LOAD && n_batches > 0) issue_batch(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 
     unsigned long long st_work = 0, st_t0 = stamps ? __builtin_amdgcn_s_memtime() : 0, st_a = st_t0;
-    for (int it = 0; it < nch + 8; ++it) {
-        if (stamps) st_a = __builtin_amdgcn_s_memtime();
-        if (wave == 0) {
+    // Each role runs its own copy of the chunk loop (same trip count, one LDS barrier per iteration), so
+    // the register allocator sees one role per loop and the kernel's VGPR count is the largest role's,
+    // not the sum of every role's loop-invariant values.
+    auto chunk_loop = [&](auto &&body) {
+        for (int it = 0; it < nch + 8; ++it) {
+            if (stamps) st_a = __builtin_amdgcn_s_memtime();
+            body(it);
+            if (stamps) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                st_work += __builtin_amdgcn_s_memtime() - st_a;
+            }
+            lds_barrier();
+        }
+    };
+    if ((skip_mask >> wave) & 1) {
+        chunk_loop([&](int) {});
+    } else if (wave == W_DC) {
+        float dc = 0.0f;  // removeDC: reset per call (:50)
+        chunk_loop([&](int it) {
             // ---- removeDC (:49-55) and the a0*x term of iir2Process, chunk it-1 ----
             const int c = it - 1;
             if (c >= 0 && c < nch && lane < PG) {
@@ -423,15 +464,25 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                         dc = alpha * dc + one_minus * v[q];
                         v[q] = a0 * (v[q] - dc);
                     }
-                } else {
-                    for (int q = 0; q < lim; q++) {
-                        dc = alpha * dc + one_minus * v[q];
-                        v[q] = a0 * (v[q] - dc);
+                } else {  // the frame's last chunk: uniform guard, no dynamic register indexing
+#pragma unroll
+                    for (int q = 0; q < CH; q++) {
+                        if (q < lim) {
+                            dc = alpha * dc + one_minus * v[q];
+                            v[q] = a0 * (v[q] - dc);
+                        }
                     }
                 }
                 write_row(&L.a[c & 1][my_s * ROW], v);
             }
-        } else if (wave == 1) {
+        });
+    } else if (wave == W_LPF) {
+        float z1 = 0.0f, z2 = 0.0f;  // rfFilter state, carried across frames
+        if (serial_live) {
+            z1 = state[s0 + my_s].lpf_z1;
+            z2 = state[s0 + my_s].lpf_z2;
+        }
+        chunk_loop([&](int it) {
             // ---- iir2Process recurrence (:75-84), chunk it-2 ----
             const int c = it - 2;
             if (c >= 0 && c < nch && lane < PG) {
@@ -451,17 +502,27 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                         v[q] = y;
                     }
                 } else {
-                    for (int q = 0; q < lim; q++) {
-                        const f2v p1 = c1 * z1, p2 = c2 * z2;
-                        const float y = (((v[q] + p1.x) + p2.x) - p1.y) - p2.y;
-                        z2 = z1;
-                        z1 = y;
-                        v[q] = y;
+#pragma unroll
+                    for (int q = 0; q < CH; q++) {
+                        if (q < lim) {
+                            const f2v p1 = c1 * z1, p2 = c2 * z2;
+                            const float y = (((v[q] + p1.x) + p2.x) - p1.y) - p2.y;
+                            z2 = z1;
+                            z1 = y;
+                            v[q] = y;
+                        }
                     }
                 }
                 write_row(&L.y[c & 3][my_s * ROW], v);
             }
-        } else if (wave == 2) {
+        });
+        if (serial_live) {
+            state[s0 + my_s].lpf_z1 = z1;
+            state[s0 + my_s].lpf_z2 = z2;
+        }
+    } else if (wave == W_AGC) {
+        float gain = 1.0f;  // adaptiveAGC: reset per call (:102)
+        chunk_loop([&](int it) {
             // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
             const int c = it - 4;
             if (c >= 0 && c < nch && lane < PG) {
@@ -481,16 +542,21 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                         v[q] = gain;
                     }
                 } else {
-                    for (int q = 0; q < lim; q++) {
-                        const float desired = v[q];
-                        const f2v cand = gain * keep + desired * rates;
-                        gain = (desired < gain) ? cand.x : cand.y;
-                        v[q] = gain;
+#pragma unroll
+                    for (int q = 0; q < CH; q++) {
+                        if (q < lim) {
+                            const float desired = v[q];
+                            const f2v cand = gain * keep + desired * rates;
+                            gain = (desired < gain) ? cand.x : cand.y;
+                            v[q] = gain;
+                        }
                     }
                 }
                 write_row(&L.g[c & 1][my_s * ROW], v);
             }
-        } else if (wave == 3) {
+        });
+    } else if (wave == W_LOAD) {
+        chunk_loop([&](int it) {
             if constexpr (DMA) {
                 // batch it/BC + 1 starts moving now; it must have landed before the barrier that ends
                 // the batch's last-but-one iteration (only this wave's DMAs are counted by its vmcnt)
@@ -526,18 +592,69 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                     *reinterpret_cast<float4 *>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
                 }
             }
-        } else if (wave == 4) {
-            // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot mod 4, stream), 4 slots per pass ----
+        });
+    } else if (wave == W_FIR0 || wave == W_FIR1) {
+        float facc[MAX_SLOTS / 4] = {0.0f, 0.0f, 0.0f, 0.0f};  // FIR accumulators (slots j*4 + lane/16)
+        chunk_loop([&](int it) {
+            // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot mod 4, stream); slot groups
+            //      4j..4j+3 split between the two FIR waves ----
             const int c = it - 6;
             if (c >= 0 && c < nch && PL > 0) {
                 const int4 r = chunk_out[c];  // outputs overlapping chunk c: [r.x, r.y] (host table, no division)
                 const int sl = lane % PG, sub = lane / PG;
-#pragma unroll
-                for (int j = 0; j < MAX_SLOTS / 4; j++) {
-                    if (j * 4 <= nsl_mask) fir_slot(L, c, c * CH, r.x, r.y, j * 4 + sub, nsl_mask, sl, D, NT, facc[j]);
+                const int t0 = c * CH;
+                if (wave == W_FIR0) {
+                    if (nsl_mask == 15) fir_chunk<2, 0>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
+                    else fir_chunk<1, 0>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
+                } else {
+                    if (nsl_mask == 15) fir_chunk<2, 2>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
+                    else if (nsl_mask == 7) fir_chunk<1, 1>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
                 }
             }
-        } else if (wave == 7) {
+        });
+    } else if (wave == W_OUT) {
+        chunk_loop([&](int it) {
+            // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5; zero beyond the frame end ----
+            // lane = 4 x stream + part of 8 samples.  x = demodSSB(y, y) = y + y (upper) or y - y (lower)
+            // is y * 2 or y * 0: equal values (the lower sideband's zero may carry y's sign, which the
+            // clamp keeps and the FIR's sums absorb: acc + (+-0) == acc).  clamp == med3 for non-NaN input.
+            {
+                const int c = it - 5;
+                if (c >= 0 && c < nch) {
+                    const int sl = lane >> 2, part = lane & 3;
+                    const float *yr = &L.y[c & 3][sl * ROW + part * 8];
+                    const float *gr = &L.g[c & 1][sl * ROW + part * 8];
+                    const float4 ya = *reinterpret_cast<const float4 *>(yr), yb = *reinterpret_cast<const float4 *>(yr + 4);
+                    const float4 ga = *reinterpret_cast<const float4 *>(gr), gb = *reinterpret_cast<const float4 *>(gr + 4);
+                    const f2v k2 = {demod_k, demod_k};
+                    f2v o[4] = {(f2v{ya.x, ya.y} * k2) * f2v{ga.x, ga.y}, (f2v{ya.z, ya.w} * k2) * f2v{ga.z, ga.w},
+                                (f2v{yb.x, yb.y} * k2) * f2v{gb.x, gb.y}, (f2v{yb.z, yb.w} * k2) * f2v{gb.z, gb.w}};
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        o[q].x = __builtin_amdgcn_fmed3f(o[q].x, -1.0f, 1.0f);
+                        o[q].y = __builtin_amdgcn_fmed3f(o[q].y, -1.0f, 1.0f);
+                    }
+                    if (c * CH + CH > S) {  // the last chunk only: the FIR reads whole chunks
+                        const int t = c * CH + part * 8;
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            if (t + 2 * q >= S) o[q].x = 0.0f;
+                            if (t + 2 * q + 1 >= S) o[q].y = 0.0f;
+                        }
+                    }
+                    float *dst = &L.out[c & 1][sl * ROW + part * 8];
+                    *reinterpret_cast<float4 *>(dst) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
+                    *reinterpret_cast<float4 *>(dst + 4) = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
+                }
+            }
+        });
+    } else if (wave == W_EQ) {
+        float h1 = 0.0f, h2 = 0.0f, q1 = 0.0f, q2 = 0.0f, prev = 0.0f;  // HP/BP state (carried), boost prev
+        if (serial_live) {
+            const SsbStreamState st = state[s0 + my_s];
+            h1 = st.hp_z1; h2 = st.hp_z2; q1 = st.bp_z1; q2 = st.bp_z2;
+        }
+        chunk_loop([&](int it) {
             // ---- HP -> BP -> transientBoost -> floatToPCM on the outputs the FIR completed, chunk it-7 ----
             const int ce = it - 7;
             if (ce >= 0 && ce < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
@@ -558,67 +675,36 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                     pcm[(size_t)(s0 + my_s) * PL + o] = (int16_t)(v * 32767.0f);
                 }
             }
-        } else {
-            // waves 5 and 6: lane = 4 consecutive samples of one stream (128 lanes x 4 = the 16 x 32 chunk)
-            const int hl = (wave - 5) * 64 + lane;
-            const int sl = hl / (CH / 4), i4 = (hl % (CH / 4)) * 4;
-            // ---- AGC "desired" level (:104-107), chunk it-3 ----
-            {
-                const int c = it - 3;
-                if (c >= 0 && c < nch) {
-                    const float4 y4 = *reinterpret_cast<const float4 *>(&L.y[c & 3][sl * ROW + i4]);
-                    const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
-                    float dv[4];
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const float a = p.upper ? (yv[q] + yv[q]) : (yv[q] - yv[q]);  // demodSSB on {y, y}
-                        const float mag = fabsf(a) + 1e-8f;
-                        dv[q] = p.agc_target / (sqrtf(mag) + 1e-6f);
-                    }
-                    *reinterpret_cast<float4 *>(&L.d[c & 1][sl * ROW + i4]) = make_float4(dv[0], dv[1], dv[2], dv[3]);
-                }
-            }
-            // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5; zero beyond the frame end ----
-            {
-                const int c = it - 5;
-                if (c >= 0 && c < nch) {
-                    const float4 y4 = *reinterpret_cast<const float4 *>(&L.y[c & 3][sl * ROW + i4]);
-                    const float4 g4 = *reinterpret_cast<const float4 *>(&L.g[c & 1][sl * ROW + i4]);
-                    const float yv[4] = {y4.x, y4.y, y4.z, y4.w}, gv[4] = {g4.x, g4.y, g4.z, g4.w};
-                    float ov[4];
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const float a = p.upper ? (yv[q] + yv[q]) : (yv[q] - yv[q]);
-                        const float o = clamp_ref(a * gv[q], -1.0f, 1.0f);
-                        ov[q] = (c * CH + i4 + q < S) ? o : 0.0f;  // the FIR reads whole chunks
-                    }
-                    *reinterpret_cast<float4 *>(&L.out[c & 1][sl * ROW + i4]) = make_float4(ov[0], ov[1], ov[2], ov[3]);
-                }
-            }
-        }
-        if (stamps) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            st_work += __builtin_amdgcn_s_memtime() - st_a;
-        }
-        lds_barrier();
-    }
-    if (stamps && lane == 0) {  // diagnostic build only: per-wave work cycles and loop cycles
-        stamps[(blockIdx.x * 8 + wave) * 2] = st_work;
-        stamps[(blockIdx.x * 8 + wave) * 2 + 1] = __builtin_amdgcn_s_memtime() - st_t0;
-    }
-
-    if (wave < 3) __builtin_amdgcn_s_setprio(0);
-    if (serial_live) {
-        if (wave == 1) {
-            state[s0 + my_s].lpf_z1 = z1;
-            state[s0 + my_s].lpf_z2 = z2;
-        } else if (wave == 7) {
+        });
+        if (serial_live) {
             state[s0 + my_s].hp_z1 = h1;
             state[s0 + my_s].hp_z2 = h2;
             state[s0 + my_s].bp_z1 = q1;
             state[s0 + my_s].bp_z2 = q2;
         }
+    } else {
+        chunk_loop([&](int it) {
+            // waves 8-11: lane = 2 consecutive samples of one stream (256 lanes x 2 = the 16 x 32 chunk)
+            const int hl = (wave == W_DES0 ? 0 : wave == W_DES1 ? 1 : wave == W_DES2 ? 2 : 3) * 64 + lane;
+            const int sl = hl / (CH / 2), i2 = (hl % (CH / 2)) * 2;
+            // ---- AGC "desired" level (:104-107), chunk it-3 ----
+            const int c = it - 3;
+            if (c >= 0 && c < nch) {
+                const float2 y2 = *reinterpret_cast<const float2 *>(&L.y[c & 3][sl * ROW + i2]);
+                // fabsf(demodSSB(y, y)) == |y| * k exactly (k = 2 or 0)
+                const f2v a = f2v{fabsf(y2.x), fabsf(y2.y)} * f2v{demod_k, demod_k};
+                // target / (sqrtf(fabsf(a) + 1e-8f) + 1e-6f), correctly rounded, two lanes per op (ssb_math.h)
+                const f2v d = agc_desired_abs2(a, p.agc_target);
+                *reinterpret_cast<float2 *>(&L.d[c & 1][sl * ROW + i2]) = make_float2(d.x, d.y);
+            }
+        });
     }
+    if (stamps && lane == 0) {  // diagnostic build only: per-wave work cycles and loop cycles
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * 2] = st_work;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * 2 + 1] = __builtin_amdgcn_s_memtime() - st_t0;
+    }
+
+    if (high) __builtin_amdgcn_s_setprio(0);
 }
 
 }  // namespace
@@ -670,7 +756,7 @@ unsigned long long *ssb_stamps_buffer(int n_frames) {
     const int groups = (n_frames + PG - 1) / PG;
     if (groups > g_stamps_groups) {
         if (g_stamps) (void)hipFree(g_stamps);
-        if (hipMalloc(reinterpret_cast<void **>(&g_stamps), sizeof(unsigned long long) * groups * 16) != hipSuccess)
+        if (hipMalloc(reinterpret_cast<void **>(&g_stamps), sizeof(unsigned long long) * groups * PIPE_WAVES * 2) != hipSuccess)
             return nullptr;
         g_stamps_groups = groups;
     }
@@ -679,14 +765,15 @@ unsigned long long *ssb_stamps_buffer(int n_frames) {
 
 void ssb_report_stamps() {
     if (!g_stamps) return;
-    std::vector<unsigned long long> h((size_t)g_stamps_groups * 16);
+    std::vector<unsigned long long> h((size_t)g_stamps_groups * PIPE_WAVES * 2);
     if (hipMemcpy(h.data(), g_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const char *names[8] = {"DC", "LPF", "AGC", "LOAD", "FIR", "DES/OUT-0", "DES/OUT-1", "EQ"};
-    for (int w = 0; w < 8; w++) {
+    const char *names[PIPE_WAVES] = {"DC", "LPF", "AGC", "LOAD", "FIR-0", "OUT", "EQ", "FIR-1", "DES-0", "DES-1",
+                                     "DES-2", "DES-3"};
+    for (int w = 0; w < PIPE_WAVES; w++) {
         double work = 0, loop = 0;
         for (int g = 0; g < g_stamps_groups; g++) {
-            work += h[(g * 8 + w) * 2];
-            loop += h[(g * 8 + w) * 2 + 1];
+            work += h[(g * PIPE_WAVES + w) * 2];
+            loop += h[(g * PIPE_WAVES + w) * 2 + 1];
         }
         fprintf(stderr, "[sdrg stamps] wave %d %-10s work %12.0f cyc  loop %12.0f cyc  (mean over %d groups)\n", w,
                 names[w], work / g_stamps_groups, loop / g_stamps_groups, g_stamps_groups);
@@ -726,13 +813,26 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         const bool dma = (n_live % (bc * CH)) == 0 && ((size_t)p.n_in * bps) % 16 == 0 &&
                          (reinterpret_cast<uintptr_t>(iq) & 15) == 0;
         unsigned long long *stamps = ssb_stamps_buffer(n_frames);
+        static const int prio_mask = [] {  // diagnostic override: SDRG_PIPE_PRIO = bit mask of high-priority waves
+            const char *e = getenv("SDRG_PIPE_PRIO");
+            return e ? (int)strtol(e, nullptr, 0) : 0x7;
+        }();
+        // role of hardware wave w = nibble w (wave w runs on SIMD w % 4); SDRG_PIPE_MAP overrides (diagnostic)
+        static const unsigned long long role_map = [] {
+            const char *e = getenv("SDRG_PIPE_MAP");
+            return e ? strtoull(e, nullptr, 16) : DEFAULT_ROLE_MAP;
+        }();
+        static const int skip_mask = [] {  // diagnostic only (wrong results): roles whose work is skipped
+            const char *e = getenv("SDRG_PIPE_SKIP");
+            return e ? (int)strtol(e, nullptr, 0) : 0;
+        }();
 #define SDRG_PIPE_LAUNCH(F)                                                                                      \
     if (dma)                                                                                                     \
         hipLaunchKernelGGL((ssb_pipe_kernel<F, true>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
-                           chunk_out, taps, state, pcm, stamps);                                                           \
+                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map);                                                \
     else                                                                                                         \
         hipLaunchKernelGGL((ssb_pipe_kernel<F, false>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
-                           chunk_out, taps, state, pcm, stamps);
+                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map);
         switch (fmt) {
         case SDRG_IQ_CS8: SDRG_PIPE_LAUNCH(SDRG_IQ_CS8); break;
         case SDRG_IQ_CU8: SDRG_PIPE_LAUNCH(SDRG_IQ_CU8); break;
