@@ -54,6 +54,22 @@ def synth_device_frames(torch, dev, n_streams: int, seed: int):
     return iq
 
 
+def pmc_traffic(kernel: str, streams: int):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*_hbm_pmc.json, made by
+    tools/profile_round.sh + tools/profile_summary.py on this same bench command), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_pmc.json")), key=os.path.getmtime):
+        try:
+            d = json.load(open(f))
+            t = d["kernels"][kernel]["traffic_bytes"]
+        except (KeyError, ValueError, OSError):
+            continue
+        if t is not None and streams == B:
+            best = (t, os.path.basename(f))
+    return best
+
+
 def cpu_baseline(threads: int, target_cpu_s: float = 15.0) -> dict:
     """The oracle (our C restatement of the reference path: FFT + stats + SSB per frame), one fresh stream per
     frame, timed on the host cores with `threads` worker threads (ctypes releases the GIL)."""
@@ -103,6 +119,7 @@ def main() -> int:
     import torch
     import torch.distributed as dist
     import sdrg
+    from sdrg import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -121,7 +138,6 @@ def main() -> int:
     rec = torch.zeros((streams, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
     plen = eng.pcm_len
     pcm = torch.empty((streams, plen), dtype=torch.int16, device=dev)
-    gathered = [torch.empty_like(rec) for _ in range(world)] if (world > 1 and rank == 0) else None
     torch.cuda.synchronize()
 
     now = [1000]
@@ -135,7 +151,7 @@ def main() -> int:
         now[0] += 8  # 16384 samples @ 2 Msps = 8.192 ms per frame
         if world > 1:
             eng.synchronize()
-            dist.gather(rec, gathered, dst=0)
+            shard.gather_records(rec, world, rank, dst=0)  # the one collective: records to rank 0 (RCCL)
 
     eng.set_profiling(True)
     for _ in range(args.warmup):
@@ -166,6 +182,7 @@ def main() -> int:
     spec_ms = ts["spectrum_ms"]
     alg_bytes = ALG_BYTES_PER_SAMPLE["spectrum"] * streams * N
     achieved = alg_bytes / (spec_ms * 1e-3) / 1e9 if spec_ms > 0 else 0.0
+    traffic = pmc_traffic("spectrum_kernel", streams)
     out = {
         "metric": "IQ Msamples/s (16384-pt FFT+SSB) at 1/2/4/8 GPUs; % HBM roofline",
         "value": round(value, 2),
@@ -187,7 +204,9 @@ def main() -> int:
         "kernel_ms": {k: round(v, 4) for k, v in ts.items() if k != "count"},
         "roofline": {"kernel": "spectrum (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic[0] if traffic else None,
+                     "traffic_source": traffic[1] if traffic else None,
                      "alg_bytes_per_launch": alg_bytes},
     }
     if args.stages != "all":

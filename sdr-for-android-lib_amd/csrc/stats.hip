@@ -65,31 +65,50 @@ __device__ __forceinline__ WinScan scan_window(const float *__restrict__ P, int 
 
 __device__ __forceinline__ float fmax_ref(float a, float b) { return (a < b) ? b : a; }  // std::max
 
-// k-th smallest (0-based) of non-negative floats in lds_vals[0..cnt) by 4 x 8-bit radix select.
-__device__ float kth_smallest(const float *vals, int cnt, int k, int *hist, int *shared_prefix) {
+// k-th smallest (0-based) of non-negative floats in vals[0..cnt) by 4 x 8-bit radix select (one wave).
+// Per digit: an LDS histogram (atomics), then a wave-parallel prefix scan (4 bins per lane) locates the
+// bucket holding the k-th element.  Same element as the reference's std::sort + gaps[k].
+__device__ float kth_smallest(const float *vals, int cnt, int k, int *hist, int *) {
     const int lane = threadIdx.x;
     uint32_t prefix = 0, mask = 0;
     for (int shift = 24; shift >= 0; shift -= 8) {
-        for (int i = lane; i < 256; i += WAVE) hist[i] = 0;
+        *reinterpret_cast<int4 *>(&hist[4 * lane]) = make_int4(0, 0, 0, 0);
         __syncthreads();
         for (int q = lane; q < cnt; q += WAVE) {
             const uint32_t b = __float_as_uint(vals[q]);
             if ((b & mask) == prefix) atomicAdd(&hist[(b >> shift) & 0xff], 1);
         }
         __syncthreads();
-        if (lane == 0) {
-            int acc = 0, d = 0;
-            for (; d < 255; d++) {
-                if (acc + hist[d] > k) break;
-                acc += hist[d];
-            }
-            k -= acc;
-            shared_prefix[0] = (int)(prefix | ((uint32_t)d << shift));
-            shared_prefix[1] = k;
+        const int4 h = *reinterpret_cast<const int4 *>(&hist[4 * lane]);
+        const int own = h.x + h.y + h.z + h.w;
+        int incl = own;
+#pragma unroll
+        for (int off = 1; off < WAVE; off <<= 1) {
+            const int v = __shfl_up(incl, off);
+            if (lane >= off) incl += v;
         }
-        __syncthreads();
-        prefix = (uint32_t)shared_prefix[0];
-        k = shared_prefix[1];
+        const unsigned long long over = __ballot(incl > k);  // non-empty: k < number of candidates
+        const int L = __ffsll((long long)over) - 1;
+        int d = 0, acc = incl - own;
+        if (lane == L) {
+            const int hv[4] = {h.x, h.y, h.z, h.w};
+            int j = 3;  // the lane's last bin unless an earlier one already passes k
+#pragma unroll
+            for (int t = 2; t >= 0; t--) {
+                int before = acc;
+#pragma unroll
+                for (int u = 0; u < t; u++) before += hv[u];
+                if (before + hv[t] > k) j = t;
+            }
+#pragma unroll
+            for (int u = 0; u < 3; u++)
+                if (u < j) acc += hv[u];
+            d = 4 * L + j;
+        }
+        d = __shfl(d, L);
+        acc = __shfl(acc, L);
+        k -= acc;
+        prefix |= (uint32_t)d << shift;
         mask |= 0xffu << shift;
         __syncthreads();
     }
@@ -102,15 +121,26 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
     extern __shared__ __attribute__((aligned(16))) float dyn[];  // [max_pool] pooled dB / gaps, then [span] staged bins
     float *pool = dyn;
     float *stage = dyn + ((g.max_pool + 3) & ~3);
-    __shared__ int hist[256];
+    __shared__ __attribute__((aligned(16))) int hist[256];
     __shared__ int sh_int[2];
     __shared__ int sh_nbottom, sh_best_start;
     __shared__ float w_mean_db[10], w_best1k_db[10];
     __shared__ int w_lo[10], w_hi[10], order[10];
     __shared__ float sh_f[4];
+    __shared__ float sh_gaps[10];       // lane-0 sorts: in LDS, not in a dynamically indexed private array
+    __shared__ int sh_geo_lo[10], sh_geo_hi[10];
 
     const int lane = threadIdx.x;
     const size_t frame = blockIdx.x;
+    // the window bounds are indexed by lane below: copy them out of the kernel arguments with constant
+    // indices (a lane-indexed kernarg array would be copied to scratch)
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        if (lane == i) {
+            sh_geo_lo[i] = g.win_lo[i];
+            sh_geo_hi[i] = g.win_hi[i];
+        }
+    }
     const float *P = spectra + frame * (size_t)g.n;
     StatsState st = state[frame];
     if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
@@ -157,8 +187,8 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
         }
         if (lane <= n_ref) {
             const bool is_focus = (lane == n_ref);
-            const int lo = is_focus ? g.focus_lo : g.win_lo[lane];
-            const int hi = is_focus ? g.focus_hi : g.win_hi[lane];
+            const int lo = is_focus ? g.focus_lo : sh_geo_lo[lane];
+            const int hi = is_focus ? g.focus_hi : sh_geo_hi[lane];
             const WinScan ws = staged ? scan_window(stage - g.span_lo, lo, hi, w1k) : scan_window(P, lo, hi, w1k);
             const int n = hi - lo + 1;
             if (is_focus) {
@@ -205,7 +235,7 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
                 float mean = 0.0f;
                 for (int i = 0; i < n_bottom; i++) mean += w_mean_db[order[i]];
                 mean /= n_bottom;
-                float gaps[10];
+                float *gaps = sh_gaps;
                 for (int i = 0; i < n_bottom; i++) gaps[i] = fabsf(w_mean_db[order[i]] - mean);
                 for (int i = 1; i < n_bottom; i++) {
                     const float v = gaps[i];
@@ -262,7 +292,7 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
                 float mean1k = 0.0f;
                 for (int i = 0; i < n_bottom; i++) mean1k += w_best1k_db[order[i]];
                 mean1k /= n_bottom;
-                float g1k[10];
+                float *g1k = sh_gaps;
                 for (int i = 0; i < n_bottom; i++) g1k[i] = fabsf(w_best1k_db[order[i]] - mean1k);
                 for (int i = 1; i < n_bottom; i++) {
                     const float v = g1k[i];
@@ -318,11 +348,17 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
                 st.peak_confirmed = 0;
             }
             const int flag = (above && st.peak_confirmed >= 1) ? 3 : 0;
-            st.det_buf[st.det_idx] = flag;
+            // det_buf[det_idx] = flag with constant indices (no private-memory indexing)
+            const int d0 = (st.det_idx == 0) ? flag : st.det_buf[0];
+            const int d1 = (st.det_idx == 1) ? flag : st.det_buf[1];
+            const int d2 = (st.det_idx == 2) ? flag : st.det_buf[2];
+            st.det_buf[0] = d0;
+            st.det_buf[1] = d1;
+            st.det_buf[2] = d2;
             st.det_idx = (st.det_idx + 1) % 3;
-            int m = st.det_buf[0];
-            if (st.det_buf[1] > m) m = st.det_buf[1];
-            if (st.det_buf[2] > m) m = st.det_buf[2];
+            int m = d0;
+            if (d1 > m) m = d1;
+            if (d2 > m) m = d2;
             st.detection_flag_sent = m;
         }
     }

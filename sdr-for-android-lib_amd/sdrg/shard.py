@@ -1,0 +1,31 @@
+"""Multi-GPU sharding of streams.
+
+Frames are independent and the per-stream state (FFTProcessor members, processSSB_opt statics) is small,
+so the path shards by stream with no data-path collective: rank r owns streams [r*B, (r+1)*B) and runs its
+own engine on its own GPU (weak scaling).  The one collective is the per-step gather of the 72-byte frame
+records to rank 0; spectra and PCM stay on the GPU that produced them.
+"""
+from __future__ import annotations
+
+
+def stream_range(rank: int, world: int, streams_per_rank: int) -> tuple[int, int]:
+    """[first, last) global stream ids owned by `rank`."""
+    if not (0 <= rank < world) or streams_per_rank < 0:
+        raise ValueError(f"bad shard rank={rank} world={world} streams_per_rank={streams_per_rank}")
+    return rank * streams_per_rank, (rank + 1) * streams_per_rank
+
+
+def gather_records(records, world: int, rank: int, dst: int = 0, group=None):
+    """Gather each rank's [B, record_bytes] uint8 record tensor to `dst`.
+
+    Returns the [world*B, record_bytes] concatenation (global stream order) on `dst`, None elsewhere.  The
+    tensor must live where the process group's backend expects it (HIP memory for nccl/RCCL, host for gloo).
+    """
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return records
+    bufs = [torch.empty_like(records) for _ in range(world)] if rank == dst else None
+    dist.gather(records, bufs, dst=dst, group=group)
+    return torch.cat(bufs, dim=0) if rank == dst else None

@@ -1,0 +1,80 @@
+"""world_size-2 test of the sharded multi-GPU path on CPU (gloo): each rank owns a contiguous block of streams
+and runs them for three steps (the per-rank engine is stood in for by the oracle here: no GPU in this suite);
+the records gathered to rank 0 must equal a single-process run over all streams bit for bit."""
+import os
+import socket
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+N, FS, CF, FOCUS, B, STEPS = 4096, 2_500_000, 100_000_000, 5, 3, 3
+
+
+def _records(O, first, last):
+    raw = O.synth_frames((last) * STEPS, N, O.CS8, tone_hz=1200.0, fs=FS)
+    states = {s: O.FftState(CF, FS, N, FOCUS) for s in range(first, last)}
+    out = []
+    for step in range(STEPS):
+        recs = []
+        for s in range(first, last):
+            iq = O.unpack(O.CS8, raw[s * STEPS + step], N)
+            _, rec = states[s].process(iq, 1000 + 10 * step)
+            recs.append(rec)
+        arr = np.zeros(len(recs), dtype=O.RECORD_DTYPE)  # fields only: the struct's tail padding is unspecified
+        for f in O.RECORD_DTYPE.names:
+            arr[f] = [r[f] for r in recs]
+        out.append(arr)
+    return out
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "sdr-for-android-lib_amd")]
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from sdrg import shard
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, last = shard.stream_range(rank, world, B)
+    got = []
+    for recs in _records(O, first, last):
+        t = torch.from_numpy(recs.view(np.uint8).reshape(B, -1).copy())
+        g = shard.gather_records(t, world, rank)
+        if rank == 0:
+            got.append(g.numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank == 0:
+        q.put(got)
+
+
+def test_sharded_records_equal_single_process(oracle_mod):
+    O = oracle_mod
+    world = 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = _records(O, 0, world * B)
+    assert len(got) == STEPS
+    for step in range(STEPS):
+        np.testing.assert_array_equal(got[step], want[step].view(np.uint8).reshape(world * B, -1))
+
+
+def test_stream_range():
+    sys.path.insert(0, os.path.join(ROOT, "sdr-for-android-lib_amd"))
+    from sdrg import shard
+    assert shard.stream_range(0, 2, 4096) == (0, 4096)
+    assert shard.stream_range(1, 2, 4096) == (4096, 8192)
