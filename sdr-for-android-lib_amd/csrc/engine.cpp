@@ -143,18 +143,8 @@ int32_t ensure_device(T **p, size_t *have, size_t need) {
 
 int32_t upload_twiddles(sdrg_engine *e, int n) {
     if (e->tw_n == n && e->d_twiddles) return SDRG_OK;
-    // layout: full table W_N^m (m < N) for the four-step kernels, then the compact factored tables of the
-    // LDS kernel: W_N^(64 i) (i < N/64) and W_N^i (i < 64)
-    const int nhi = n / 64 > 0 ? n / 64 : 1;
-    std::vector<float> tw(2 * ((size_t)n + nhi + 64));
-    auto put = [&](size_t slot, double m) {
-        const double a = -2.0 * M_PI * m / (double)n;
-        tw[2 * slot] = (float)cos(a);
-        tw[2 * slot + 1] = (float)sin(a);
-    };
-    for (int m = 0; m < n; m++) put(m, m);
-    for (int i = 0; i < nhi; i++) put((size_t)n + i, 64.0 * i);
-    for (int i = 0; i < 64; i++) put((size_t)n + nhi + i, i);
+    std::vector<float> tw(spectrum_twiddle_floats(n));
+    spectrum_fill_twiddles(n, tw.data());
     if (e->d_twiddles) (void)hipFree(e->d_twiddles);
     e->d_twiddles = nullptr;
     e->tw_n = 0;

@@ -17,6 +17,9 @@ namespace sdrg {
 constexpr int SPECTRUM_WAVE_FRAMES = 128;
 bool spectrum_supported(int n);
 size_t spectrum_scratch_floats(int n, int n_frames);
+// Twiddle buffer the spectrum kernels read (floats) and its contents for frame size n.
+size_t spectrum_twiddle_floats(int n);
+void spectrum_fill_twiddles(int n, float *out);
 // twiddles: exp(-2 pi i m / N), m in [0, N), float2, computed in double on the host.
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles,
                            float *spectra, float *scratch, hipStream_t stream);

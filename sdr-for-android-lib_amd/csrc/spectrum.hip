@@ -13,6 +13,12 @@
 // come from two small factored tables (L1-resident).  Complex arithmetic is written on
 // 2-wide float vectors so it maps onto v_pk_{add,mul,fma}_f32.  HBM traffic = bytes in + 4 B out per
 // sample (6 B/sample for CS8), the algorithmic minimum.
+#include <math.h>
+#include <string.h>
+
+#include <type_traits>
+#include <vector>
+
 #include "sdrg_internal.h"
 
 namespace sdrg {
@@ -106,12 +112,6 @@ constexpr int bytes_per_sample() {
     return FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2;
 }
 
-// Twiddle W_N^m from the compact factored tables: W_N^m = W_N^(64 (m >> 6)) * W_N^(m & 63).
-// hi: N/64 entries W_N^(64 i); lo: 64 entries W_N^i.  Both stay in L1 (2.5 KB at N = 16384).
-__device__ __forceinline__ f2 twiddle_n(const f2 *__restrict__ hi, const f2 *__restrict__ lo, int m) {
-    return cmul(hi[m >> 6], lo[m & 63]);
-}
-
 template <int LOG2N>
 struct Plan {
     static constexpr int N = 1 << LOG2N;
@@ -122,6 +122,24 @@ struct Plan {
     static constexpr int LDS_BYTES = (HALF + HALF / 32) * 8;  // half the frame + pad (66 KiB at 16384)
     template <int P>
     static constexpr int radix() { return P == NP - 1 ? RLAST : 32; }
+    static constexpr int radix_of(int p) { return p == NP - 1 ? RLAST : 32; }
+    static constexpr int ns_of(int p) {
+        int s = 1;
+        for (int i = 0; i < p; i++) s *= radix_of(i);
+        return s;
+    }
+    // per-pass twiddle table of pass p >= 1: [R/2 pairs][NS] of float4 (w^(r k), w^((r+1) k)), r = 2q+1,
+    // w = exp(-2 pi i / (NS R)); offset in float4 units from the start of the pass tables
+    static constexpr int tw_off(int p) {
+        int o = 0;
+        for (int i = 1; i < p; i++) o += (radix_of(i) / 2) * ns_of(i);
+        return o;
+    }
+    template <int P>
+    static constexpr int ns() { return ns_of(P); }
+    template <int P>
+    static constexpr int tw_offset() { return tw_off(P); }
+    static constexpr int TW_F4 = tw_off(NP);
 };
 
 // Stockham pass P (radix R, NS = product of the previous radices) on the E values a thread holds as
@@ -129,7 +147,7 @@ struct Plan {
 //   x[r] = A[j + r N/R] * w^(r k), k = j mod NS, w = exp(-2 pi i/(NS R));  X = DFT_R(x);
 //   B[(j/NS) NS R + k + r NS] = X[r]
 template <int LOG2N, int R, int NS>
-__device__ __forceinline__ void pass_compute(f2 (&v)[E], const f2 *__restrict__ thi, const f2 *__restrict__ tlo) {
+__device__ __forceinline__ void pass_compute(f2 (&v)[E], const float4 *__restrict__ tw) {
     constexpr int N = 1 << LOG2N;
     constexpr int T = N / E;
     constexpr int NB = E / R;
@@ -140,9 +158,14 @@ __device__ __forceinline__ void pass_compute(f2 (&v)[E], const f2 *__restrict__ 
 #pragma unroll
         for (int r = 0; r < R; ++r) x[r] = v[b * R + r];
         if constexpr (NS > 1) {
+            // this pass's table, laid out [pair][k]: lanes (consecutive k) read consecutive 16 B
             const int k = j & (NS - 1);
 #pragma unroll
-            for (int r = 1; r < R; ++r) x[r] = cmul(x[r], twiddle_n(thi, tlo, (r * k) * (N / (NS * R))));
+            for (int q = 0; q < R / 2; ++q) {
+                const float4 w = tw[q * NS + k];
+                x[2 * q + 1] = cmul(x[2 * q + 1], f2{w.x, w.y});
+                if (2 * q + 2 < R) x[2 * q + 2] = cmul(x[2 * q + 2], f2{w.z, w.w});
+            }
         }
         dft<R>(x);
 #pragma unroll
@@ -188,11 +211,11 @@ __device__ __forceinline__ void exchange(f2 *lds, f2 (&v)[E]) {
 }
 
 template <int LOG2N, int P, int NS>
-__device__ __forceinline__ void run_passes(f2 *lds, f2 (&v)[E], float *out, const f2 *thi, const f2 *tlo) {
+__device__ __forceinline__ void run_passes(f2 *lds, f2 (&v)[E], float *out, const float4 *tw) {
     using PL = Plan<LOG2N>;
     constexpr int N = 1 << LOG2N;
     constexpr int R = PL::template radix<P>();
-    pass_compute<LOG2N, R, NS>(v, thi, tlo);
+    pass_compute<LOG2N, R, NS>(v, tw + (P >= 1 ? PL::template tw_offset<P>() : 0));
     if constexpr (P == PL::NP - 1) {
         // last pass: output positions j + r N/R; |X|^2 at the fftshifted index (fft_process.cpp:83-97)
         constexpr int T = N / E, NB = E / R;
@@ -208,15 +231,14 @@ __device__ __forceinline__ void run_passes(f2 *lds, f2 (&v)[E], float *out, cons
     } else {
         constexpr int R2 = PL::template radix<P + 1>();
         exchange<LOG2N, R, NS, R2>(lds, v);
-        run_passes<LOG2N, P + 1, NS * R>(lds, v, out, thi, tlo);
+        run_passes<LOG2N, P + 1, NS * R>(lds, v, out, tw);
     }
 }
 
 template <int LOG2N, int FMT>
 __global__ __launch_bounds__(Plan<LOG2N>::T, 2) void spectrum_kernel(const void *__restrict__ iq,
                                                                      float *__restrict__ spectra,
-                                                                     const f2 *__restrict__ thi,
-                                                                     const f2 *__restrict__ tlo) {
+                                                                     const float4 *__restrict__ tw) {
     using PL = Plan<LOG2N>;
     constexpr int N = PL::N, T = PL::T, R0 = PL::template radix<0>(), NB0 = E / R0;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -230,7 +252,7 @@ __global__ __launch_bounds__(Plan<LOG2N>::T, 2) void spectrum_kernel(const void 
 #pragma unroll
         for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_sample<FMT>(src, j + r * (N / R0));
     }
-    run_passes<LOG2N, 0, 1>(lds, v, spectra + frame * (size_t)N, thi, tlo);
+    run_passes<LOG2N, 0, 1>(lds, v, spectra + frame * (size_t)N, tw);
 }
 
 template <int LOG2N, int FMT>
@@ -244,10 +266,9 @@ hipError_t launch_t(const void *iq, int n_frames, const float *tw, float *spectr
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    const f2 *base = reinterpret_cast<const f2 *>(tw);
-    const f2 *thi = base + PL::N;                 // compact tables follow the full table (engine layout)
-    const f2 *tlo = thi + PL::N / 64;
-    hipLaunchKernelGGL(k, dim3(n_frames), dim3(PL::T), PL::LDS_BYTES, s, iq, spectra, thi, tlo);
+    // the per-pass tables follow the full W_N table (layout of spectrum_fill_twiddles)
+    const float4 *pass_tw = reinterpret_cast<const float4 *>(tw + 2 * (size_t)PL::N);
+    hipLaunchKernelGGL(k, dim3(n_frames), dim3(PL::T), PL::LDS_BYTES, s, iq, spectra, pass_tw);
     return hipGetLastError();
 }
 
@@ -402,6 +423,63 @@ hipError_t launch_four_step_fmt(const void *iq, int fmt, int n_frames, const flo
 }
 
 }  // namespace
+
+template <int LOG2N>
+static void fill_pass_tables(std::vector<float> &tw, size_t at) {
+    using PL = Plan<LOG2N>;
+    auto fill = [&](auto pc) {
+        constexpr int P = decltype(pc)::value;
+        if constexpr (P >= 1 && P < PL::NP) {
+            constexpr int R = PL::template radix<P>(), NS = PL::template ns<P>();
+            const size_t base = at + 4 * (size_t)PL::template tw_offset<P>();
+            for (int q = 0; q < R / 2; q++)
+                for (int k = 0; k < NS; k++)
+                    for (int h = 0; h < 2; h++) {
+                        const int r = 2 * q + 1 + h;
+                        const double a = -2.0 * M_PI * (double)((long long)r * k % (NS * R)) / (double)(NS * R);
+                        const size_t o = base + 4 * ((size_t)q * NS + k) + 2 * h;
+                        tw[o] = (r < R) ? (float)cos(a) : 0.0f;
+                        tw[o + 1] = (r < R) ? (float)sin(a) : 0.0f;
+                    }
+        }
+    };
+    fill(std::integral_constant<int, 1>{});
+    fill(std::integral_constant<int, 2>{});
+    fill(std::integral_constant<int, 3>{});
+}
+
+size_t spectrum_twiddle_floats(int n) {
+    size_t pass = 0;
+    switch (n) {
+#define SDRG_TW_CASE(L) \
+    case 1 << L: pass = 4 * (size_t)Plan<L>::TW_F4; break;
+        SDRG_TW_CASE(6) SDRG_TW_CASE(7) SDRG_TW_CASE(8) SDRG_TW_CASE(9) SDRG_TW_CASE(10) SDRG_TW_CASE(11)
+        SDRG_TW_CASE(12) SDRG_TW_CASE(13) SDRG_TW_CASE(14)
+#undef SDRG_TW_CASE
+    default: break;
+    }
+    return 2 * (size_t)n + pass;
+}
+
+// Layout: the full table W_N^m (m < N, the four-step kernels), then for N <= 16384 the LDS kernel's
+// per-pass tables.  Every entry is exp(-2 pi i m / M) evaluated in double and rounded once to float.
+void spectrum_fill_twiddles(int n, float *out) {
+    std::vector<float> tw(spectrum_twiddle_floats(n));
+    for (int m = 0; m < n; m++) {
+        const double a = -2.0 * M_PI * m / (double)n;
+        tw[2 * (size_t)m] = (float)cos(a);
+        tw[2 * (size_t)m + 1] = (float)sin(a);
+    }
+    switch (n) {
+#define SDRG_TW_CASE(L) \
+    case 1 << L: fill_pass_tables<L>(tw, 2 * (size_t)n); break;
+        SDRG_TW_CASE(6) SDRG_TW_CASE(7) SDRG_TW_CASE(8) SDRG_TW_CASE(9) SDRG_TW_CASE(10) SDRG_TW_CASE(11)
+        SDRG_TW_CASE(12) SDRG_TW_CASE(13) SDRG_TW_CASE(14)
+#undef SDRG_TW_CASE
+    default: break;
+    }
+    memcpy(out, tw.data(), tw.size() * sizeof(float));
+}
 
 bool spectrum_supported(int n) {
     return n >= 64 && n <= 65536 && (n & (n - 1)) == 0;
