@@ -142,18 +142,28 @@ struct Plan {
     static constexpr int TW_F4 = tw_off(NP);
 };
 
+// Butterfly handled as block b by this thread.  The last pass pairs consecutive butterflies (j = 2t + b)
+// when a thread holds two, so its |X|^2 stores are 8 bytes wide; every other pass uses j = t + b T.
+template <int LOG2N, int R, bool LAST = false>
+__device__ __forceinline__ int bfly_j(int b) {
+    constexpr int N = 1 << LOG2N, T = N / E, NB = E / R;
+    if constexpr (LAST && NB == 2) return 2 * (int)threadIdx.x + b;
+    return (int)threadIdx.x + b * T;
+}
+
+template <int LOG2N, int R>
+__device__ __forceinline__ int last_j(int b) { return bfly_j<LOG2N, R, true>(b); }
+
 // Stockham pass P (radix R, NS = product of the previous radices) on the E values a thread holds as
 // v[b*R + r] for butterflies j = t + b*T:
 //   x[r] = A[j + r N/R] * w^(r k), k = j mod NS, w = exp(-2 pi i/(NS R));  X = DFT_R(x);
 //   B[(j/NS) NS R + k + r NS] = X[r]
-template <int LOG2N, int R, int NS>
+template <int LOG2N, int R, int NS, bool LAST>
 __device__ __forceinline__ void pass_compute(f2 (&v)[E], const float4 *__restrict__ tw) {
-    constexpr int N = 1 << LOG2N;
-    constexpr int T = N / E;
     constexpr int NB = E / R;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-        const int j = threadIdx.x + b * T;
+        const int j = bfly_j<LOG2N, R, LAST>(b);
         f2 x[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) x[r] = v[b * R + r];
@@ -162,7 +172,11 @@ __device__ __forceinline__ void pass_compute(f2 (&v)[E], const float4 *__restric
             const int k = j & (NS - 1);
 #pragma unroll
             for (int q = 0; q < R / 2; ++q) {
+#ifdef SDRG_DIAG_NO_TWIDDLE  // diagnostic builds only (wrong results): time the pass without twiddle loads
+                const float4 w = make_float4(1.0f, (float)k * 1e-30f, 1.0f, 0.0f);
+#else
                 const float4 w = tw[q * NS + k];
+#endif
                 x[2 * q + 1] = cmul(x[2 * q + 1], f2{w.x, w.y});
                 if (2 * q + 2 < R) x[2 * q + 2] = cmul(x[2 * q + 2], f2{w.z, w.w});
             }
@@ -179,7 +193,7 @@ __device__ __forceinline__ void pass_compute(f2 (&v)[E], const float4 *__restric
 // thread's next inputs; a writer's outputs all fall in one half when NB = 1, so in phase 0 the waves of
 // the lower half of the threads empty their registers while the upper half still hold theirs (48 live
 // complex values at most).
-template <int LOG2N, int R, int NS, int R2>
+template <int LOG2N, int R, int NS, int R2, bool NEXT_LAST>
 __device__ __forceinline__ void exchange(f2 *lds, f2 (&v)[E]) {
     constexpr int N = 1 << LOG2N;
     constexpr int T = N / E;
@@ -200,7 +214,7 @@ __device__ __forceinline__ void exchange(f2 *lds, f2 (&v)[E]) {
         __syncthreads();
 #pragma unroll
         for (int b = 0; b < NB2; ++b) {
-            const int j = threadIdx.x + b * T;
+            const int j = bfly_j<LOG2N, R2, NEXT_LAST>(b);
 #pragma unroll
             for (int r = h * (R2 / 2); r < (h + 1) * (R2 / 2); ++r) nxt[b * R2 + r] = lds[lds_idx(j + r * (N / R2) - h * HALF)];
         }
@@ -215,22 +229,33 @@ __device__ __forceinline__ void run_passes(f2 *lds, f2 (&v)[E], float *out, cons
     using PL = Plan<LOG2N>;
     constexpr int N = 1 << LOG2N;
     constexpr int R = PL::template radix<P>();
-    pass_compute<LOG2N, R, NS>(v, tw + (P >= 1 ? PL::template tw_offset<P>() : 0));
+    pass_compute<LOG2N, R, NS, P == PL::NP - 1>(v, tw + (P >= 1 ? PL::template tw_offset<P>() : 0));
     if constexpr (P == PL::NP - 1) {
         // last pass: output positions j + r N/R; |X|^2 at the fftshifted index (fft_process.cpp:83-97)
-        constexpr int T = N / E, NB = E / R;
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const int j = threadIdx.x + b * T;
+        constexpr int NB = E / R;
+        if constexpr (NB == 2) {
+            // this thread's two butterflies are j = 2t, 2t+1 (see last_j): one 8-byte store per r
+            const int j = 2 * threadIdx.x;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const f2 x = v[b * R + r];
-                out[(j + r * (N / R) + N / 2) & (N - 1)] = x.x * x.x + x.y * x.y;
+                const f2 x0 = v[r], x1 = v[R + r];
+                *reinterpret_cast<float2 *>(&out[(j + r * (N / R) + N / 2) & (N - 1)]) =
+                    make_float2(x0.x * x0.x + x0.y * x0.y, x1.x * x1.x + x1.y * x1.y);
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int j = last_j<LOG2N, R>(b);
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const f2 x = v[b * R + r];
+                    out[(j + r * (N / R) + N / 2) & (N - 1)] = x.x * x.x + x.y * x.y;
+                }
             }
         }
     } else {
         constexpr int R2 = PL::template radix<P + 1>();
-        exchange<LOG2N, R, NS, R2>(lds, v);
+        exchange<LOG2N, R, NS, R2, P + 1 == PL::NP - 1>(lds, v);
         run_passes<LOG2N, P + 1, NS * R>(lds, v, out, tw);
     }
 }
@@ -246,11 +271,42 @@ __global__ __launch_bounds__(Plan<LOG2N>::T, 2) void spectrum_kernel(const void 
     const size_t frame = blockIdx.x;
     const void *src = reinterpret_cast<const char *>(iq) + frame * (size_t)N * bytes_per_sample<FMT>();
     f2 v[E];
+    constexpr int BYTES = N * bytes_per_sample<FMT>();
+    constexpr int WAVES = T / 64;
+    // measured (tools/gpu_variants.sh): staging the raw frame through LDS by LDS-DMA is slower than the
+    // direct strided loads at N = 16384 (0.157 vs 0.148 ms per 4096 frames); kept as a build option
+#ifdef SDRG_SPEC_DMA
+    constexpr bool DMA = FMT != SDRG_IQ_CF32 && WAVES >= 1 && BYTES <= PL::LDS_BYTES && BYTES % (WAVES * 1024) == 0;
+#else
+    constexpr bool DMA = false;
+#endif
+    if constexpr (DMA) {
+        // the raw frame (32 KiB CS8, 64 KiB CS16) lands in the exchange buffer by LDS-DMA, 16 B per lane and
+        // 1 KiB per wave instruction, then each thread picks its strided samples out of LDS
+        const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
 #pragma unroll
-    for (int b = 0; b < NB0; ++b) {
-        const int j = threadIdx.x + b * T;
+        for (int q = 0; q < BYTES / (WAVES * 1024); q++) {
+            const int piece = wave + q * WAVES;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(reinterpret_cast<const char *>(src) + piece * 1024 + lane * 16),
+                (__attribute__((address_space(3))) void *)(smem + piece * 1024), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
 #pragma unroll
-        for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_sample<FMT>(src, j + r * (N / R0));
+        for (int b = 0; b < NB0; ++b) {
+            const int j = threadIdx.x + b * T;
+#pragma unroll
+            for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_sample<FMT>(smem, j + r * (N / R0));
+        }
+        __syncthreads();  // the first exchange overwrites the raw bytes
+    } else {
+#pragma unroll
+        for (int b = 0; b < NB0; ++b) {
+            const int j = threadIdx.x + b * T;
+#pragma unroll
+            for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_sample<FMT>(src, j + r * (N / R0));
+        }
     }
     run_passes<LOG2N, 0, 1>(lds, v, spectra + frame * (size_t)N, tw);
 }

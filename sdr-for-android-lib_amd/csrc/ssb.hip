@@ -378,7 +378,9 @@ __device__ __forceinline__ void fir_chunk(PipeLds &L, int c, int t0, int o_lo, i
 }
 
 template <int FMT, bool DMA>
-__global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
+// waves_per_eu(6): at most 80 VGPRs, so 3 pipeline waves (240) plus a spectrum workgroup's 2 waves of 128
+// fit one SIMD's 512 and the FFT of the same step runs on the same CUs
+__global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
                                                           int nsl_mask, const int4 *__restrict__ chunk_out,
                                                           const float *__restrict__ taps,
                                                           SsbStreamState *__restrict__ state,
@@ -456,22 +458,13 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
             if (c >= 0 && c < nch && lane < PG) {
                 float v[CH];
                 read_row(&L.re[c & 1][my_s * ROW], v);
-                const int lim = min(CH, S - c * CH);
+                // the frame's last chunk runs whole too: dc restarts every frame and the samples past the
+                // frame end (zeros from the loader) only feed outputs nothing reads
                 const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
-                if (lim == CH) {
 #pragma unroll
-                    for (int q = 0; q < CH; q++) {
-                        dc = alpha * dc + one_minus * v[q];
-                        v[q] = a0 * (v[q] - dc);
-                    }
-                } else {  // the frame's last chunk: uniform guard, no dynamic register indexing
-#pragma unroll
-                    for (int q = 0; q < CH; q++) {
-                        if (q < lim) {
-                            dc = alpha * dc + one_minus * v[q];
-                            v[q] = a0 * (v[q] - dc);
-                        }
-                    }
+                for (int q = 0; q < CH; q++) {
+                    dc = alpha * dc + one_minus * v[q];
+                    v[q] = a0 * (v[q] - dc);
                 }
                 write_row(&L.a[c & 1][my_s * ROW], v);
             }
@@ -528,29 +521,17 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
             if (c >= 0 && c < nch && lane < PG) {
                 float v[CH];
                 read_row(&L.d[c & 1][my_s * ROW], v);
-                const int lim = min(CH, S - c * CH);
                 // gain = gain*(1-rate) + desired*rate, rate = desired < gain ? fast : slow: both candidates
-                // (fast, slow) in one packed lane pair, then the select
+                // (fast, slow) in one packed lane pair, then the select.  The last chunk runs whole: gain
+                // restarts every frame and outputs past the frame end are zeroed by the clamp role.
                 const f2v rates = {p.agc_fast, 0.00035f};
                 const f2v keep = {1.0f - p.agc_fast, 1.0f - 0.00035f};
-                if (lim == CH) {
 #pragma unroll
-                    for (int q = 0; q < CH; q++) {
-                        const float desired = v[q];
-                        const f2v cand = gain * keep + desired * rates;
-                        gain = (desired < gain) ? cand.x : cand.y;
-                        v[q] = gain;
-                    }
-                } else {
-#pragma unroll
-                    for (int q = 0; q < CH; q++) {
-                        if (q < lim) {
-                            const float desired = v[q];
-                            const f2v cand = gain * keep + desired * rates;
-                            gain = (desired < gain) ? cand.x : cand.y;
-                            v[q] = gain;
-                        }
-                    }
+                for (int q = 0; q < CH; q++) {
+                    const float desired = v[q];
+                    const f2v cand = gain * keep + desired * rates;
+                    gain = (desired < gain) ? cand.x : cand.y;
+                    v[q] = gain;
                 }
                 write_row(&L.g[c & 1][my_s * ROW], v);
             }

@@ -47,23 +47,59 @@ __device__ __forceinline__ WinScan scan_window(const float *__restrict__ P, int 
         float rs = 0.0f;
 #pragma unroll 8
         for (int i = lo; i < lo + w; i++) rs += P[i];
-        float best = rs / w, bv = rs;
+        float bv = rs;
 #pragma unroll 4
         for (int st = lo + 1; st + w - 1 <= hi; st++) {
             rs += P[st + w - 1] - P[st - 1];
-            const float m = rs / w;
-            if (m > best) best = m;
             if (rs > bv) {
                 bv = rs;
                 r.best_start = st;
             }
         }
-        r.best1k = best;
+        // the reference keeps best = max over st of rs/w (:171-178); x -> RN(x / w) is monotone for w > 0,
+        // so that maximum is exactly RN(max rs / w): one division instead of one per step
+        r.best1k = bv / w;
     }
     return r;
 }
 
 __device__ __forceinline__ float fmax_ref(float a, float b) { return (a < b) ? b : a; }  // std::max
+
+// Ascending sort of 10 (key, index) pairs by (key, index): odd-even transposition network, registers only.
+__device__ __forceinline__ void sort_pairs10(float (&k)[10], int (&ix)[10]) {
+#pragma unroll
+    for (int round = 0; round < 10; round++) {
+#pragma unroll
+        for (int i = round & 1; i + 1 < 10; i += 2) {
+            const bool sw = (k[i + 1] < k[i]) || (k[i + 1] == k[i] && ix[i + 1] < ix[i]);
+            const float ka = sw ? k[i + 1] : k[i], kb = sw ? k[i] : k[i + 1];
+            const int ia = sw ? ix[i + 1] : ix[i], ib = sw ? ix[i] : ix[i + 1];
+            k[i] = ka; k[i + 1] = kb; ix[i] = ia; ix[i + 1] = ib;
+        }
+    }
+}
+
+// k-th smallest (k < 4) of 4 floats (the reference sorts then indexes: same value).
+__device__ __forceinline__ float kth_of4(float (&g)[4], int k) {
+#pragma unroll
+    for (int round = 0; round < 4; round++) {
+#pragma unroll
+        for (int i = round & 1; i + 1 < 4; i += 2) {
+            const float a = fminf(g[i], g[i + 1]), b = fmaxf(g[i], g[i + 1]);
+            g[i] = a;
+            g[i + 1] = b;
+        }
+    }
+    // selects, not an indexed load (the compiler would place g in scratch to index it)
+    float r = g[0];
+    asm volatile("" : "+v"(r));
+    r = (k == 1) ? g[1] : r;
+    asm volatile("" : "+v"(r));
+    r = (k == 2) ? g[2] : r;
+    asm volatile("" : "+v"(r));
+    r = (k == 3) ? g[3] : r;
+    return r;
+}
 
 // k-th smallest (0-based) of non-negative floats in vals[0..cnt) by 4 x 8-bit radix select (one wave).
 // Per digit: an LDS histogram (atomics), then a wave-parallel prefix scan (4 bins per lane) locates the
@@ -127,7 +163,6 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
     __shared__ float w_mean_db[10], w_best1k_db[10];
     __shared__ int w_lo[10], w_hi[10], order[10];
     __shared__ float sh_f[4];
-    __shared__ float sh_gaps[10];       // lane-0 sorts: in LDS, not in a dynamically indexed private array
     __shared__ int sh_geo_lo[10], sh_geo_hi[10];
 
     const int lane = threadIdx.x;
@@ -218,32 +253,31 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
         } else {
             int n_bottom = 1;
             if (lane == 0) {
-                // std::sort of <= 16 elements in libstdc++ is a (stable) insertion sort
-                for (int i = 0; i < n_ref; i++) order[i] = i;
-                for (int i = 1; i < n_ref; i++) {
-                    const int v = order[i];
-                    int j = i;
-                    while (j > 0 && w_mean_db[v] < w_mean_db[order[j - 1]]) {
-                        order[j] = order[j - 1];
-                        j--;
-                    }
-                    order[j] = v;
+                // std::sort of <= 16 elements in libstdc++ is a (stable) insertion sort: the same order is a
+                // sort by (meanDb, window index), done here by a network on registers
+                float key[10];
+                int ix[10];
+#pragma unroll
+                for (int i = 0; i < 10; i++) {
+                    key[i] = (i < n_ref) ? w_mean_db[i] : INFINITY;
+                    ix[i] = i;
                 }
+                sort_pairs10(key, ix);
+#pragma unroll
+                for (int i = 0; i < 10; i++)
+                    if (i < n_ref) order[i] = ix[i];
                 const int nb0 = (int)(n_ref * 0.4f);
-                n_bottom = nb0 > 1 ? nb0 : 1;
+                n_bottom = nb0 > 1 ? nb0 : 1;  // <= 4 (n_ref <= 10)
                 // 6.4a (:235-247)
                 float mean = 0.0f;
-                for (int i = 0; i < n_bottom; i++) mean += w_mean_db[order[i]];
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (i < n_bottom) mean += key[i];
                 mean /= n_bottom;
-                float *gaps = sh_gaps;
-                for (int i = 0; i < n_bottom; i++) gaps[i] = fabsf(w_mean_db[order[i]] - mean);
-                for (int i = 1; i < n_bottom; i++) {
-                    const float v = gaps[i];
-                    int j = i;
-                    while (j > 0 && v < gaps[j - 1]) { gaps[j] = gaps[j - 1]; j--; }
-                    gaps[j] = v;
-                }
-                const float sigma = fmax_ref(1.4816f * gaps[n_bottom / 2], 0.5f);
+                float gp[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) gp[i] = (i < n_bottom) ? fabsf(key[i] - mean) : INFINITY;
+                const float sigma = fmax_ref(1.4816f * kth_of4(gp, n_bottom / 2), 0.5f);
                 const float snr_db = signal_power_db - mean;
                 st.mean_snr_db = snr_db;
                 st.mean_snr_sigma = snr_db / sigma;
@@ -265,8 +299,22 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
             if (cnt > g.max_pool) cnt = g.max_pool;  // host sizes max_pool from the geometry
             __syncthreads();
             if (lane == 0) {
+                // sequential sum in pool order (:259-263); 16 values per step read with 4 ds_read_b128
                 float m = 0.0f;
-                for (int q = 0; q < cnt; q++) m += pool[q];
+                int q = 0;
+                for (; q + 16 <= cnt; q += 16) {
+                    float4 b[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) b[u] = *reinterpret_cast<const float4 *>(&pool[q + 4 * u]);
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        m += b[u].x;
+                        m += b[u].y;
+                        m += b[u].z;
+                        m += b[u].w;
+                    }
+                }
+                for (; q < cnt; q++) m += pool[q];
                 m /= (float)cnt;
                 sh_f[2] = m;
             }
@@ -292,16 +340,11 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
                 float mean1k = 0.0f;
                 for (int i = 0; i < n_bottom; i++) mean1k += w_best1k_db[order[i]];
                 mean1k /= n_bottom;
-                float *g1k = sh_gaps;
-                for (int i = 0; i < n_bottom; i++) g1k[i] = fabsf(w_best1k_db[order[i]] - mean1k);
-                for (int i = 1; i < n_bottom; i++) {
-                    const float v = g1k[i];
-                    int j = i;
-                    while (j > 0 && v < g1k[j - 1]) { g1k[j] = g1k[j - 1]; j--; }
-                    g1k[j] = v;
-                }
+                float g1k[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) g1k[i] = (i < n_bottom) ? fabsf(w_best1k_db[order[i]] - mean1k) : INFINITY;
                 const float sigma_floor_1k = sigma_bin / sqrtf((float)w1k);
-                float sigma1k = 1.4816f * g1k[n_bottom / 2];
+                float sigma1k = 1.4816f * kth_of4(g1k, n_bottom / 2);
                 if (sigma1k < sigma_floor_1k) sigma1k = sigma_floor_1k;
                 if (sigma1k < 0.5f) sigma1k = 0.5f;
                 const float focus_best1k_linear = sh_f[1];

@@ -23,7 +23,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG, "lib", "libsdrg.so")
+LIB_PATH = os.environ.get("SDRG_LIB_PATH") or os.path.join(PKG, "lib", "libsdrg.so")  # override: diagnostic builds
 
 # include/sdrg.h
 CF32, CS8, CU8, CS16 = 0, 1, 2, 3

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Diagnostic library variant: tools/build_variant.sh NAME "EXTRA_HIPFLAGS" -> sdr-for-android-lib_amd/lib/libsdrg_NAME.so
+# (use with SDRG_LIB_PATH=...; never the product library)
+set -e
+NAME=$1; FLAGS=$2
+D=sdr-for-android-lib_amd; B=$D/build/variant_$NAME; mkdir -p $B
+HIP="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics $FLAGS"
+$HIP -c $D/csrc/spectrum.hip -o $B/spectrum.o
+$HIP -ffp-contract=off -c $D/csrc/stats.hip -o $B/stats.o
+$HIP -ffp-contract=off -fno-slp-vectorize -c $D/csrc/ssb.hip -o $B/ssb.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/lib/libsdrg_$NAME.so $B/spectrum.o $B/stats.o $B/ssb.o $D/build/design.o $D/build/engine.o $D/build/compat.o -lm
+echo built $D/lib/libsdrg_$NAME.so
