@@ -1,18 +1,25 @@
-// spectrum.hip — fused IQ unpack -> N-point forward FFT -> |X|^2 -> fftshift, one frame per workgroup.
+// spectrum.hip — fused IQ unpack -> N-point forward FFT -> |X|^2 -> fftshift for a batch of frames.
 //
 // Replaces FFTProcessor::process steps 1-4 (src/dsp/fft_process.cpp:42-97): copy into the FFTW buffer,
 // fftwf_plan_dft_1d(N, FORWARD, ESTIMATE) + execute (unnormalised, no window), power = re^2 + im^2,
 // fftshift.  The unused 10-frame ring buffer (:62-73) has no observable output and is not kept.
 //
-// Design (gfx950): Stockham autosort FFT with radix-32 register butterflies (N = 16384: 3 passes =
-// 32 * 32 * 16, two exchanges).  Each thread owns E = 32 complex values (T = N/32 threads, 512 at
-// N = 16384).  Between passes the values move through an LDS buffer of HALF the frame (66 KiB) in two
-// phases, so two frames' workgroups fit a CU beside the SSB pipeline's workgroup.  Pass 0 reads the raw
-// int8/uint8/int16/float samples straight from HBM (coalesced across lanes) and converts them in
-// registers; the last pass writes |X|^2 straight to HBM at the fftshifted index (coalesced).  Twiddles
-// come from two small factored tables (L1-resident).  Complex arithmetic is written on
-// 2-wide float vectors so it maps onto v_pk_{add,mul,fma}_f32.  HBM traffic = bytes in + 4 B out per
-// sample (6 B/sample for CS8), the algorithmic minimum.
+// Design (gfx950):
+//   * Stockham autosort FFT with radix-32 register butterflies: each thread owns E = 32 complex values
+//     (T = N/32 threads per frame); N = 16384 is 32 x 32 x 16 (3 passes, two LDS exchanges).
+//   * Codelets are written against gfx950's packed f32 ops (v_pk_add/mul/fma_f32, 2 lanes = one complex
+//     number): the -i and (+-1-i)/sqrt2 twiddles cost no multiply (op_sel swaps and neg modifiers), a
+//     general twiddled butterfly is three packed ops (x = a + bW by two fmas, y = 2a - x).
+//   * int8/int16 samples are converted unscaled (one SDWA sign-extending convert per component) and the
+//     format's power-of-two scale is applied once to |X|^2: scaling by a power of two commutes exactly with
+//     every rounding step, so this equals scaling the input.  CU8 subtracts its 127.4 offset on input.
+//   * Pass 0 reads the raw samples straight from HBM (coalesced 128-B rows per wave instruction), the last
+//     pass writes |X|^2 straight to HBM at the fftshifted index (512-B rows): HBM traffic = bytes in +
+//     4 B out per sample (6 B/sample for CS8), the algorithmic minimum.
+//   * N = 16384 (the benchmark size) has its own persistent kernel (two 512-thread workgroups per CU looping
+//     over frames, twiddles in LDS, the next frame's raw samples loaded before this frame's stores).
+//   * N = 32768 / 65536 do not fit a CU's LDS and run as a two-kernel four-step FFT.
+// MFMA is not used: there is no dense contraction on this path.
 #include <math.h>
 #include <string.h>
 
@@ -38,20 +45,6 @@ __device__ constexpr float W32_IM[16] = {-0.0f, -0.195090324f, -0.382683426f, -0
                                          -0.923879504f, -0.831469595f, -0.707106769f, -0.555570245f,
                                          -0.382683426f, -0.195090324f};
 
-__device__ __forceinline__ f2 cmul(f2 a, f2 w) {
-    // (a.x w.x - a.y w.y, a.x w.y + a.y w.x)
-    f2 r = a.xx * w;
-    f2 wr = {-w.y, w.x};
-    return r + a.yy * wr;
-}
-
-// multiply by W32^t (t compile-time after unrolling)
-__device__ __forceinline__ f2 twiddle32(f2 a, int t) {
-    if (t == 0) return a;
-    if (t == 8) return f2{a.y, -a.x};  // * (-i)
-    return cmul(a, f2{W32_RE[t], W32_IM[t]});
-}
-
 template <int R>
 __device__ __forceinline__ constexpr int bitrev(int i) {
     int r = 0;
@@ -62,35 +55,117 @@ __device__ __forceinline__ constexpr int bitrev(int i) {
     return r;
 }
 
-// In-register DFT of R points (R | 32), natural order in and out (radix-2 DIT).
-template <int R>
-__device__ __forceinline__ void dft(f2 (&v)[R]) {
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-        const int j = bitrev<R>(i);
-        if (j > i) {
-            f2 t = v[i];
-            v[i] = v[j];
-            v[j] = t;
-        }
-    }
-#pragma unroll
-    for (int len = 2; len <= R; len <<= 1) {
-#pragma unroll
-        for (int base = 0; base < R; base += len) {
-#pragma unroll
-            for (int k = 0; k < len / 2; ++k) {
-                const f2 b = twiddle32(v[base + k + len / 2], k * (32 / len));
-                const f2 a = v[base + k];
-                v[base + k] = a + b;
-                v[base + k + len / 2] = a - b;
-            }
-        }
+template <int FMT>
+constexpr int bytes_per_sample() {
+    return FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Packed complex helpers (f2 = {re, im} in one 64-bit register pair)
+// ------------------------------------------------------------------------------------------------
+// a + (-i) b = (a.x + b.y, a.y - b.x)
+__device__ __forceinline__ f2 add_mi(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// a - (-i) b = (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ f2 sub_mi(f2 a, f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// (b.x + b.y, b.y - b.x) = b (1 - i) = b W32^4 / c, c = 1/sqrt2
+__device__ __forceinline__ f2 rot45(f2 b) {
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b));
+    return r;
+}
+// a + c (-i) s = (a.x + c s.y, a.y - c s.x)
+__device__ __forceinline__ f2 fma_mi(f2 s, f2 c, f2 a) {
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]" : "=v"(r) : "v"(s), "v"(c), "v"(a));
+    return r;
+}
+// a - c (-i) s = (a.x - c s.y, a.y + c s.x)
+__device__ __forceinline__ f2 fma_pi(f2 s, f2 c, f2 a) {
+    f2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(s), "v"(c), "v"(a));
+    return r;
+}
+// a * w for a twiddle w held in registers: (a.x w.x, a.x w.y), then + (-a.y w.y, a.y w.x) with the swap
+// and the sign as operand modifiers (the compiler otherwise materialises (-w.y, w.x) with v_xor + v_mov)
+__device__ __forceinline__ f2 cmul_v(f2 a, f2 w) {
+    f2 u, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(u) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(w), "v"(u));
+    return r;
+}
+
+// radix-2 butterfly with twiddle W32^t on b: (a + W b, a - W b)
+template <int t>
+__device__ __forceinline__ void bfly(f2 &a, f2 &b) {
+    constexpr float C = 0.707106769f;
+    if constexpr (t == 0) {
+        const f2 x = a + b, y = a - b;
+        a = x; b = y;
+    } else if constexpr (t == 8) {
+        const f2 x = add_mi(a, b), y = sub_mi(a, b);
+        a = x; b = y;
+    } else if constexpr (t == 4) {
+        const f2 s = rot45(b);
+        const f2 x = a + s * f2{C, C}, y = a - s * f2{C, C};
+        a = x; b = y;
+    } else if constexpr (t == 12) {
+        const f2 s = rot45(b);
+        const f2 x = fma_mi(s, f2{C, C}, a), y = fma_pi(s, f2{C, C}, a);
+        a = x; b = y;
+    } else {
+        // x = a + b W as two fmas (b.x W, then b.y iW), y = 2a - x: three packed ops instead of four
+        const f2 w = {W32_RE[t], W32_IM[t]}, wi = {-W32_IM[t], W32_RE[t]};
+        const f2 x = (a + b.xx * w) + b.yy * wi;
+        const f2 y = a * f2{2.0f, 2.0f} - x;
+        a = x; b = y;
     }
 }
 
-__device__ __forceinline__ int lds_idx(int e) { return e + (e >> 5); }  // one pad slot per 32 values
+template <int R, int LEN, int BASE, int K>
+__device__ __forceinline__ void stage_k(f2 (&v)[R]) {
+    if constexpr (K < LEN / 2) {
+        bfly<K * (32 / LEN)>(v[BASE + K], v[BASE + K + LEN / 2]);
+        stage_k<R, LEN, BASE, K + 1>(v);
+    }
+}
+template <int R, int LEN, int BASE>
+__device__ __forceinline__ void stage(f2 (&v)[R]) {
+    if constexpr (BASE < R) {
+        stage_k<R, LEN, BASE, 0>(v);
+        stage<R, LEN, BASE + LEN>(v);
+    }
+}
+template <int R, int LEN>
+__device__ __forceinline__ void stages(f2 (&v)[R]) {
+    if constexpr (LEN <= R) {
+        stage<R, LEN, 0>(v);
+        stages<R, LEN * 2>(v);
+    }
+}
 
+// In-register DFT of R points (R | 32), natural order in and out (radix-2 DIT, bit reversal = renaming).
+template <int R>
+__device__ __forceinline__ void dft(f2 (&v)[R]) {
+    f2 w[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) w[bitrev<R>(i)] = v[i];
+    stages<R, 2>(w);
+#pragma unroll
+    for (int i = 0; i < R; ++i) v[i] = w[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Samples
+// ------------------------------------------------------------------------------------------------
+// Sample e of a frame with the format's scale (four-step kernels).
 template <int FMT>
 __device__ __forceinline__ f2 load_sample(const void *frame, int e) {
     if constexpr (FMT == SDRG_IQ_CS8) {
@@ -107,11 +182,53 @@ __device__ __forceinline__ f2 load_sample(const void *frame, int e) {
     }
 }
 
+// Unscaled sample from its raw 16-bit (CS8/CU8) or 32-bit (CS16) word; the power-of-two scale goes on |X|^2.
 template <int FMT>
-constexpr int bytes_per_sample() {
-    return FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2;
+__device__ __forceinline__ f2 convert_raw(uint32_t v) {
+    f2 r;
+    if constexpr (FMT == SDRG_IQ_CS8) {
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0" : "=v"(r.x) : "v"(v));
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(r.y) : "v"(v));
+    } else if constexpr (FMT == SDRG_IQ_CU8) {
+        // (v - 127.4f) * (1/128): the subtraction here (not a power of two), the 1/128 on |X|^2
+        r = f2{(float)(v & 0xffu), (float)((v >> 8) & 0xffu)} - f2{127.4f, 127.4f};
+    } else {
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(r.x) : "v"(v));
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1" : "=v"(r.y) : "v"(v));
+    }
+    return r;
 }
 
+// buffer resource over one frame: per-lane offset in a VGPR, per-element offset as a scalar
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const void *base, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
+}
+
+template <int FMT>
+__device__ __forceinline__ uint32_t load_raw_word(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    if constexpr (bytes_per_sample<FMT>() == 2) return __builtin_amdgcn_raw_buffer_load_b16(rs, voff, soff, 0);
+    else return __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0);
+}
+
+template <int FMT>
+__device__ __forceinline__ f2 load_unscaled(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    if constexpr (FMT == SDRG_IQ_CF32) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+        return f2{__uint_as_float(v[0]), __uint_as_float(v[1])};
+    } else {
+        return convert_raw<FMT>(load_raw_word<FMT>(rs, voff, soff));
+    }
+}
+
+// |X|^2 scale of a format: (2^-7)^2 for 8-bit, (2^-15)^2 for 16-bit, 1 for float
+template <int FMT>
+constexpr float power_scale() {
+    return FMT == SDRG_IQ_CF32 ? 1.0f : FMT == SDRG_IQ_CS16 ? 1.0f / 1073741824.0f : 1.0f / 16384.0f;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Generic LDS kernel (N = 64 .. 8192): one frame per workgroup of T = N/32 threads
+// ------------------------------------------------------------------------------------------------
 template <int LOG2N>
 struct Plan {
     static constexpr int N = 1 << LOG2N;
@@ -119,7 +236,7 @@ struct Plan {
     static constexpr int NP = (LOG2N + 4) / 5;  // passes: radix 32 ..., last = remainder
     static constexpr int RLAST = (LOG2N % 5 == 0) ? 32 : (1 << (LOG2N % 5));
     static constexpr int HALF = N / 2;
-    static constexpr int LDS_BYTES = (HALF + HALF / 32) * 8;  // half the frame + pad (66 KiB at 16384)
+    static constexpr int LDS_BYTES = (HALF + HALF / 32) * 8;  // half the frame + pad
     template <int P>
     static constexpr int radix() { return P == NP - 1 ? RLAST : 32; }
     static constexpr int radix_of(int p) { return p == NP - 1 ? RLAST : 32; }
@@ -151,13 +268,14 @@ __device__ __forceinline__ int bfly_j(int b) {
     return (int)threadIdx.x + b * T;
 }
 
-template <int LOG2N, int R>
-__device__ __forceinline__ int last_j(int b) { return bfly_j<LOG2N, R, true>(b); }
+// LDS slot of element A + c (A per thread, c compile-time) with one pad slot per 32 values: when
+// (A mod 32) + (c mod 32) < 32, (A + c) + ((A + c) >> 5) = pad_base(A) + pad_off(c).
+__device__ __forceinline__ int pad_base(int a) { return a + (a >> 5); }
+constexpr int pad_off(int c) { return c + c / 32; }
 
-// Stockham pass P (radix R, NS = product of the previous radices) on the E values a thread holds as
-// v[b*R + r] for butterflies j = t + b*T:
-//   x[r] = A[j + r N/R] * w^(r k), k = j mod NS, w = exp(-2 pi i/(NS R));  X = DFT_R(x);
-//   B[(j/NS) NS R + k + r NS] = X[r]
+// Stockham pass (radix R, NS = product of the previous radices) on the E values a thread holds as
+// v[b*R + r] for butterflies j:  x[r] = A[j + r N/R] * w^(r k), k = j mod NS, w = exp(-2 pi i/(NS R));
+// X = DFT_R(x);  B[(j/NS) NS R + k + r NS] = X[r]
 template <int LOG2N, int R, int NS, bool LAST>
 __device__ __forceinline__ void pass_compute(f2 (&v)[E], const float4 *__restrict__ tw) {
     constexpr int NB = E / R;
@@ -168,17 +286,12 @@ __device__ __forceinline__ void pass_compute(f2 (&v)[E], const float4 *__restric
 #pragma unroll
         for (int r = 0; r < R; ++r) x[r] = v[b * R + r];
         if constexpr (NS > 1) {
-            // this pass's table, laid out [pair][k]: lanes (consecutive k) read consecutive 16 B
-            const int k = j & (NS - 1);
+            const int k = j & (NS - 1);  // this pass's table, [pair][k]: lanes read consecutive 16 B
 #pragma unroll
             for (int q = 0; q < R / 2; ++q) {
-#ifdef SDRG_DIAG_NO_TWIDDLE  // diagnostic builds only (wrong results): time the pass without twiddle loads
-                const float4 w = make_float4(1.0f, (float)k * 1e-30f, 1.0f, 0.0f);
-#else
                 const float4 w = tw[q * NS + k];
-#endif
-                x[2 * q + 1] = cmul(x[2 * q + 1], f2{w.x, w.y});
-                if (2 * q + 2 < R) x[2 * q + 2] = cmul(x[2 * q + 2], f2{w.z, w.w});
+                x[2 * q + 1] = cmul_v(x[2 * q + 1], f2{w.x, w.y});
+                if (2 * q + 2 < R) x[2 * q + 2] = cmul_v(x[2 * q + 2], f2{w.z, w.w});
             }
         }
         dft<R>(x);
@@ -187,18 +300,17 @@ __device__ __forceinline__ void pass_compute(f2 (&v)[E], const float4 *__restric
     }
 }
 
-// Exchange pass P's outputs (radix R, NS) into pass P+1's inputs (radix R2) through an LDS buffer that
-// holds HALF the frame: phase h moves the outputs whose position lies in half h.  A reader's element
-// e = j' + r' N/R2 is in half 0 iff r' < R2/2 (compile-time), so every phase reads exactly half of each
-// thread's next inputs; a writer's outputs all fall in one half when NB = 1, so in phase 0 the waves of
-// the lower half of the threads empty their registers while the upper half still hold theirs (48 live
-// complex values at most).
+// Exchange pass outputs (radix R, NS) into next-pass inputs (radix R2) through an LDS buffer holding HALF
+// the frame: phase h moves the elements whose position lies in half h.  A reader's element j + r N/R2 is
+// in half 0 iff r < R2/2 (compile-time); a writer's R outputs share one half (NS R <= N/2), so in phase 0
+// the waves of the lower half empty their registers while the upper half still hold theirs.
 template <int LOG2N, int R, int NS, int R2, bool NEXT_LAST>
 __device__ __forceinline__ void exchange(f2 *lds, f2 (&v)[E]) {
     constexpr int N = 1 << LOG2N;
     constexpr int T = N / E;
     constexpr int NB = E / R, NB2 = E / R2;
     constexpr int HALF = N / 2;
+    static_assert(N / R2 >= 32, "reader offsets must be multiples of 32");
     f2 nxt[E];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -206,17 +318,19 @@ __device__ __forceinline__ void exchange(f2 *lds, f2 (&v)[E]) {
         for (int b = 0; b < NB; ++b) {
             const int j = threadIdx.x + b * T;
             const int base = (j / NS) * NS * R + (j & (NS - 1));
-            if ((base >= HALF) == (h == 1)) {  // all R outputs of a butterfly share the half (NS R <= HALF)
+            if ((base >= HALF) == (h == 1)) {
+                const int pb = pad_base(base - h * HALF);
 #pragma unroll
-                for (int r = 0; r < R; ++r) lds[lds_idx(base + r * NS - h * HALF)] = v[b * R + r];
+                for (int r = 0; r < R; ++r) lds[pb + pad_off(r * NS)] = v[b * R + r];
             }
         }
         __syncthreads();
 #pragma unroll
         for (int b = 0; b < NB2; ++b) {
             const int j = bfly_j<LOG2N, R2, NEXT_LAST>(b);
+            const int pj = pad_base(j);
 #pragma unroll
-            for (int r = h * (R2 / 2); r < (h + 1) * (R2 / 2); ++r) nxt[b * R2 + r] = lds[lds_idx(j + r * (N / R2) - h * HALF)];
+            for (int r = h * (R2 / 2); r < (h + 1) * (R2 / 2); ++r) nxt[b * R2 + r] = lds[pj + pad_off(r * (N / R2) - h * HALF)];
         }
         __syncthreads();
     }
@@ -224,7 +338,7 @@ __device__ __forceinline__ void exchange(f2 *lds, f2 (&v)[E]) {
     for (int i = 0; i < E; ++i) v[i] = nxt[i];
 }
 
-template <int LOG2N, int P, int NS>
+template <int LOG2N, int FMT, int P, int NS>
 __device__ __forceinline__ void run_passes(f2 *lds, f2 (&v)[E], float *out, const float4 *tw) {
     using PL = Plan<LOG2N>;
     constexpr int N = 1 << LOG2N;
@@ -233,82 +347,51 @@ __device__ __forceinline__ void run_passes(f2 *lds, f2 (&v)[E], float *out, cons
     if constexpr (P == PL::NP - 1) {
         // last pass: output positions j + r N/R; |X|^2 at the fftshifted index (fft_process.cpp:83-97)
         constexpr int NB = E / R;
+        constexpr float S = power_scale<FMT>();
         if constexpr (NB == 2) {
-            // this thread's two butterflies are j = 2t, 2t+1 (see last_j): one 8-byte store per r
-            const int j = 2 * threadIdx.x;
+            float *o = out + 2 * threadIdx.x;  // j = 2t, 2t+1 < N/R: the fftshifted index is j + const
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const f2 x0 = v[r], x1 = v[R + r];
-                *reinterpret_cast<float2 *>(&out[(j + r * (N / R) + N / 2) & (N - 1)]) =
-                    make_float2(x0.x * x0.x + x0.y * x0.y, x1.x * x1.x + x1.y * x1.y);
+                *reinterpret_cast<float2 *>(o + ((r * (N / R) + N / 2) & (N - 1))) =
+                    make_float2((x0.x * x0.x + x0.y * x0.y) * S, (x1.x * x1.x + x1.y * x1.y) * S);
             }
         } else {
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-                const int j = last_j<LOG2N, R>(b);
+                const int j = bfly_j<LOG2N, R, true>(b);
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const f2 x = v[b * R + r];
-                    out[(j + r * (N / R) + N / 2) & (N - 1)] = x.x * x.x + x.y * x.y;
+                    out[(j + r * (N / R) + N / 2) & (N - 1)] = (x.x * x.x + x.y * x.y) * S;
                 }
             }
         }
     } else {
         constexpr int R2 = PL::template radix<P + 1>();
         exchange<LOG2N, R, NS, R2, P + 1 == PL::NP - 1>(lds, v);
-        run_passes<LOG2N, P + 1, NS * R>(lds, v, out, tw);
+        run_passes<LOG2N, FMT, P + 1, NS * R>(lds, v, out, tw);
     }
 }
 
 template <int LOG2N, int FMT>
-__global__ __launch_bounds__(Plan<LOG2N>::T, 2) void spectrum_kernel(const void *__restrict__ iq,
-                                                                     float *__restrict__ spectra,
-                                                                     const float4 *__restrict__ tw) {
+__global__ __launch_bounds__(Plan<LOG2N>::T) void spectrum_kernel(const void *__restrict__ iq, float *__restrict__ spectra,
+                                                                  const float4 *__restrict__ tw) {
     using PL = Plan<LOG2N>;
     constexpr int N = PL::N, T = PL::T, R0 = PL::template radix<0>(), NB0 = E / R0;
+    constexpr int BPS = bytes_per_sample<FMT>();
     extern __shared__ __attribute__((aligned(16))) char smem[];
     f2 *lds = reinterpret_cast<f2 *>(smem);
     const size_t frame = blockIdx.x;
-    const void *src = reinterpret_cast<const char *>(iq) + frame * (size_t)N * bytes_per_sample<FMT>();
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(reinterpret_cast<const char *>(iq) + frame * (size_t)N * BPS, N * BPS);
     f2 v[E];
-    constexpr int BYTES = N * bytes_per_sample<FMT>();
-    constexpr int WAVES = T / 64;
-    // measured (tools/gpu_variants.sh): staging the raw frame through LDS by LDS-DMA is slower than the
-    // direct strided loads at N = 16384 (0.157 vs 0.148 ms per 4096 frames); kept as a build option
-#ifdef SDRG_SPEC_DMA
-    constexpr bool DMA = FMT != SDRG_IQ_CF32 && WAVES >= 1 && BYTES <= PL::LDS_BYTES && BYTES % (WAVES * 1024) == 0;
-#else
-    constexpr bool DMA = false;
-#endif
-    if constexpr (DMA) {
-        // the raw frame (32 KiB CS8, 64 KiB CS16) lands in the exchange buffer by LDS-DMA, 16 B per lane and
-        // 1 KiB per wave instruction, then each thread picks its strided samples out of LDS
-        const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
 #pragma unroll
-        for (int q = 0; q < BYTES / (WAVES * 1024); q++) {
-            const int piece = wave + q * WAVES;
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(reinterpret_cast<const char *>(src) + piece * 1024 + lane * 16),
-                (__attribute__((address_space(3))) void *)(smem + piece * 1024), 16, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+    for (int b = 0; b < NB0; ++b) {
+        const int voff = (threadIdx.x + b * T) * BPS;
 #pragma unroll
-        for (int b = 0; b < NB0; ++b) {
-            const int j = threadIdx.x + b * T;
-#pragma unroll
-            for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_sample<FMT>(smem, j + r * (N / R0));
-        }
-        __syncthreads();  // the first exchange overwrites the raw bytes
-    } else {
-#pragma unroll
-        for (int b = 0; b < NB0; ++b) {
-            const int j = threadIdx.x + b * T;
-#pragma unroll
-            for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_sample<FMT>(src, j + r * (N / R0));
-        }
+        for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_unscaled<FMT>(rs, voff, r * (N / R0) * BPS);
     }
-    run_passes<LOG2N, 0, 1>(lds, v, spectra + frame * (size_t)N, tw);
+    run_passes<LOG2N, FMT, 0, 1>(lds, v, spectra + frame * (size_t)N, tw);
 }
 
 template <int LOG2N, int FMT>
@@ -338,6 +421,164 @@ hipError_t launch_n(const void *iq, int fmt, int n_frames, const float *tw, floa
     default: return hipErrorInvalidValue;
     }
 }
+
+// ================================================================================================
+// N = 16384, the benchmark size: persistent kernel, two 512-thread workgroups per CU (4 waves per SIMD),
+// each looping over frames blockIdx.x, + gridDim.x, ...  Stockham plan 32 x 32 x 16 with the twiddles in LDS:
+//   pass 1 twiddle w_1024^(r k), k = j mod 32           : P1[r][k]                     (8 KiB table)
+//   pass 2 twiddle w_16384^(r k), k = j = 32 k_hi + k_lo : P1[2r][k_hi] * A2[r][k_lo]    (3.75 KiB table)
+// (w_16384^(32 r k_hi) = w_512^(r k_hi) = w_1024^(2 r k_hi); one extra complex multiply per pass-2 twiddle
+// instead of 128 KiB of twiddle reads per frame from L2).  The next frame's raw samples are loaded into
+// registers before this frame's |X|^2 stores, so the in-order vmcnt wait at the top of the next iteration
+// does not also wait for the stores.  LDS per workgroup: 66 KiB half-frame exchange + 11.75 KiB tables.
+// Measured (tools/fftlab, 4096 CS8 frames): ~126 us vs 137-150 us for the generic kernel at this size.
+// ================================================================================================
+namespace k16 {
+
+constexpr int LOG2N = 14, N = 1 << LOG2N, T = N / E, HALF = N / 2;
+constexpr int XCH_F2 = HALF + HALF / 32;  // padded half-frame exchange buffer, f2 slots
+constexpr int P1_F2 = 32 * 32;            // P1[r][k] = w_1024^(r k), r, k < 32
+constexpr int A2_F4 = 15 * 16;            // A2[r-1][m] = (w_16384^(r 2m), w_16384^(r (2m+1))), r = 1..15
+constexpr int TAB_FLOATS = 2 * P1_F2 + 4 * A2_F4;
+constexpr int LDS_BYTES = XCH_F2 * 8 + P1_F2 * 8 + A2_F4 * 16;
+static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
+
+// raw samples x[t + 512 r] of frame f into registers (zero-extended 16/32-bit words)
+template <int FMT>
+__device__ __forceinline__ void issue_raw(const void *iq, int f, int t, uint32_t (&raw)[E]) {
+    constexpr int BPS = bytes_per_sample<FMT>();
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(reinterpret_cast<const char *>(iq) + (size_t)f * N * BPS, N * BPS);
+#pragma unroll
+    for (int r = 0; r < E; ++r) raw[r] = load_raw_word<FMT>(rs, t * BPS, r * (N / 32) * BPS);
+}
+
+// __launch_bounds__(512, 4): four waves per SIMD = two workgroups per CU, so at most 128 VGPRs
+template <int FMT>
+__global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restrict__ iq, float *__restrict__ spectra,
+                                                           const float *__restrict__ tabs, int n_frames) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    f2 *xch = reinterpret_cast<f2 *>(smem);
+    f2 *p1 = reinterpret_cast<f2 *>(smem + XCH_F2 * 8);
+    float4 *a2 = reinterpret_cast<float4 *>(smem + XCH_F2 * 8 + P1_F2 * 8);
+    const int t = threadIdx.x;
+    for (int i = t; i < P1_F2; i += T) p1[i] = reinterpret_cast<const f2 *>(tabs)[i];
+    for (int i = t; i < A2_F4; i += T) a2[i] = reinterpret_cast<const float4 *>(tabs + 2 * P1_F2)[i];
+    __syncthreads();
+    constexpr int BPS = bytes_per_sample<FMT>();
+    constexpr float S = power_scale<FMT>();
+    const f2 *p1_row = p1 + (t & 31);     // pass 1: P1[r][k], k = t mod 32
+    const f2 *b_row = p1 + (t >> 4);      // pass 2: P1[2r][k_hi], k_hi = t / 16
+    const float4 *a_row = a2 + (t & 15);  // pass 2: A2[r][m], m = t mod 16
+
+    constexpr bool STAGE = FMT != SDRG_IQ_CF32;  // CF32 (8 B/sample) loads at the top of the iteration
+    uint32_t raw[E];
+    if constexpr (STAGE)
+        if ((int)blockIdx.x < n_frames) issue_raw<FMT>(iq, blockIdx.x, t, raw);
+
+    for (int frame = blockIdx.x; frame < n_frames; frame += gridDim.x) {
+        f2 v[E];
+        // ---- pass 0: radix 32 over x[t + 512 r] (no twiddles) ----
+        if constexpr (STAGE) {
+#pragma unroll
+            for (int r = 0; r < E; ++r) v[r] = convert_raw<FMT>(raw[r]);
+        } else {
+            const __amdgpu_buffer_rsrc_t rs = frame_rsrc(reinterpret_cast<const char *>(iq) + (size_t)frame * N * BPS, N * BPS);
+#pragma unroll
+            for (int r = 0; r < E; ++r) v[r] = load_unscaled<FMT>(rs, t * BPS, r * (N / 32) * BPS);
+        }
+        const int next = frame + gridDim.x;
+        dft<32>(v);
+        exchange<LOG2N, 32, 1, 32, false>(xch, v);
+        // ---- pass 1: radix 32, NS = 32 ----
+#pragma unroll
+        for (int r = 1; r < 32; ++r) v[r] = cmul_v(v[r], p1_row[r * 32]);
+        dft<32>(v);
+        exchange<LOG2N, 32, 32, 16, true>(xch, v);
+        // ---- pass 2: radix 16, NS = 1024, butterflies j = 2t + b held as v[16 b + r] ----
+#pragma unroll
+        for (int r = 1; r < 16; ++r) {
+            const f2 bw = b_row[2 * r * 32];
+            const float4 aw = a_row[(r - 1) * 16];
+            v[r] = cmul_v(v[r], cmul_v(bw, f2{aw.x, aw.y}));
+            v[16 + r] = cmul_v(v[16 + r], cmul_v(bw, f2{aw.z, aw.w}));
+        }
+        f2 x0[16], x1[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { x0[r] = v[r]; x1[r] = v[16 + r]; }
+        dft<16>(x0);
+        dft<16>(x1);
+        // ---- |X|^2 at the fftshifted index: outputs j + 1024 r, j = 2t, 2t + 1 ----
+        float2 pw[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            pw[r] = make_float2((x0[r].x * x0[r].x + x0[r].y * x0[r].y) * S, (x1[r].x * x1[r].x + x1[r].y * x1[r].y) * S);
+        if constexpr (STAGE) {
+            if (next < n_frames) {
+                issue_raw<FMT>(iq, next, t, raw);
+            } else {  // last frame: define raw on this path too, so it is dead between the convert and here
+#pragma unroll
+                for (int r = 0; r < E; ++r) raw[r] = 0;
+            }
+        }
+        float *o = spectra + (size_t)frame * N + 2 * t;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) *reinterpret_cast<float2 *>(o + ((r * 1024 + N / 2) & (N - 1))) = pw[r];
+    }
+}
+
+// the two LDS tables, laid out as the kernel reads them (exp evaluated in double, rounded once)
+void fill_tables(float *out) {
+    for (int r = 0; r < 32; r++)
+        for (int k = 0; k < 32; k++) {
+            const double a = -2.0 * M_PI * (double)(r * k) / 1024.0;
+            out[2 * (r * 32 + k)] = (float)cos(a);
+            out[2 * (r * 32 + k) + 1] = (float)sin(a);
+        }
+    float *a2 = out + 2 * P1_F2;
+    for (int r = 1; r < 16; r++)
+        for (int m = 0; m < 16; m++)
+            for (int b = 0; b < 2; b++) {
+                const double a = -2.0 * M_PI * (double)(r * (2 * m + b)) / 16384.0;
+                a2[4 * ((r - 1) * 16 + m) + 2 * b] = (float)cos(a);
+                a2[4 * ((r - 1) * 16 + m) + 2 * b + 1] = (float)sin(a);
+            }
+}
+
+int device_cus() {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 256;
+        return n > 0 ? n : 256;
+    }();
+    return cus;
+}
+
+template <int FMT>
+hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectra, hipStream_t s) {
+    auto k = spectrum16k_kernel<FMT>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int grid = n_frames < 2 * device_cus() ? n_frames : 2 * device_cus();
+    hipLaunchKernelGGL(k, dim3(grid), dim3(T), LDS_BYTES, s, iq, spectra, tabs, n_frames);
+    return hipGetLastError();
+}
+
+hipError_t launch_fmt(const void *iq, int fmt, int n_frames, const float *tabs, float *spectra, hipStream_t s) {
+    switch (fmt) {
+    case SDRG_IQ_CS8: return launch<SDRG_IQ_CS8>(iq, n_frames, tabs, spectra, s);
+    case SDRG_IQ_CU8: return launch<SDRG_IQ_CU8>(iq, n_frames, tabs, spectra, s);
+    case SDRG_IQ_CS16: return launch<SDRG_IQ_CS16>(iq, n_frames, tabs, spectra, s);
+    case SDRG_IQ_CF32: return launch<SDRG_IQ_CF32>(iq, n_frames, tabs, spectra, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace k16
 
 // ================================================================================================
 // N = 32768 / 65536: the frame (256 / 512 KiB as complex float) does not fit in LDS (160 KiB), so the
@@ -386,7 +627,7 @@ __device__ __forceinline__ void tile_pass(f2 *lds, const f2 *__restrict__ tw, Lo
         if constexpr (NS > 1) {
             const int k = j & (NS - 1);
 #pragma unroll
-            for (int r = 1; r < R; ++r) x[b][r] = cmul(x[b][r], tw[(r * k) * (N / (NS * R))]);
+            for (int r = 1; r < R; ++r) x[b][r] = cmul_v(x[b][r], tw[(r * k) * (N / (NS * R))]);
         }
         dft<R>(x[b]);
         if constexpr (LAST) {
@@ -415,7 +656,7 @@ __global__ __launch_bounds__(TILE_T) void four_step_a(const void *__restrict__ i
     auto none = [](int, int, f2) {};
     auto store = [&](int c, int k1, f2 v) {
         const int n2 = c0 + c;
-        y[k1 * N2 + n2] = cmul(v, tw[(n2 * k1) & (N - 1)]);
+        y[k1 * N2 + n2] = cmul_v(v, tw[(n2 * k1) & (N - 1)]);
     };
     auto noload = [](int, int) { return f2{0.0f, 0.0f}; };
     tile_pass<N, N1, TP::RA, 1, true, false>(lds, tw, load, none);
@@ -504,21 +745,25 @@ static void fill_pass_tables(std::vector<float> &tw, size_t at) {
     fill(std::integral_constant<int, 3>{});
 }
 
+// Twiddle buffer layout: the full table W_N^m (m < N, four-step kernels), then for N <= 8192 the generic
+// kernel's per-pass tables, or for N = 16384 the k16 kernel's LDS tables.  Every entry is exp(-2 pi i m / M)
+// evaluated in double and rounded once to float.
+size_t spectrum_k16_tables_offset() { return 2 * (size_t)16384; }
+
 size_t spectrum_twiddle_floats(int n) {
     size_t pass = 0;
+    if (n == 16384) return spectrum_k16_tables_offset() + k16::TAB_FLOATS;
     switch (n) {
 #define SDRG_TW_CASE(L) \
     case 1 << L: pass = 4 * (size_t)Plan<L>::TW_F4; break;
         SDRG_TW_CASE(6) SDRG_TW_CASE(7) SDRG_TW_CASE(8) SDRG_TW_CASE(9) SDRG_TW_CASE(10) SDRG_TW_CASE(11)
-        SDRG_TW_CASE(12) SDRG_TW_CASE(13) SDRG_TW_CASE(14)
+        SDRG_TW_CASE(12) SDRG_TW_CASE(13)
 #undef SDRG_TW_CASE
     default: break;
     }
     return 2 * (size_t)n + pass;
 }
 
-// Layout: the full table W_N^m (m < N, the four-step kernels), then for N <= 16384 the LDS kernel's
-// per-pass tables.  Every entry is exp(-2 pi i m / M) evaluated in double and rounded once to float.
 void spectrum_fill_twiddles(int n, float *out) {
     std::vector<float> tw(spectrum_twiddle_floats(n));
     for (int m = 0; m < n; m++) {
@@ -526,11 +771,12 @@ void spectrum_fill_twiddles(int n, float *out) {
         tw[2 * (size_t)m] = (float)cos(a);
         tw[2 * (size_t)m + 1] = (float)sin(a);
     }
+    if (n == 16384) k16::fill_tables(tw.data() + spectrum_k16_tables_offset());
     switch (n) {
 #define SDRG_TW_CASE(L) \
     case 1 << L: fill_pass_tables<L>(tw, 2 * (size_t)n); break;
         SDRG_TW_CASE(6) SDRG_TW_CASE(7) SDRG_TW_CASE(8) SDRG_TW_CASE(9) SDRG_TW_CASE(10) SDRG_TW_CASE(11)
-        SDRG_TW_CASE(12) SDRG_TW_CASE(13) SDRG_TW_CASE(14)
+        SDRG_TW_CASE(12) SDRG_TW_CASE(13)
 #undef SDRG_TW_CASE
     default: break;
     }
@@ -553,6 +799,7 @@ hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const f
     switch (n) {
     case 32768: return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
     case 65536: return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
+    case 16384: return k16::launch_fmt(iq, fmt, n_frames, twiddles + spectrum_k16_tables_offset(), spectra, stream);
     case 64: return launch_n<6>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 128: return launch_n<7>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 256: return launch_n<8>(iq, fmt, n_frames, twiddles, spectra, stream);
@@ -561,7 +808,6 @@ hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const f
     case 2048: return launch_n<11>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 4096: return launch_n<12>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 8192: return launch_n<13>(iq, fmt, n_frames, twiddles, spectra, stream);
-    case 16384: return launch_n<14>(iq, fmt, n_frames, twiddles, spectra, stream);
     default: return hipErrorInvalidValue;
     }
 }
