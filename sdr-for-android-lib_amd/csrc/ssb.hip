@@ -256,7 +256,7 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 //   SIMD3: load, FIR (slot group 0), FIR (slot group 1)
 // ================================================================================================
 constexpr int PG = 16;          // streams per workgroup
-constexpr int CH = 32;          // samples per chunk
+constexpr int CH = 64;          // samples per chunk
 constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_read_b128 by stream lanes
 constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
 constexpr int PIPE_WAVES = 12;
@@ -266,20 +266,22 @@ enum PipeWave : int { W_DC = 0, W_LPF = 1, W_AGC = 2, W_LOAD = 3, W_FIR0 = 4, W_
 // role of hardware wave w = nibble w: w0 DC, w1 LPF, w2 AGC, w3 load, w4 OUT, w5 EQ, w6 DES2, w7 FIR0,
 // w8 DES0, w9 DES1, w10 DES3, w11 FIR1
 constexpr unsigned long long DEFAULT_ROLE_MAP = 0x7B984A653210ull;
-constexpr int MAX_SLOTS = 16;   // concurrent FIR outputs per stream (2 per FIR lane)
-constexpr int MAX_DONE = 4;     // FIR outputs completed per stream per chunk
+constexpr int MAX_SLOTS = 32;   // concurrent FIR outputs per stream (up to 4 per FIR lane)
+constexpr int MAX_DONE = 8;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
 
 constexpr int TAPS_ROW = CH + 256 + CH + 4;
 constexpr int RAW_U4 = PG * 32;  // one prefetch batch: 512 B per stream = 32 uint4, as [piece 8][lane 64]
 
 template <int FMT>
-constexpr int batch_chunks() {  // chunks per 512-B-per-stream prefetch batch
-    return FMT == SDRG_IQ_CF32 ? 2 : FMT == SDRG_IQ_CS16 ? 4 : 8;
+constexpr int batch_chunks() {  // chunks per 512-B-per-stream prefetch batch (DMA needs CH * bps <= 512)
+    constexpr int b = 512 / (CH * (FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2));
+    return b > 0 ? b : 1;
 }
+constexpr int NRAW = 3;  // raw-IQ batches in LDS: one being unpacked, two in flight
 
 struct PipeLds {
-    uint4 raw[2][RAW_U4];  // raw IQ bytes of two prefetch batches (LDS-DMA), [piece][loader lane]
+    uint4 raw[NRAW][RAW_U4];  // raw IQ bytes of the prefetch batches (LDS-DMA), [piece][loader lane]
     float re[2][BUFF];
     float a[2][BUFF];
     float y[4][BUFF];
@@ -314,17 +316,39 @@ __device__ __forceinline__ void load_i8_masked(const char *frame, int t, int n_i
     }
 }
 
-__device__ __forceinline__ void read_row(const float *row, float (&v)[CH]) {
+// A serial role's pass over one stream's chunk row in sub-blocks of SB samples, double-buffered in registers:
+// sub-block i + 1 is read from LDS while sub-block i runs through the recurrence, so the LDS latency is off
+// the recurrence's critical path.  step(v) updates the role's carried state and v in place; the results go
+// to dst when store (lanes that hold a stream's first copy).
+constexpr int SB = 32;
+template <class Step>
+__device__ __forceinline__ void row_pipeline(const float *src, float *dst, bool store, Step step) {
+    constexpr int NSB = CH / SB;
+    static_assert(NSB % 2 == 0, "pairs of sub-blocks");
+    float va[SB], vb[SB];
+    auto rd = [&](const float *r, float (&v)[SB]) {
 #pragma unroll
-    for (int i = 0; i < CH; i += 4) {
-        const float4 r = *reinterpret_cast<const float4 *>(row + i);
-        v[i] = r.x; v[i + 1] = r.y; v[i + 2] = r.z; v[i + 3] = r.w;
+        for (int i = 0; i < SB; i += 4) {
+            const float4 x = *reinterpret_cast<const float4 *>(r + i);
+            v[i] = x.x; v[i + 1] = x.y; v[i + 2] = x.z; v[i + 3] = x.w;
+        }
+    };
+    auto wr = [&](float *r, const float (&v)[SB]) {
+        if (store) {
+#pragma unroll
+            for (int i = 0; i < SB; i += 4) *reinterpret_cast<float4 *>(r + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+        }
+    };
+    rd(src, va);
+#pragma unroll
+    for (int sb = 0; sb < NSB; sb += 2) {
+        rd(src + SB * (sb + 1), vb);
+        step(va);
+        wr(dst + SB * sb, va);
+        if (sb + 2 < NSB) rd(src + SB * (sb + 2), va);
+        step(vb);
+        wr(dst + SB * (sb + 1), vb);
     }
-}
-
-__device__ __forceinline__ void write_row(float *row, const float (&v)[CH]) {
-#pragma unroll
-    for (int i = 0; i < CH; i += 4) *reinterpret_cast<float4 *>(row + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
 }
 
 // The FIR slots of one stream over one chunk: lane = (stream, sub); slot 4j+sub holds the output o active
@@ -352,7 +376,7 @@ __device__ __forceinline__ void fir_chunk(PipeLds &L, int c, int t0, int o_lo, i
         k0[j] = active[j] ? (t0 - base + CH) : 0;  // taps_pad index of step 0 (inactive: the zero padding)
     }
     const float4 *in = reinterpret_cast<const float4 *>(&L.out[c & 1][sl * ROW]);  // 0 beyond frame end
-#pragma unroll
+#pragma unroll 4
     for (int i = 0; i < CH / 4; i++) {
         const float4 x = in[i];
         f2v lo[NP], hi[NP];
@@ -378,9 +402,7 @@ __device__ __forceinline__ void fir_chunk(PipeLds &L, int c, int t0, int o_lo, i
 }
 
 template <int FMT, bool DMA>
-// waves_per_eu(6): at most 80 VGPRs, so 3 pipeline waves (240) plus a spectrum workgroup's 2 waves of 128
-// fit one SIMD's 512 and the FFT of the same step runs on the same CUs
-__global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
+__global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
                                                           int nsl_mask, const int4 *__restrict__ chunk_out,
                                                           const float *__restrict__ taps,
                                                           SsbStreamState *__restrict__ state,
@@ -403,7 +425,7 @@ __global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) voi
         L.taps_sh[sh][j] = (k >= 0 && k < NT) ? taps[k] : 0.0f;
     }
 
-    const int my_s = lane;  // serial roles: lane = stream within the group
+    const int my_s = lane & (PG - 1);  // serial roles: lane = 16 x copy + stream (all 64 lanes run; lanes < PG store)
     const float demod_k = p.upper ? 2.0f : 0.0f;  // demodSSB(y, y) = y + y or y - y (:89-94) as y * k
     const bool serial_live = (wave < 3 || wave == W_EQ) && (lane < PG) && (s0 + lane < n_frames);
     const bool high = (prio_mask >> wave) & 1;  // masks are per role  // default: the recurrences (waves 0-2) own their SIMD's issue slots
@@ -425,11 +447,13 @@ __global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) voi
 #pragma unroll
         for (int q = 0; q < 8; q++)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + 16 * q),
-                                             (__attribute__((address_space(3))) void *)&L.raw[kb & 1][q * 64], 16, 0, 0);
+                                             (__attribute__((address_space(3))) void *)&L.raw[kb % NRAW][q * 64], 16, 0, 0);
     };
     if constexpr (DMA) {
         if (wave == W_LOAD && n_batches > 0) issue_batch(0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wave == W_LOAD && n_batches > 1) issue_batch(1);
+        if (n_batches > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // batch 0 landed, 1 in flight
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 
@@ -455,58 +479,56 @@ __global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) voi
         chunk_loop([&](int it) {
             // ---- removeDC (:49-55) and the a0*x term of iir2Process, chunk it-1 ----
             const int c = it - 1;
-            if (c >= 0 && c < nch && lane < PG) {
-                float v[CH];
-                read_row(&L.re[c & 1][my_s * ROW], v);
+            if (c >= 0 && c < nch) {
                 // the frame's last chunk runs whole too: dc restarts every frame and the samples past the
                 // frame end (zeros from the loader) only feed outputs nothing reads
                 const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
+                row_pipeline(&L.re[c & 1][my_s * ROW], &L.a[c & 1][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
-                for (int q = 0; q < CH; q++) {
-                    dc = alpha * dc + one_minus * v[q];
-                    v[q] = a0 * (v[q] - dc);
-                }
-                write_row(&L.a[c & 1][my_s * ROW], v);
+                    for (int q = 0; q < SB; q++) {
+                        dc = alpha * dc + one_minus * v[q];
+                        v[q] = a0 * (v[q] - dc);
+                    }
+                });
             }
         });
     } else if (wave == W_LPF) {
         float z1 = 0.0f, z2 = 0.0f;  // rfFilter state, carried across frames
-        if (serial_live) {
+        if (s0 + my_s < n_frames) {
             z1 = state[s0 + my_s].lpf_z1;
             z2 = state[s0 + my_s].lpf_z2;
         }
+        // y = ((((a0 x + a1 z1) + a2 z2) - b1 z1) - b2 z2): the four products as two packed multiplies (each
+        // lane of v_pk_mul_f32 rounds like v_mul_f32), the adds in order; the subtractions are additions of
+        // (-b) z (a - b == a + (-b) exactly, and (-b) z == -(b z))
+        const f2v c1 = {p.lpf[1], -p.lpf[3]}, c2 = {p.lpf[2], -p.lpf[4]};
         chunk_loop([&](int it) {
             // ---- iir2Process recurrence (:75-84), chunk it-2 ----
             const int c = it - 2;
-            if (c >= 0 && c < nch && lane < PG) {
-                float v[CH];
-                read_row(&L.a[c & 1][my_s * ROW], v);
+            if (c >= 0 && c < nch) {
                 const int lim = min(CH, S - c * CH);
-                // y = ((((a0 x + a1 z1) + a2 z2) - b1 z1) - b2 z2): the four products as two packed
-                // multiplies (each lane of v_pk_mul_f32 rounds like v_mul_f32), the adds in order
-                const f2v c1 = {p.lpf[1], p.lpf[3]}, c2 = {p.lpf[2], p.lpf[4]};
                 if (lim == CH) {
+                    row_pipeline(&L.a[c & 1][my_s * ROW], &L.y[c & 3][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
-                    for (int q = 0; q < CH; q++) {
-                        const f2v p1 = c1 * z1, p2 = c2 * z2;
-                        const float y = (((v[q] + p1.x) + p2.x) - p1.y) - p2.y;
-                        z2 = z1;
-                        z1 = y;
-                        v[q] = y;
-                    }
-                } else {
-#pragma unroll
-                    for (int q = 0; q < CH; q++) {
-                        if (q < lim) {
+                        for (int q = 0; q < SB; q++) {
                             const f2v p1 = c1 * z1, p2 = c2 * z2;
-                            const float y = (((v[q] + p1.x) + p2.x) - p1.y) - p2.y;
+                            const float y = (((v[q] + p1.x) + p2.x) + p1.y) + p2.y;
                             z2 = z1;
                             z1 = y;
                             v[q] = y;
                         }
+                    });
+                } else {
+                    // the frame's last, partial chunk (S not a multiple of CH): sample by sample through LDS,
+                    // so the carried state is the one after exactly S samples
+                    for (int q = 0; q < lim; q++) {
+                        const f2v p1 = c1 * z1, p2 = c2 * z2;
+                        const float y = (((L.a[c & 1][my_s * ROW + q] + p1.x) + p2.x) + p1.y) + p2.y;
+                        z2 = z1;
+                        z1 = y;
+                        if (lane < PG) L.y[c & 3][my_s * ROW + q] = y;
                     }
                 }
-                write_row(&L.y[c & 3][my_s * ROW], v);
             }
         });
         if (serial_live) {
@@ -515,67 +537,76 @@ __global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) voi
         }
     } else if (wave == W_AGC) {
         float gain = 1.0f;  // adaptiveAGC: reset per call (:102)
+        // gain = gain*(1-rate) + desired*rate, rate = desired < gain ? fast : slow: both candidates (fast,
+        // slow) in one packed lane pair, then the select.  The last chunk runs whole: gain restarts every
+        // frame and outputs past the frame end are zeroed by the clamp role.
+        const f2v rates = {p.agc_fast, 0.00035f};
+        const f2v keep = {1.0f - p.agc_fast, 1.0f - 0.00035f};
         chunk_loop([&](int it) {
             // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
             const int c = it - 4;
-            if (c >= 0 && c < nch && lane < PG) {
-                float v[CH];
-                read_row(&L.d[c & 1][my_s * ROW], v);
-                // gain = gain*(1-rate) + desired*rate, rate = desired < gain ? fast : slow: both candidates
-                // (fast, slow) in one packed lane pair, then the select.  The last chunk runs whole: gain
-                // restarts every frame and outputs past the frame end are zeroed by the clamp role.
-                const f2v rates = {p.agc_fast, 0.00035f};
-                const f2v keep = {1.0f - p.agc_fast, 1.0f - 0.00035f};
+            if (c >= 0 && c < nch) {
+                row_pipeline(&L.d[c & 1][my_s * ROW], &L.g[c & 1][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
-                for (int q = 0; q < CH; q++) {
-                    const float desired = v[q];
-                    const f2v cand = gain * keep + desired * rates;
-                    gain = (desired < gain) ? cand.x : cand.y;
-                    v[q] = gain;
-                }
-                write_row(&L.g[c & 1][my_s * ROW], v);
+                    for (int q = 0; q < SB; q++) {
+                        const float desired = v[q];
+                        const f2v cand = gain * keep + desired * rates;
+                        gain = (desired < gain) ? cand.x : cand.y;
+                        v[q] = gain;
+                    }
+                });
             }
         });
     } else if (wave == W_LOAD) {
         chunk_loop([&](int it) {
             if constexpr (DMA) {
-                // batch it/BC + 1 starts moving now; it must have landed before the barrier that ends
-                // the batch's last-but-one iteration (only this wave's DMAs are counted by its vmcnt)
-                if (it % BC == 0 && it / BC + 1 < n_batches) issue_batch(it / BC + 1);
-                if (it % BC == BC - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // batch kb + 2 starts moving when batch kb's first chunk is unpacked (its buffer held batch
+                // kb - 1); batch kb + 1 must have landed before the barrier that ends batch kb's last
+                // iteration: wait until at most batch kb + 2's 8 DMAs are outstanding (only this wave's
+                // DMAs are counted by its vmcnt)
+                const int kb = it / BC;
+                if (it % BC == 0 && kb + 2 < n_batches) issue_batch(kb + 2);
+                if (it % BC == BC - 1) {
+                    if (kb + 2 < n_batches) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             }
-            // ---- unpack the I channel of chunk it (lane = 4 x stream + part of 8 samples) ----
+            // ---- unpack the I channel of chunk it (lane = 4 x stream + part of CH/4 samples) ----
             {
                 const int c = it;
                 if (c < nch) {
                     const int sl = lane >> 2, part = lane & 3;
-                    const int t = c * CH + part * 8;
-                    float x[8];
-                    if constexpr (DMA) {
-                        constexpr int U4 = 8 * (int)bytes_per_sample<FMT>() / 16;  // 16-B pieces per 8 samples
-                        const int off = ((c % BC) * CH + part * 8) * (int)bytes_per_sample<FMT>();
-                        const int quarter = off >> 7, piece = (off & 127) >> 4;
-                        uint4 u[U4];
 #pragma unroll
-                        for (int q = 0; q < U4; q++) u[q] = L.raw[(c / BC) & 1][(piece + q) * 64 + sl * 4 + quarter];
-                        unpack_i8<FMT>(u, x);
-                    } else {
-                        if (s0 + sl < n_frames) {
-                            const char *frame = iq + (size_t)(s0 + sl) * p.n_in * bps;
-                            load_i8_masked<FMT>(frame, t, n_live, x);
+                    for (int g8 = 0; g8 < CH / 32; ++g8) {
+                        const int within = part * (CH / 4) + g8 * 8;
+                        const int t = c * CH + within;
+                        float x[8];
+                        if constexpr (DMA) {
+                            constexpr int U4 = 8 * (int)bytes_per_sample<FMT>() / 16;  // 16-B pieces per 8 samples
+                            const int off = ((c % BC) * CH + within) * (int)bytes_per_sample<FMT>();
+                            const int quarter = off >> 7, piece = (off & 127) >> 4;
+                            uint4 u[U4];
+#pragma unroll
+                            for (int q = 0; q < U4; q++) u[q] = L.raw[(c / BC) % NRAW][(piece + q) * 64 + sl * 4 + quarter];
+                            unpack_i8<FMT>(u, x);
+                        } else {
+                            if (s0 + sl < n_frames) {
+                                const char *frame = iq + (size_t)(s0 + sl) * p.n_in * bps;
+                                load_i8_masked<FMT>(frame, t, n_live, x);
+                            }
                         }
-                    }
 #pragma unroll
-                    for (int q = 0; q < 8; q++)
-                        if (t + q >= n_live || s0 + sl >= n_frames) x[q] = 0.0f;  // iq.resize() zero padding
-                    float *dst = &L.re[c & 1][sl * ROW + part * 8];
-                    *reinterpret_cast<float4 *>(dst) = make_float4(x[0], x[1], x[2], x[3]);
-                    *reinterpret_cast<float4 *>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
+                        for (int q = 0; q < 8; q++)
+                            if (t + q >= n_live || s0 + sl >= n_frames) x[q] = 0.0f;  // iq.resize() zero padding
+                        float *dst = &L.re[c & 1][sl * ROW + within];
+                        *reinterpret_cast<float4 *>(dst) = make_float4(x[0], x[1], x[2], x[3]);
+                        *reinterpret_cast<float4 *>(dst + 4) = make_float4(x[4], x[5], x[6], x[7]);
+                    }
                 }
             }
         });
     } else if (wave == W_FIR0 || wave == W_FIR1) {
-        float facc[MAX_SLOTS / 4] = {0.0f, 0.0f, 0.0f, 0.0f};  // FIR accumulators (slots j*4 + lane/16)
+        float facc[MAX_SLOTS / 4] = {};  // FIR accumulators (slots j*4 + lane/16)
         chunk_loop([&](int it) {
             // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot mod 4, stream); slot groups
             //      4j..4j+3 split between the two FIR waves ----
@@ -585,10 +616,12 @@ __global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) voi
                 const int sl = lane % PG, sub = lane / PG;
                 const int t0 = c * CH;
                 if (wave == W_FIR0) {
-                    if (nsl_mask == 15) fir_chunk<2, 0>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
+                    if (nsl_mask == 31) fir_chunk<4, 0>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
+                    else if (nsl_mask == 15) fir_chunk<2, 0>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
                     else fir_chunk<1, 0>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
                 } else {
-                    if (nsl_mask == 15) fir_chunk<2, 2>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
+                    if (nsl_mask == 31) fir_chunk<4, 4>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
+                    else if (nsl_mask == 15) fir_chunk<2, 2>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
                     else if (nsl_mask == 7) fir_chunk<1, 1>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
                 }
             }
@@ -599,12 +632,13 @@ __global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) voi
             // lane = 4 x stream + part of 8 samples.  x = demodSSB(y, y) = y + y (upper) or y - y (lower)
             // is y * 2 or y * 0: equal values (the lower sideband's zero may carry y's sign, which the
             // clamp keeps and the FIR's sums absorb: acc + (+-0) == acc).  clamp == med3 for non-NaN input.
-            {
-                const int c = it - 5;
-                if (c >= 0 && c < nch) {
-                    const int sl = lane >> 2, part = lane & 3;
-                    const float *yr = &L.y[c & 3][sl * ROW + part * 8];
-                    const float *gr = &L.g[c & 1][sl * ROW + part * 8];
+            const int c = it - 5;
+            if (c >= 0 && c < nch) {
+#pragma unroll
+                for (int g8 = 0; g8 < CH / 32; ++g8) {
+                    const int sl = lane >> 2, part = lane & 3, within = part * (CH / 4) + g8 * 8;
+                    const float *yr = &L.y[c & 3][sl * ROW + within];
+                    const float *gr = &L.g[c & 1][sl * ROW + within];
                     const float4 ya = *reinterpret_cast<const float4 *>(yr), yb = *reinterpret_cast<const float4 *>(yr + 4);
                     const float4 ga = *reinterpret_cast<const float4 *>(gr), gb = *reinterpret_cast<const float4 *>(gr + 4);
                     const f2v k2 = {demod_k, demod_k};
@@ -616,14 +650,14 @@ __global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) voi
                         o[q].y = __builtin_amdgcn_fmed3f(o[q].y, -1.0f, 1.0f);
                     }
                     if (c * CH + CH > S) {  // the last chunk only: the FIR reads whole chunks
-                        const int t = c * CH + part * 8;
+                        const int t = c * CH + within;
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
                             if (t + 2 * q >= S) o[q].x = 0.0f;
                             if (t + 2 * q + 1 >= S) o[q].y = 0.0f;
                         }
                     }
-                    float *dst = &L.out[c & 1][sl * ROW + part * 8];
+                    float *dst = &L.out[c & 1][sl * ROW + within];
                     *reinterpret_cast<float4 *>(dst) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
                     *reinterpret_cast<float4 *>(dst + 4) = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
                 }
@@ -665,18 +699,22 @@ __global__ __launch_bounds__(PIPE_T) __attribute__((amdgpu_waves_per_eu(6))) voi
         }
     } else {
         chunk_loop([&](int it) {
-            // waves 8-11: lane = 2 consecutive samples of one stream (256 lanes x 2 = the 16 x 32 chunk)
+            // waves 8-11: lane = CH/16 consecutive samples of one stream (256 lanes = the 16 x CH chunk)
+            constexpr int SPL = CH / 16;
             const int hl = (wave == W_DES0 ? 0 : wave == W_DES1 ? 1 : wave == W_DES2 ? 2 : 3) * 64 + lane;
-            const int sl = hl / (CH / 2), i2 = (hl % (CH / 2)) * 2;
+            const int sl = hl / (CH / SPL), i0 = (hl % (CH / SPL)) * SPL;
             // ---- AGC "desired" level (:104-107), chunk it-3 ----
             const int c = it - 3;
             if (c >= 0 && c < nch) {
-                const float2 y2 = *reinterpret_cast<const float2 *>(&L.y[c & 3][sl * ROW + i2]);
-                // fabsf(demodSSB(y, y)) == |y| * k exactly (k = 2 or 0)
-                const f2v a = f2v{fabsf(y2.x), fabsf(y2.y)} * f2v{demod_k, demod_k};
-                // target / (sqrtf(fabsf(a) + 1e-8f) + 1e-6f), correctly rounded, two lanes per op (ssb_math.h)
-                const f2v d = agc_desired_abs2(a, p.agc_target);
-                *reinterpret_cast<float2 *>(&L.d[c & 1][sl * ROW + i2]) = make_float2(d.x, d.y);
+#pragma unroll
+                for (int h = 0; h < SPL; h += 2) {
+                    const float2 y2 = *reinterpret_cast<const float2 *>(&L.y[c & 3][sl * ROW + i0 + h]);
+                    // fabsf(demodSSB(y, y)) == |y| * k exactly (k = 2 or 0)
+                    const f2v a = f2v{fabsf(y2.x), fabsf(y2.y)} * f2v{demod_k, demod_k};
+                    // target / (sqrtf(fabsf(a) + 1e-8f) + 1e-6f), correctly rounded, two lanes per op (ssb_math.h)
+                    const f2v d = agc_desired_abs2(a, p.agc_target);
+                    *reinterpret_cast<float2 *>(&L.d[c & 1][sl * ROW + i0 + h]) = make_float2(d.x, d.y);
+                }
             }
         });
     }
@@ -788,10 +826,10 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         const dim3 grid((n_frames + PG - 1) / PG);
         const size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
         const int bps = fmt == SDRG_IQ_CF32 ? 8 : fmt == SDRG_IQ_CS16 ? 4 : 2;
-        const int bc = fmt == SDRG_IQ_CF32 ? 2 : fmt == SDRG_IQ_CS16 ? 4 : 8;
+        const int bc = 512 / (CH * bps) > 0 ? 512 / (CH * bps) : 1;  // batch_chunks<FMT>()
         const int n_live = p.n_in < p.samp_count ? p.n_in : p.samp_count;
         // LDS-DMA batches need whole 16-B pieces inside every frame
-        const bool dma = (n_live % (bc * CH)) == 0 && ((size_t)p.n_in * bps) % 16 == 0 &&
+        const bool dma = CH * bps <= 512 && (n_live % (bc * CH)) == 0 && ((size_t)p.n_in * bps) % 16 == 0 &&
                          (reinterpret_cast<uintptr_t>(iq) & 15) == 0;
         unsigned long long *stamps = ssb_stamps_buffer(n_frames);
         static const int prio_mask = [] {  // diagnostic override: SDRG_PIPE_PRIO = bit mask of high-priority waves
