@@ -182,7 +182,7 @@ def main() -> int:
     spec_ms = ts["spectrum_ms"]
     alg_bytes = ALG_BYTES_PER_SAMPLE["spectrum"] * streams * N
     achieved = alg_bytes / (spec_ms * 1e-3) / 1e9 if spec_ms > 0 else 0.0
-    traffic = pmc_traffic("spectrum_kernel", streams)
+    traffic = pmc_traffic("spectrum16k_kernel", streams)
     out = {
         "metric": "IQ Msamples/s (16384-pt FFT+SSB) at 1/2/4/8 GPUs; % HBM roofline",
         "value": round(value, 2),
@@ -202,7 +202,7 @@ def main() -> int:
                    "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (", RCCL gather of records"
                                                                                          if world > 1 else "")},
         "kernel_ms": {k: round(v, 4) for k, v in ts.items() if k != "count"},
-        "roofline": {"kernel": "spectrum (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
+        "roofline": {"kernel": "spectrum16k_kernel (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic[0] if traffic else None,

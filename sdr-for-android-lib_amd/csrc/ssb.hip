@@ -256,6 +256,12 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 //   SIMD3: load, FIR (slot group 0), FIR (slot group 1)
 // ================================================================================================
 constexpr int PG = 16;          // streams per workgroup
+// serial roles (bit 0 DC, 1 LPF, 2 AGC) that run on all 64 lanes (16 copies of the 16 streams) instead of the
+// first 16: a dependent VALU chain issues faster with the full EXEC mask, while the LDS reads of 16 copies cost
+// more LDS cycles (tools/microbench/valu5.hip, valu6.hip; tools/build_variant.sh for the trade per role)
+#ifndef SDRG_SERIAL_FULL_EXEC
+#define SDRG_SERIAL_FULL_EXEC 0x0
+#endif
 constexpr int CH = 64;          // samples per chunk
 constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_read_b128 by stream lanes
 constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
@@ -479,7 +485,7 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
         chunk_loop([&](int it) {
             // ---- removeDC (:49-55) and the a0*x term of iir2Process, chunk it-1 ----
             const int c = it - 1;
-            if (c >= 0 && c < nch) {
+            if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 1) || lane < PG)) {
                 // the frame's last chunk runs whole too: dc restarts every frame and the samples past the
                 // frame end (zeros from the loader) only feed outputs nothing reads
                 const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
@@ -505,7 +511,7 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
         chunk_loop([&](int it) {
             // ---- iir2Process recurrence (:75-84), chunk it-2 ----
             const int c = it - 2;
-            if (c >= 0 && c < nch) {
+            if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 2) || lane < PG)) {
                 const int lim = min(CH, S - c * CH);
                 if (lim == CH) {
                     row_pipeline(&L.a[c & 1][my_s * ROW], &L.y[c & 3][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
@@ -545,7 +551,7 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
         chunk_loop([&](int it) {
             // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
             const int c = it - 4;
-            if (c >= 0 && c < nch) {
+            if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 4) || lane < PG)) {
                 row_pipeline(&L.d[c & 1][my_s * ROW], &L.g[c & 1][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                     for (int q = 0; q < SB; q++) {

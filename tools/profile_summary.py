@@ -18,7 +18,7 @@ from collections import defaultdict
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r1"
 OUT = "profiles"
 os.makedirs(OUT, exist_ok=True)
-ENGINE = ("spectrum_kernel", "stats_kernel", "ssb_pipe_kernel", "four_step_a", "four_step_b", "ssb_chain_kernel",
+ENGINE = ("spectrum16k_kernel", "spectrum_kernel", "stats_kernel", "ssb_pipe_kernel", "four_step_a", "four_step_b", "ssb_chain_kernel",
           "ssb_fir_kernel", "ssb_eq_kernel")
 
 
