@@ -71,7 +71,7 @@ def pmc_traffic(kernel: str, streams: int):
 
 
 def cpu_baseline(threads: int, target_cpu_s: float = 15.0) -> dict:
-    """The oracle (our C restatement of the reference path: FFT + stats + SSB per frame), one fresh stream per
+    """The oracle (our C restatement of the reference path: FFT + stats + SSB + pulse detectors per frame), one fresh stream per
     frame, timed on the host cores with `threads` worker threads (ctypes releases the GIL)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -100,7 +100,8 @@ def cpu_baseline(threads: int, target_cpu_s: float = 15.0) -> dict:
     wall = time.perf_counter() - t0
     total = per_thread * threads
     return {"value": round(total * N / wall / 1e6, 3), "unit": "IQ Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{total} frames x {N} CS8 samples (FFT+stats+SSB per frame, fresh stream each), "
+            "sample": f"{total} frames x {N} CS8 samples (FFT+stats+SSB+pulse detectors per frame, fresh stream "
+                      "each), "
                       f"{threads} threads, {wall:.2f} s wall, {per_frame * 1e3:.3f} ms/frame single-thread"}
 
 
@@ -112,7 +113,7 @@ def main() -> int:
     ap.add_argument("--streams", type=int, default=B)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--stages", default="all", choices=["all", "spectrum", "spectrum+stats", "ssb"],
+    ap.add_argument("--stages", default="all", choices=["all", "hot", "spectrum", "spectrum+stats", "ssb"],
                     help="ablation only: the metric is defined on 'all'")
     args = ap.parse_args()
 
@@ -142,7 +143,7 @@ def main() -> int:
 
     now = [1000]
 
-    stages = {"all": sdrg.STAGE_ALL, "spectrum": sdrg.STAGE_SPECTRUM, "ssb": sdrg.STAGE_SSB,
+    stages = {"all": sdrg.STAGE_ALL, "hot": sdrg.STAGE_HOT_PATH, "spectrum": sdrg.STAGE_SPECTRUM, "ssb": sdrg.STAGE_SSB,
               "spectrum+stats": sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS}[args.stages]
 
     def step():
@@ -197,7 +198,8 @@ def main() -> int:
         "dtype": "f32 (int8 CS8 in, int16 PCM out)",
         "data": "synthetic CS8 CW tones + Gaussian noise, generated on device",
         "config": {"workload": f"C3: {streams} streams x {N}-pt CS8 frames @2 Msps per GPU; FFT + |X|^2 + fftshift "
-                               "+ signal-strength stats + SSB (DC, LPF, AGC, 255-tap FIR decim 41, EQ, PCM)",
+                               "+ signal-strength stats + SSB (DC, LPF, AGC, 255-tap FIR decim 41, EQ, PCM) + spectral and audio "
+                               "pulse detectors",
                    "streams_per_gpu": streams, "samples_per_frame": N, "sample_rate": FS, "format": "CS8",
                    "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (", RCCL gather of records"
                                                                                          if world > 1 else "")},

@@ -61,7 +61,11 @@ enum {
     SDRG_STAGE_SPECTRUM = 1,  /* FFT -> |X|^2 -> fftshift (fft_process.cpp:42-97) */
     SDRG_STAGE_STATS = 2,     /* evaluateSignalStrength (fft_process.cpp:122-379); needs SPECTRUM */
     SDRG_STAGE_SSB = 4,       /* processSSB_opt (ssb_demod_opt.cpp:221-296) */
-    SDRG_STAGE_ALL = 7
+    SDRG_STAGE_HOT_PATH = 7,  /* the three above: the accelerated per-frame DSP path */
+    SDRG_STAGE_SPECTRAL_PULSE = 8,  /* SpectralPulseDetector::process(best1kHzSnrSigma, best1kHzCenterFreqHz)
+                                       (sdr-bridge-java-soapy.cpp:477-488); needs STATS */
+    SDRG_STAGE_AUDIO_PULSE = 16,    /* AudioPulseDetector::process(pcm) (ssb_processor.cpp:109-113); needs SSB */
+    SDRG_STAGE_ALL = 31             /* everything soapyCallback + the SSB worker do per frame */
 };
 
 /* Mirror of Kotlin SDRConfig (SDRBridge.kt:23-37) / the 9 JNI applyConfig arguments
@@ -107,8 +111,9 @@ typedef struct sdrg_frame_record {
  * batch.  The order of invocation per frame is soapyCallback's (sdr-bridge-java-soapy.cpp:458-475):
  * fft, detection_flag, mean_snr, mean_snr_sigma, peak_frequency, peak_above_noise_mean, max_bin,
  * best1khz, noise_level; pcm comes from the SSB worker (ssb_processor.cpp:103-113) and is invoked
- * after them, only when the frame produced samples.  The audio-pulse and spectral-pulse callbacks
- * belong to the pulse detectors, which are outside this engine. */
+ * after them, only when the frame produced samples.  spectral_pulse follows noise_level (:477-488, only
+ * with SDRG_STAGE_SPECTRAL_PULSE); audio_pulse follows pcm (ssb_processor.cpp:109-113, every frame, only with
+ * SDRG_STAGE_AUDIO_PULSE). */
 typedef struct sdrg_callbacks {
     void *user;
     void (*fft)(void *user, int32_t stream, const float *power_shifted, int32_t n);        /* ([F)V  */
@@ -121,16 +126,102 @@ typedef struct sdrg_callbacks {
     void (*max_bin)(void *user, int32_t stream, float snr_db, float snr_sigma);           /* (FF)V  */
     void (*best1khz)(void *user, int32_t stream, float snr_db, float snr_sigma);          /* (FF)V  */
     void (*noise_level)(void *user, int32_t stream, float per_bin_mean);                  /* (F)V   */
+    /* (FIJ)V: this frame's best1kHzSnrSigma, SpectralPulseDetector::liveEtat(), llround(estimatedFreqHz()) */
+    void (*spectral_pulse)(void *user, int32_t stream, float snr_sigma, int32_t live_etat, int64_t freq_hz);
+    /* (FI)V: AudioPulseDetector::lastPulseStrength(), liveEtat() */
+    void (*audio_pulse)(void *user, int32_t stream, float strength, int32_t live_etat);
 } sdrg_callbacks;
 
 /* Per-kernel device times of the last process call, from hipEvents recorded on the stream each
  * kernel was launched on (only filled while profiling is enabled). */
 typedef struct sdrg_timings {
     float spectrum_ms;   /* unpack + FFT + |X|^2 + fftshift kernel */
-    float stats_ms;      /* signal-strength kernel */
-    float ssb_ms;        /* whole SSB chain (all its kernels) */
+    float stats_ms;      /* signal-strength kernel (+ spectral pulse detector when requested) */
+    float ssb_ms;        /* whole SSB chain (all its kernels, + audio pulse detector when requested) */
     float total_ms;      /* first launch start -> last kernel end, across both streams */
 } sdrg_timings;
+
+/* ------------------------------------------------------------------------------------------------
+ * Beacon pulse detectors.  One detector per stream, state in HBM, one wavefront per stream per frame:
+ *   SpectralPulseDetector  src/dsp/spectral_pulse_detector.h:19-79, .cpp:1-196   (kind SDRG_PULSE_SPECTRAL)
+ *     fed one (snrSigma, freqHz) pair per FFT frame (sdr-bridge-java-soapy.cpp:477-479)
+ *   AudioPulseDetector     src/ssb/audio_pulse_detector.h:15-104, .cpp:1-256    (kind SDRG_PULSE_AUDIO)
+ *     fed each SSB frame's PCM (ssb_processor.cpp:109)
+ * Both run the reference's ROI / phase-lock / live-state logic with the same float (and, for the spectral
+ * frequency estimate, double) operation order, so outputs are bit-identical to the reference classes.
+ * ---------------------------------------------------------------------------------------------- */
+enum { SDRG_PULSE_SPECTRAL = 0, SDRG_PULSE_AUDIO = 1 };
+
+/* Union of SpectralPulseDetector::Config (spectral_pulse_detector.h:23-35) and AudioPulseDetector::Config
+ * (audio_pulse_detector.h:19-37); sdrg_pulse_config_default() fills the reference defaults of a kind. */
+typedef struct sdrg_pulse_config {
+    float fs_energy;        /* energy frame rate, Hz (spectral 20, set to fs/N by applyConfig; audio 100) */
+    float z_default_s;      /* local-max half-width while unlocked, s (0.666) */
+    float t_target_init;    /* initial period, s (1.75) */
+    float dt_tol_s;         /* rhythm / lock tolerance, s (0.150) */
+    float snr_min;          /* spectral 1.5, audio 1.0 */
+    float snr_rhythm;       /* spectral 2.5, audio 1.1 */
+    float snr_strong;       /* spectral 4.0, audio 2.0 */
+    float dispersion_max;   /* 1.3 */
+    int32_t sum_n_max;      /* 7 */
+    float live_window_t;    /* live-state look-back in periods (4.0) */
+    float live_divisor;     /* 3.0 */
+    /* audio front end only */
+    float sample_rate;      /* PCM rate the filters are designed for (48000) */
+    float f_min, f_max;     /* band-pass edges, Hz (1500, 4000) */
+    float smooth_cutoff;    /* energy low-pass, Hz (5) */
+    int32_t noise_ref_far;  /* noise reference [i-far, i-near) in energy frames (80, 40) */
+    int32_t noise_ref_near;
+} sdrg_pulse_config;
+
+/* What the reference getters return after a frame (spectral_pulse_detector.h:41-48,
+ * audio_pulse_detector.h:45-49), plus the callback arguments. */
+typedef struct sdrg_pulse_output {
+    float strength;            /* lastPulseStrength(): snr of the last admitted ROI */
+    int32_t live_etat;         /* liveEtat(), 0..5 */
+    int32_t level;             /* pulseDetected(): 0 NONE, 1 LOW, 2 MEDIUM, 3 STRONG */
+    int32_t locked;            /* isLocked() */
+    float period_s;            /* lockedPeriodS() */
+    float est_freq_hz;         /* estimatedFreqHz() (spectral; 0 for audio) */
+    int64_t est_freq_hz_rounded;  /* std::llround(estimatedFreqHz()), the spectralPulse callback's J */
+    float input;               /* spectral: the snrSigma fed this frame (the callback's F); audio: strength */
+    int32_t n_energy;          /* energy frames held (diagnostic) */
+    int32_t n_rois;            /* ROIs held (diagnostic) */
+    int32_t overflow;          /* ROI ring overflows (always 0 within the documented bound; diagnostic) */
+} sdrg_pulse_output;
+
+typedef struct sdrg_pulse_bank sdrg_pulse_bank;
+
+/* Reference defaults of a detector kind. */
+int32_t sdrg_pulse_config_default(int32_t kind, sdrg_pulse_config *out);
+/* n_streams detectors of one kind on HIP device `device` (the reference constructor per stream). */
+int32_t sdrg_pulse_bank_create(int32_t kind, const sdrg_pulse_config *cfg, int32_t n_streams, int32_t device,
+                               sdrg_pulse_bank **out);
+int32_t sdrg_pulse_bank_destroy(sdrg_pulse_bank *bank);
+/* SPECTRAL: SpectralPulseDetector::configure (cfg replaced, detector state kept, :6-8).
+ * AUDIO: a fresh AudioPulseDetector(cfg) per stream (what SSBProcessor::setPulseConfig does,
+ * ssb_processor.cpp:70-95).  Applied in stream order with the process calls. */
+int32_t sdrg_pulse_bank_configure(sdrg_pulse_bank *bank, const sdrg_pulse_config *cfg);
+int32_t sdrg_pulse_bank_get_config(const sdrg_pulse_bank *bank, sdrg_pulse_config *out);
+/* reset() of every detector (spectral_pulse_detector.cpp:179-196, audio_pulse_detector.cpp:242-256). */
+int32_t sdrg_pulse_bank_reset(sdrg_pulse_bank *bank);
+/* SPECTRAL, one frame per stream, device pointers: stream s reads *(float*)((char*)snr_sigma + s*stride_bytes)
+ * and the same for freq_hz (so an sdrg_frame_record array can be passed directly); out: [n_streams]. */
+int32_t sdrg_pulse_bank_process_spectral_device(sdrg_pulse_bank *bank, const float *snr_sigma,
+                                                const float *freq_hz, int32_t stride_bytes,
+                                                sdrg_pulse_output *out);
+/* AUDIO, one PCM block per stream, device pointers: stream s has n samples at audio + s*stride samples;
+ * sample_format 0 = int16 (process(vector<int16_t>), scaled by 1/32767), 1 = float (process(vector<float>)). */
+int32_t sdrg_pulse_bank_process_audio_device(sdrg_pulse_bank *bank, const void *audio, int32_t sample_format,
+                                             int32_t n, int32_t stride, sdrg_pulse_output *out);
+/* Host-memory variants: copy in, run, copy out, synchronise. */
+int32_t sdrg_pulse_bank_process_spectral_host(sdrg_pulse_bank *bank, const float *snr_sigma, const float *freq_hz,
+                                              sdrg_pulse_output *out);
+int32_t sdrg_pulse_bank_process_audio_host(sdrg_pulse_bank *bank, const void *audio, int32_t sample_format,
+                                           int32_t n, sdrg_pulse_output *out);
+int32_t sdrg_pulse_bank_synchronize(sdrg_pulse_bank *bank);
+/* Run the device-pointer calls on the caller's HIP stream (a hipStream_t; NULL = the bank's own stream). */
+int32_t sdrg_pulse_bank_set_stream(sdrg_pulse_bank *bank, void *hip_stream);
 
 typedef struct sdrg_engine sdrg_engine;
 
@@ -176,8 +267,19 @@ int32_t sdrg_engine_n_streams(const sdrg_engine *eng);
 /* Samples per frame the SSB chain of every stream emits (constant for a configuration). */
 int32_t sdrg_engine_pcm_len(const sdrg_engine *eng);
 
-/* Reset every stream's cross-frame state (tracking latch, detection ring, SSB filter state) to the
- * state of a freshly constructed reference process. */
+/* The engine's pulse detectors (one SPECTRAL and one AUDIO detector per stream, run by the
+ * SDRG_STAGE_SPECTRAL_PULSE / SDRG_STAGE_AUDIO_PULSE stages).  applyConfig sets the spectral detector to
+ * the default config with fs_energy = (float)sample_rate / (float)samples_per_reading
+ * (sdr-bridge-java-soapy.cpp:1130-1138); create does the same.  set_spectral_pulse_config = configure();
+ * set_audio_pulse_config = SSBProcessor::setPulseConfig (fresh detectors at the next frame). */
+int32_t sdrg_engine_set_spectral_pulse_config(sdrg_engine *eng, const sdrg_pulse_config *cfg);
+int32_t sdrg_engine_set_audio_pulse_config(sdrg_engine *eng, const sdrg_pulse_config *cfg);
+/* Device arrays [n_streams] the last process call wrote (valid until the next call; either may be NULL). */
+int32_t sdrg_engine_pulse_outputs(const sdrg_engine *eng, const sdrg_pulse_output **spectral,
+                                  const sdrg_pulse_output **audio);
+
+/* Reset every stream's cross-frame state (tracking latch, detection ring, SSB filter state, pulse
+ * detectors) to the state of a freshly constructed reference process. */
 int32_t sdrg_engine_reset_state(sdrg_engine *eng);
 
 /* Process one frame of every stream, all buffers in device memory (HBM).
@@ -199,6 +301,8 @@ int32_t sdrg_engine_synchronize(sdrg_engine *eng);
 int32_t sdrg_engine_process_host(sdrg_engine *eng, const void *iq, int32_t format, int32_t stages,
                                  float *spectra, sdrg_frame_record *records, int16_t *pcm,
                                  int64_t now_ms);
+/* Host copies of the last call's pulse outputs ([n_streams] each; either may be NULL); synchronises. */
+int32_t sdrg_engine_get_pulse_outputs(sdrg_engine *eng, sdrg_pulse_output *spectral, sdrg_pulse_output *audio);
 
 /* JNI read(): register the callback table (copied). NULL clears it. */
 int32_t sdrg_engine_set_callbacks(sdrg_engine *eng, const sdrg_callbacks *cbs);

@@ -18,7 +18,8 @@ REF_SSB = os.path.join(HERE, "_ref", "ref_ssb")
 
 # include/sdrg.h formats / stages
 CF32, CS8, CU8, CS16 = 0, 1, 2, 3
-STAGE_SPECTRUM, STAGE_STATS, STAGE_SSB, STAGE_ALL = 1, 2, 4, 7
+STAGE_SPECTRUM, STAGE_STATS, STAGE_SSB, STAGE_HOT_PATH = 1, 2, 4, 7
+STAGE_SPECTRAL_PULSE, STAGE_AUDIO_PULSE, STAGE_ALL = 8, 16, 31
 
 RECORD_DTYPE = np.dtype(
     [
@@ -41,6 +42,36 @@ RECORD_DTYPE = np.dtype(
     ],
     align=True,
 )
+
+# include/sdrg.h sdrg_pulse_config / sdrg_pulse_output
+PULSE_SPECTRAL, PULSE_AUDIO = 0, 1
+PULSE_CONFIG_DTYPE = np.dtype(
+    [(k, "<f4") for k in ("fs_energy", "z_default_s", "t_target_init", "dt_tol_s", "snr_min", "snr_rhythm",
+                          "snr_strong", "dispersion_max")]
+    + [("sum_n_max", "<i4"), ("live_window_t", "<f4"), ("live_divisor", "<f4"), ("sample_rate", "<f4"),
+       ("f_min", "<f4"), ("f_max", "<f4"), ("smooth_cutoff", "<f4"), ("noise_ref_far", "<i4"),
+       ("noise_ref_near", "<i4")],
+    align=True,
+)
+PULSE_OUTPUT_DTYPE = np.dtype(
+    [
+        ("strength", "<f4"),
+        ("live_etat", "<i4"),
+        ("level", "<i4"),
+        ("locked", "<i4"),
+        ("period_s", "<f4"),
+        ("est_freq_hz", "<f4"),
+        ("est_freq_hz_rounded", "<i8"),
+        ("input", "<f4"),
+        ("n_energy", "<i4"),
+        ("n_rois", "<i4"),
+        ("overflow", "<i4"),
+    ],
+    align=True,
+)
+# fields the reference getters expose (n_energy / n_rois / overflow are engine diagnostics)
+PULSE_REF_FIELDS = ("strength", "live_etat", "level", "locked", "period_s", "est_freq_hz", "est_freq_hz_rounded",
+                    "input")
 
 _lib = None
 
@@ -81,6 +112,14 @@ def lib() -> ctypes.CDLL:
             "oracle_ssb_process": (ctypes.c_int, [P, P, i64, u32, ctypes.c_int, ctypes.c_int, P, P, P]),
             "oracle_run_streams": (ctypes.c_int, [P, ctypes.c_int, i32, i32, i32, u32, u32, i32, ctypes.c_int,
                                                   ctypes.c_int, P, P]),
+            "oracle_pulse_config_default": (ctypes.c_int, [ctypes.c_int, P]),
+            "oracle_pulse_create": (P, [ctypes.c_int, P]),
+            "oracle_pulse_destroy": (None, [P]),
+            "oracle_pulse_configure": (ctypes.c_int, [P, P]),
+            "oracle_pulse_reset": (None, [P]),
+            "oracle_pulse_spectral": (ctypes.c_int, [P, P, P, ctypes.c_int, P]),
+            "oracle_pulse_audio": (ctypes.c_int, [P, P, ctypes.c_int, ctypes.c_int, P]),
+            "oracle_pulse_output_size": (ctypes.c_int, []),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -239,6 +278,81 @@ def run_streams(raw: np.ndarray, fmt: int, n: int, f0: int, f1: int, sample_rate
 # ---------------------------------------------------------------------------------------------------------
 # Reference SSB (oracle/_ref/ref_ssb, the reference's own ssb_demod_opt.cpp) — container only
 # ---------------------------------------------------------------------------------------------------------
+def pulse_config_default(kind: int) -> np.ndarray:
+    c = np.zeros(1, PULSE_CONFIG_DTYPE)
+    lib().oracle_pulse_config_default(kind, _ptr(c))
+    return c
+
+
+class PulseDetector:
+    """One SpectralPulseDetector (kind 0) or AudioPulseDetector (kind 1), restated in pulse_oracle.c."""
+
+    def __init__(self, kind: int, cfg: np.ndarray | None = None, **overrides):
+        self.kind = kind
+        self.cfg = pulse_config_default(kind) if cfg is None else cfg.copy()
+        for k, v in overrides.items():
+            self.cfg[k] = v
+        self.h = lib().oracle_pulse_create(kind, _ptr(self.cfg))
+        assert self.h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_pulse_destroy(self.h)
+            self.h = None
+
+    def configure(self, **overrides) -> None:
+        for k, v in overrides.items():
+            self.cfg[k] = v
+        assert lib().oracle_pulse_configure(self.h, _ptr(self.cfg)) == 0
+
+    def reset(self) -> None:
+        lib().oracle_pulse_reset(self.h)
+
+    def spectral(self, snr_sigma: np.ndarray, freq_hz: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(snr_sigma, np.float32)
+        b = np.ascontiguousarray(freq_hz, np.float32)
+        out = np.zeros(a.size, PULSE_OUTPUT_DTYPE)
+        assert lib().oracle_pulse_spectral(self.h, _ptr(a), _ptr(b), a.size, _ptr(out)) == 0
+        return out
+
+    def audio(self, block: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(block)
+        fmt = 0 if a.dtype == np.int16 else 1
+        if fmt:
+            a = a.astype(np.float32)
+        out = np.zeros(1, PULSE_OUTPUT_DTYPE)
+        assert lib().oracle_pulse_audio(self.h, _ptr(a), fmt, a.size, _ptr(out)) == 0
+        return out[0]
+
+    def audio_blocks(self, samples: np.ndarray, block: int) -> np.ndarray:
+        outs = [self.audio(samples[k:k + block]) for k in range(0, samples.size, block)]
+        return np.array(outs, PULSE_OUTPUT_DTYPE)
+
+
+REF_PULSE = os.path.join(HERE, "_ref", "ref_pulse")
+
+
+def ref_pulse_spectral(snr_sigma: np.ndarray, freq_hz: np.ndarray, fs_energy: float, reconf=None) -> np.ndarray:
+    """The reference's own SpectralPulseDetector (oracle/_ref/ref_pulse, container only)."""
+    inp = np.stack([np.asarray(snr_sigma, np.float32), np.asarray(freq_hz, np.float32)], axis=1)
+    args = [REF_PULSE, "spectral", repr(float(np.float32(fs_energy)))]
+    if reconf is not None:
+        args += [str(int(reconf[0])), repr(float(np.float32(reconf[1])))]
+    out = subprocess.run(args, input=inp.tobytes(), capture_output=True, check=True).stdout
+    return np.frombuffer(out, PULSE_OUTPUT_DTYPE).copy()
+
+
+def ref_pulse_audio(samples: np.ndarray, block: int) -> np.ndarray:
+    """The reference's own AudioPulseDetector over int16 / float32 samples in blocks (container only)."""
+    a = np.ascontiguousarray(samples)
+    fmt = 0 if a.dtype == np.int16 else 1
+    if fmt:
+        a = a.astype(np.float32)
+    out = subprocess.run([REF_PULSE, "audio", str(fmt), str(block)], input=a.tobytes(), capture_output=True,
+                         check=True).stdout
+    return np.frombuffer(out, PULSE_OUTPUT_DTYPE).copy()
+
+
 def have_ref() -> bool:
     return os.path.exists(REF_SSB)
 

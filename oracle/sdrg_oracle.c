@@ -792,7 +792,18 @@ ORACLE_API int oracle_frame(oracle_fft_state *fst, oracle_ssb_state *sst, const 
     return rc;
 }
 
-/* Batched CPU baseline: frames [f0, f1) of a [n_frames][n] raw buffer, each an independent stream. */
+/* pulse_oracle.c */
+typedef struct oracle_pulse oracle_pulse;
+int oracle_pulse_config_default(int kind, sdrg_pulse_config *c);
+oracle_pulse *oracle_pulse_create(int kind, const sdrg_pulse_config *cfg);
+void oracle_pulse_destroy(oracle_pulse *p);
+int oracle_pulse_spectral(oracle_pulse *p, const float *snr_sigma, const float *freq_hz, int n_frames,
+                          sdrg_pulse_output *out);
+int oracle_pulse_audio(oracle_pulse *p, const void *audio, int fmt, int n, sdrg_pulse_output *out);
+
+/* Batched CPU baseline: frames [f0, f1) of a [n_frames][n] raw buffer, each an independent stream (with the
+ * pulse detectors of soapyCallback / the SSB worker when stages has SDRG_STAGE_SPECTRAL_PULSE /
+ * SDRG_STAGE_AUDIO_PULSE). */
 ORACLE_API int oracle_run_streams(const void *raw, int fmt, int32_t n, int32_t f0, int32_t f1, uint32_t sample_rate,
                                   uint32_t center_frequency, int32_t focus_khz, int stages, int mode, float *spectrum_scratch,
                                   int16_t *pcm_scratch) {
@@ -808,6 +819,25 @@ ORACLE_API int oracle_run_streams(const void *raw, int fmt, int32_t n, int32_t f
         int rc = oracle_frame(&fst, &sst, (const char *)raw + (size_t)f * (size_t)n * bps, fmt, n, 1000, stages, mode,
                               spectrum_scratch, &rec, pcm_scratch, &pcm_len);
         if (rc) return rc;
+        if (stages & (SDRG_STAGE_SPECTRAL_PULSE | SDRG_STAGE_AUDIO_PULSE)) {
+            sdrg_pulse_config pc;
+            sdrg_pulse_output po;
+            if (stages & SDRG_STAGE_SPECTRAL_PULSE) {
+                oracle_pulse_config_default(SDRG_PULSE_SPECTRAL, &pc);
+                pc.fs_energy = (float)sample_rate / (float)n;
+                oracle_pulse *d = oracle_pulse_create(SDRG_PULSE_SPECTRAL, &pc);
+                if (!d) return -3;
+                oracle_pulse_spectral(d, &rec.best1khz_snr_sigma, &rec.best1khz_center_freq_hz, 1, &po);
+                oracle_pulse_destroy(d);
+            }
+            if (stages & SDRG_STAGE_AUDIO_PULSE) {
+                oracle_pulse_config_default(SDRG_PULSE_AUDIO, &pc);
+                oracle_pulse *d = oracle_pulse_create(SDRG_PULSE_AUDIO, &pc);
+                if (!d) return -3;
+                oracle_pulse_audio(d, pcm_scratch, 0, pcm_len, &po);
+                oracle_pulse_destroy(d);
+            }
+        }
     }
     return 0;
 }

@@ -171,4 +171,25 @@ StatsGeometry stats_geometry(uint32_t sample_rate, uint32_t center_frequency, in
     return g;
 }
 
+// Bilinear-transform Butterworth sections of the audio pulse detector, in float with the reference's
+// expression order (audio_pulse_detector.cpp:4, :29-55).
+void design_pulse_sos(float fs, float fc, bool highpass, float c[5]) {
+    const float pi = 3.14159265358979f;
+    const float Q = 0.7071f;
+    const float K = tanf(pi * fc / fs);
+    const float K2 = K * K;
+    const float norm = K2 + K / Q + 1.f;
+    if (highpass) {
+        c[0] = 1.f / norm;
+        c[1] = -2.f / norm;
+        c[2] = 1.f / norm;
+    } else {
+        c[0] = K2 / norm;
+        c[1] = 2.f * K2 / norm;
+        c[2] = K2 / norm;
+    }
+    c[3] = 2.f * (K2 - 1.f) / norm;
+    c[4] = (K2 - K / Q + 1.f) / norm;
+}
+
 }  // namespace sdrg

@@ -14,6 +14,8 @@ int design_fir(int64_t in_size, int decim, float cutoff_rel, float *h);
 int ssb_decim(uint32_t sample_rate);
 int ssb_taps_for(int64_t samp_count);
 int ssb_pcm_len(int64_t samp_count, uint32_t sample_rate);
+// AudioPulseDetector::makeLP2 / makeHP2 (audio_pulse_detector.cpp:29-55), Q = 0.7071: {b0, b1, b2, a1, a2}
+void design_pulse_sos(float fs, float fc, bool highpass, float c[5]);
 StatsGeometry stats_geometry(uint32_t sample_rate, uint32_t center_frequency, int n, int focus_khz);
 
 }  // namespace sdrg

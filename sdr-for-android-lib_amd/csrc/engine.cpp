@@ -22,15 +22,16 @@
 #include <vector>
 
 #include "design.h"
+#include "pulse_bank.h"
 #include "sdrg_internal.h"
 
 using namespace sdrg;
 
 namespace {
-
 thread_local std::string g_last_error;
+}  // namespace
 
-int32_t fail(int32_t code, const char *fmt, ...) {
+int32_t sdrg::fail(int32_t code, const char *fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -39,6 +40,8 @@ int32_t fail(int32_t code, const char *fmt, ...) {
     g_last_error = buf;
     return code;
 }
+
+namespace {
 
 #define HIP_TRY(expr)                                                                              \
     do {                                                                                           \
@@ -112,6 +115,11 @@ struct sdrg_engine {
     std::vector<int16_t> h_pcm;
 
     SsbControl ssb;
+    // pulse detectors (created at the first call that runs their stage)
+    sdrg_pulse_config spec_pulse_cfg{}, audio_pulse_cfg{};
+    sdrg_pulse_bank spec_bank, audio_bank;
+    bool spec_bank_live = false, audio_bank_live = false;
+    std::vector<sdrg_pulse_output> h_pspec, h_paudio;
     bool cf_changed_pending = false;
     int upper = 1;
     bool has_cbs = false;
@@ -119,6 +127,15 @@ struct sdrg_engine {
 };
 
 namespace {
+
+// applyConfig's SpectralPulseDetector configuration (sdr-bridge-java-soapy.cpp:1130-1138): the default
+// Config with fsEnergy = sampleRate / samplesPerReading (20 when samplesPerReading <= 0)
+sdrg_pulse_config spectral_pulse_cfg_for(const sdrg_config &c) {
+    sdrg_pulse_config p;
+    sdrg_pulse_config_default(SDRG_PULSE_SPECTRAL, &p);
+    p.fs_energy = c.samples_per_reading > 0 ? (float)c.sample_rate / (float)c.samples_per_reading : 20.f;
+    return p;
+}
 
 int32_t validate_config(const sdrg_config *cfg) {
     if (!cfg) return fail(SDRG_E_INVALID, "null config");
@@ -301,8 +318,23 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     if (stages & ~SDRG_STAGE_ALL) return fail(SDRG_E_INVALID, "unknown stage bits 0x%x", stages);
     if ((stages & SDRG_STAGE_STATS) && !(stages & SDRG_STAGE_SPECTRUM))
         return fail(SDRG_E_INVALID, "STATS needs SPECTRUM");
+    if ((stages & SDRG_STAGE_SPECTRAL_PULSE) && !(stages & SDRG_STAGE_STATS))
+        return fail(SDRG_E_INVALID, "SPECTRAL_PULSE needs STATS");
+    if ((stages & SDRG_STAGE_AUDIO_PULSE) && !(stages & SDRG_STAGE_SSB))
+        return fail(SDRG_E_INVALID, "AUDIO_PULSE needs SSB");
     const bool do_spec = stages & SDRG_STAGE_SPECTRUM, do_stats = stages & SDRG_STAGE_STATS,
-               do_ssb = stages & SDRG_STAGE_SSB;
+               do_ssb = stages & SDRG_STAGE_SSB, do_sp = stages & SDRG_STAGE_SPECTRAL_PULSE,
+               do_ap = stages & SDRG_STAGE_AUDIO_PULSE;
+    if (do_sp && !e->spec_bank_live) {
+        int32_t rc = pulse_bank_init(&e->spec_bank, SDRG_PULSE_SPECTRAL, &e->spec_pulse_cfg, B, e->device);
+        if (rc) return rc;
+        e->spec_bank_live = true;
+    }
+    if (do_ap && !e->audio_bank_live) {
+        int32_t rc = pulse_bank_init(&e->audio_bank, SDRG_PULSE_AUDIO, &e->audio_pulse_cfg, B, e->device);
+        if (rc) return rc;
+        e->audio_bank_live = true;
+    }
     if (do_spec && !spectrum_supported(n))
         return fail(SDRG_E_UNSUPPORTED, "spectrum for N=%d not supported by this build", n);
 
@@ -369,12 +401,29 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
         HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
         if (prof) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
-        HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_chunk_table, e->d_ssb, e->d_ssb_scratch, pcm, e->s_ssb));
+        // AudioPulseDetector::process(pcm) after processSSB_opt (ssb_processor.cpp:109): its per-sample front
+        // end runs inside the SSB kernel on the PCM it produces, the detector right after
+        AudioFront af;
+        if (do_ap) {
+            int32_t rc = pulse_bank_audio_front(&e->audio_bank, sp.pcm_len, &af, e->s_ssb);
+            if (rc) return rc;
+        }
+        HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_chunk_table, e->d_ssb, e->d_ssb_scratch, pcm,
+                           do_ap ? &af : nullptr, e->s_ssb));
+        if (do_ap) {
+            int32_t rc = pulse_bank_audio_detect(&e->audio_bank, e->audio_bank.d_out, e->s_ssb);
+            if (rc) return rc;
+        }
         if (prof) HIP_TRY(hipEventRecord(ev->ssb1, e->s_ssb));
         HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
     }
     if (do_stats) {
         HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->s_main));
+        if (do_sp) {  // spectralPulseDetector.process(best1kHzSnrSigma, best1kHzCenterFreqHz) (:477-479)
+            int32_t rc = pulse_bank_spectral(&e->spec_bank, &recs->best1khz_snr_sigma, &recs->best1khz_center_freq_hz,
+                                             (int)sizeof(sdrg_frame_record), e->spec_bank.d_out, e->s_main);
+            if (rc) return rc;
+        }
         if (prof) HIP_TRY(hipEventRecord(ev->stats, e->s_main));
         e->cf_changed_pending = false;
     }
@@ -404,9 +453,17 @@ void dispatch_callbacks(sdrg_engine *e, int32_t stages, int pcm_len) {
             if (c.max_bin) c.max_bin(c.user, s, r.max_bin_snr_db, r.max_bin_snr_sigma);
             if (c.best1khz) c.best1khz(c.user, s, r.best1khz_snr_db, r.best1khz_snr_sigma);
             if (c.noise_level) c.noise_level(c.user, s, r.per_bin_mean);
+            if ((stages & SDRG_STAGE_SPECTRAL_PULSE) && c.spectral_pulse) {
+                const sdrg_pulse_output &o = e->h_pspec[s];
+                c.spectral_pulse(c.user, s, o.input, o.live_etat, o.est_freq_hz_rounded);
+            }
         }
         if ((stages & SDRG_STAGE_SSB) && c.pcm && pcm_len > 0)
             c.pcm(c.user, s, e->h_pcm.data() + (size_t)s * pcm_len, pcm_len);
+        if ((stages & SDRG_STAGE_AUDIO_PULSE) && c.audio_pulse) {  // every frame (ssb_processor.cpp:109-113)
+            const sdrg_pulse_output &o = e->h_paudio[s];
+            c.audio_pulse(c.user, s, o.strength, o.live_etat);
+        }
     }
 }
 
@@ -458,6 +515,8 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
     HIP_TRY(hipSetDevice(device));
     sdrg_engine *e = new sdrg_engine();
     e->cfg = *cfg;
+    e->spec_pulse_cfg = spectral_pulse_cfg_for(*cfg);
+    sdrg_pulse_config_default(SDRG_PULSE_AUDIO, &e->audio_pulse_cfg);
     e->n_streams = n_streams;
     e->device = device;
     auto cleanup = [&](int32_t code) {
@@ -494,6 +553,8 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
         for (hipEvent_t ev : rev)
             if (ev) (void)hipEventDestroy(ev);
     }
+    if (e->spec_bank_live) pulse_bank_release(&e->spec_bank);
+    if (e->audio_bank_live) pulse_bank_release(&e->audio_bank);
     if (e->s_main) (void)hipStreamDestroy(e->s_main);
     if (e->s_ssb) (void)hipStreamDestroy(e->s_ssb);
     delete e;
@@ -505,6 +566,8 @@ int32_t sdrg_engine_apply_config(sdrg_engine *e, const sdrg_config *cfg) {
     int32_t rc = validate_config(cfg);
     if (rc) return rc;
     e->cfg = *cfg;  // applied at the next process call (frame boundary)
+    e->spec_pulse_cfg = spectral_pulse_cfg_for(*cfg);
+    if (e->spec_bank_live) return pulse_bank_configure(&e->spec_bank, &e->spec_pulse_cfg);
     return SDRG_OK;
 }
 
@@ -556,6 +619,51 @@ int32_t sdrg_engine_reset_state(sdrg_engine *e) {
     HIP_TRY(hipMemset(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
     e->ssb = SsbControl{};
     e->cf_changed_pending = false;
+    e->spec_bank.reset_pending = true;
+    e->audio_bank.reset_pending = true;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_spectral_pulse_config(sdrg_engine *e, const sdrg_pulse_config *cfg) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    int32_t rc = pulse_config_check(SDRG_PULSE_SPECTRAL, cfg);
+    if (rc) return rc;
+    e->spec_pulse_cfg = *cfg;
+    if (e->spec_bank_live) return pulse_bank_configure(&e->spec_bank, cfg);
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_audio_pulse_config(sdrg_engine *e, const sdrg_pulse_config *cfg) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    int32_t rc = pulse_config_check(SDRG_PULSE_AUDIO, cfg);
+    if (rc) return rc;
+    e->audio_pulse_cfg = *cfg;
+    if (e->audio_bank_live) return pulse_bank_configure(&e->audio_bank, cfg);
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_pulse_outputs(const sdrg_engine *e, const sdrg_pulse_output **spectral,
+                                  const sdrg_pulse_output **audio) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if (spectral) *spectral = e->spec_bank_live ? e->spec_bank.d_out : nullptr;
+    if (audio) *audio = e->audio_bank_live ? e->audio_bank.d_out : nullptr;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_get_pulse_outputs(sdrg_engine *e, sdrg_pulse_output *spectral, sdrg_pulse_output *audio) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->s_main));
+    HIP_TRY(hipStreamSynchronize(e->s_ssb));
+    const size_t bytes = sizeof(sdrg_pulse_output) * (size_t)e->n_streams;
+    if (spectral) {
+        if (!e->spec_bank_live) return fail(SDRG_E_INVALID, "the spectral pulse stage has not run");
+        HIP_TRY(hipMemcpy(spectral, e->spec_bank.d_out, bytes, hipMemcpyDeviceToHost));
+    }
+    if (audio) {
+        if (!e->audio_bank_live) return fail(SDRG_E_INVALID, "the audio pulse stage has not run");
+        HIP_TRY(hipMemcpy(audio, e->audio_bank.d_out, bytes, hipMemcpyDeviceToHost));
+    }
     return SDRG_OK;
 }
 
@@ -631,6 +739,16 @@ int32_t sdrg_engine_process_host(sdrg_engine *e, const void *iq, int32_t format,
     if (do_ssb && h_pcm && pcm_len > 0)
         HIP_TRY(hipMemcpyAsync(h_pcm, e->d_pcm_stage, sizeof(int16_t) * (size_t)B * pcm_len, hipMemcpyDeviceToHost,
                                e->s_main));
+    if (want_cb && (stages & SDRG_STAGE_SPECTRAL_PULSE)) {
+        e->h_pspec.resize(B);
+        HIP_TRY(hipMemcpyAsync(e->h_pspec.data(), e->spec_bank.d_out, sizeof(sdrg_pulse_output) * (size_t)B,
+                               hipMemcpyDeviceToHost, e->s_main));
+    }
+    if (want_cb && (stages & SDRG_STAGE_AUDIO_PULSE)) {
+        e->h_paudio.resize(B);
+        HIP_TRY(hipMemcpyAsync(e->h_paudio.data(), e->audio_bank.d_out, sizeof(sdrg_pulse_output) * (size_t)B,
+                               hipMemcpyDeviceToHost, e->s_main));
+    }
     HIP_TRY(hipStreamSynchronize(e->s_main));
     if (want_cb) {
         // callbacks read the engine-owned host copies; make sure they hold this call's data

@@ -35,8 +35,24 @@ void ssb_report_stamps();  // diagnostic (SDRG_PIPE_STAMPS=1)
 // chunk_table: per chunk of ssb_pipe_chunk() samples {first, last output overlapping it, first, last output
 // completed in it} (host-computed, see engine.cpp); may be null (reference kernels).
 int ssb_pipe_chunk(void);
+// audio (nullable): run the audio pulse detector's front end on the PCM as it is produced
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,
-                      hipStream_t stream);
+                      const AudioFront *audio, hipStream_t stream);
+
+// Pulse detectors (pulse.hip): one wavefront per stream.  Rings are [n_streams][cap] (cap = cap_mask + 1),
+// fh [n_streams][2][PULSE_FH_SLOTS].
+hipError_t launch_pulse_reset(PulseStreamState *states, int n_streams, float t_target_init, hipStream_t stream);
+hipError_t launch_spectral_pulse(const PulseParams &p, int n_streams, PulseStreamState *states, float *ebuf,
+                                 float *fbuf, float *roi_t, int *roi_etat, float *fh, const float *snr_sigma,
+                                 const float *freq_hz, int stride_bytes, sdrg_pulse_output *out, hipStream_t stream);
+// audio: the front end (lane per stream; also fused into the SSB kernels, see launch_ssb) writes each call's
+// energy values to a.new_e [n_streams][a.max_new] (a.max_new >= n_samples / frame_samples + 1) and counts;
+// the detector (wave per stream) consumes them.
+hipError_t launch_audio_front(const AudioFront &a, const void *audio, int fmt, int n_samples, int stride, int n_streams,
+                              hipStream_t stream);
+hipError_t launch_audio_detect(const PulseParams &p, int n_streams, PulseStreamState *states, float *ebuf, float *roi_t,
+                               int *roi_etat, const float *new_e, int max_new, const int *new_count,
+                               sdrg_pulse_output *out, hipStream_t stream);
 
 }  // namespace sdrg

@@ -74,4 +74,67 @@ struct SsbParams {
     float bp[5];
 };
 
+// ------------------------------------------------------------------------------------------------
+// Beacon pulse detectors (SpectralPulseDetector / AudioPulseDetector).  The reference's std::deque members
+// become per-stream rings in HBM of `cap` slots (a power of two >= maxBuf + 8): eBuf_ / freqBuf_ and the
+// ROI list, addressed as slot (head + logical index) & (cap - 1); the small bounded deques (last3Dts_,
+// histDts_, histN_) live in the state record itself, and the 30-entry freqHistory_ in a 32-slot ring.
+// ------------------------------------------------------------------------------------------------
+constexpr int PULSE_FH_SLOTS = 32;  // freqHistory_ ring (kFreqHistoryMax = 30, spectral_pulse_detector.h:67)
+
+struct PulseStreamState {
+    double ols_a, ols_b;       // estimatedFreqHz regression f = a t + b over freqHistory_ (recomputed per ROI)
+    uint32_t head;             // ring slot of eBuf_[0]
+    int32_t n;                 // eBuf_.size()
+    float t0;                  // eBufT0_
+    int32_t last_scan;         // lastScanIdx_
+    float t_last_roi;          // tLastRoi_
+    int32_t locked;            // isLocked_
+    float t_target;            // tTarget_
+    int32_t live_etat;         // liveEtat_
+    float last_snr;            // lastSnr_
+    int32_t level;             // lastLevel_
+    uint32_t roi_head;         // ring slot of rois_[0]
+    int32_t n_rois;
+    int32_t n_last3, n_hist;
+    float last3[3];            // last3Dts_
+    float hist_dts[5];         // histDts_
+    int32_t hist_n[5];         // histN_
+    int32_t fh_head, n_fh;     // freqHistory_ ring
+    int32_t ols_mode;          // 0: < 2 samples (0 Hz), 1: degenerate (mean), 2: a t + b
+    float ols_mean;            // (float)(sum_f / n) for mode 1
+    int32_t overflow;          // ROI ring overflows (diagnostic; never within the documented bound)
+    float band_z[4];           // audio: band-pass SOS z1/z2 (HP, LP)
+    float low_z[2];            // audio: energy low-pass z1/z2
+    int32_t frame_count;       // audio: frameCount_
+    float frame_acc;           // audio: frameAcc_
+    int32_t pad_[2];
+};
+
+struct PulseParams {
+    int32_t cap_mask;          // ring slots - 1
+    int32_t max_buf;           // (int)(10.f * fsEnergy)   (spectral :31, audio :118)
+    float fs_energy, inv_fs;   // fsEnergy, 1.f / fsEnergy (the eBufT0_ increment)
+    float z_default_s, dt_tol_s, snr_min, snr_rhythm, snr_strong, dispersion_max;
+    int32_t sum_n_max;
+    float live_window_t, live_divisor;
+    int32_t noise_far, noise_near;
+    int32_t frame_samples;     // audio: max(1, (int)(sampleRate / fsEnergy))
+    float band[2][5];          // audio: HP(fMin), LP(fMax) b0 b1 b2 a1 a2
+    float low[5];              // audio: LP(smoothCutoff) at fsEnergy
+};
+
+// The audio detector's front end as the SSB kernels run it on the PCM they produce (band-pass, RMS per
+// energy frame, energy low-pass): its coefficients, the per-stream state records (only the front-end
+// fields are touched) and where the energy values of the call go ([n_streams][max_new], counts).
+struct AudioFront {
+    float band[2][5];
+    float low[5];
+    int32_t frame_samples;
+    int32_t max_new;
+    PulseStreamState *state;
+    float *new_e;
+    int32_t *new_count;
+};
+
 }  // namespace sdrg

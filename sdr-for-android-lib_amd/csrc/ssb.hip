@@ -21,6 +21,7 @@
 
 #include <vector>
 
+#include "pulse_front.h"
 #include "sdrg_internal.h"
 #include "ssb_math.h"
 
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                                                           SsbStreamState *__restrict__ state,
                                                           int16_t *__restrict__ pcm,
                                                           unsigned long long *__restrict__ stamps, int prio_mask,
-                                                          int skip_mask, unsigned long long role_map) {
+                                                          int skip_mask, unsigned long long role_map, AudioFront af) {
     __shared__ PipeLds L;
     const int tid = threadIdx.x;
     const int hw_wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // runs on SIMD hw_wave % 4
@@ -675,6 +676,12 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
             const SsbStreamState st = state[s0 + my_s];
             h1 = st.hp_z1; h2 = st.hp_z2; q1 = st.bp_z1; q2 = st.bp_z2;
         }
+        // audio pulse detector front end on each PCM sample (AudioPulseDetector::process(pcm), pulse_front.h)
+        const bool front = af.state != nullptr;
+        FrontState fst{};
+        if (front && serial_live) fst = front_load(af.state + s0 + my_s);
+        float *my_new = front ? af.new_e + (size_t)(serial_live ? s0 + my_s : 0) * (size_t)af.max_new : nullptr;
+        int np = 0;
         chunk_loop([&](int it) {
             // ---- HP -> BP -> transientBoost -> floatToPCM on the outputs the FIR completed, chunk it-7 ----
             const int ce = it - 7;
@@ -693,7 +700,9 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                     prev = yb;
                     const float boosted = yb + p.transient_coeff * diff;
                     const float v = clamp_ref(boosted * p.gain, -1.0f, 1.0f);
-                    pcm[(size_t)(s0 + my_s) * PL + o] = (int16_t)(v * 32767.0f);
+                    const int16_t q = (int16_t)(v * 32767.0f);
+                    pcm[(size_t)(s0 + my_s) * PL + o] = q;
+                    if (front) front_sample(af, fst, (float)q * PCM_TO_FLOAT, my_new, np);
                 }
             }
         });
@@ -702,6 +711,10 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
             state[s0 + my_s].hp_z2 = h2;
             state[s0 + my_s].bp_z1 = q1;
             state[s0 + my_s].bp_z2 = q2;
+            if (front) {
+                front_store(af.state + s0 + my_s, fst);
+                af.new_count[s0 + my_s] = np;
+            }
         }
     } else {
         chunk_loop([&](int it) {
@@ -735,7 +748,8 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
 }  // namespace
 
 hipError_t launch_ssb_reference(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
-                      SsbStreamState *state, float *scratch, int16_t *pcm, hipStream_t stream) {
+                      SsbStreamState *state, float *scratch, int16_t *pcm, const AudioFront *audio,
+                      hipStream_t stream) {
     if (n_frames <= 0) return hipSuccess;
     const dim3 grid((n_frames + WAVE - 1) / WAVE);
     const char *src = reinterpret_cast<const char *>(iq);
@@ -757,7 +771,9 @@ hipError_t launch_ssb_reference(const void *iq, int fmt, int n_frames, const Ssb
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(ssb_eq_kernel, grid, dim3(WAVE), 0, stream, fir_out, n_frames, p, state, pcm);
-    return hipGetLastError();
+    e = hipGetLastError();
+    if (e != hipSuccess || !audio) return e;
+    return launch_audio_front(*audio, pcm, 0, p.pcm_len, p.pcm_len, n_frames, stream);
 }
 
 bool ssb_force_reference_kernels() {
@@ -823,7 +839,7 @@ int ssb_pipe_chunk(void) { return CH; }
 
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,
-                      hipStream_t stream) {
+                      const AudioFront *audio, hipStream_t stream) {
     if (n_frames <= 0) return hipSuccess;
     int nsl_mask = 3;
     const char *src = reinterpret_cast<const char *>(iq);
@@ -838,6 +854,8 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         const bool dma = CH * bps <= 512 && (n_live % (bc * CH)) == 0 && ((size_t)p.n_in * bps) % 16 == 0 &&
                          (reinterpret_cast<uintptr_t>(iq) & 15) == 0;
         unsigned long long *stamps = ssb_stamps_buffer(n_frames);
+        AudioFront af{};
+        if (audio) af = *audio;
         static const int prio_mask = [] {  // diagnostic override: SDRG_PIPE_PRIO = bit mask of high-priority waves
             const char *e = getenv("SDRG_PIPE_PRIO");
             return e ? (int)strtol(e, nullptr, 0) : 0x7;
@@ -854,10 +872,10 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
 #define SDRG_PIPE_LAUNCH(F)                                                                                      \
     if (dma)                                                                                                     \
         hipLaunchKernelGGL((ssb_pipe_kernel<F, true>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
-                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map);                                                \
+                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map, af);                                                \
     else                                                                                                         \
         hipLaunchKernelGGL((ssb_pipe_kernel<F, false>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
-                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map);
+                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map, af);
         switch (fmt) {
         case SDRG_IQ_CS8: SDRG_PIPE_LAUNCH(SDRG_IQ_CS8); break;
         case SDRG_IQ_CU8: SDRG_PIPE_LAUNCH(SDRG_IQ_CU8); break;
@@ -868,7 +886,7 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         }
         return hipGetLastError();
     }
-    return launch_ssb_reference(iq, fmt, n_frames, p, taps, state, scratch, pcm, stream);
+    return launch_ssb_reference(iq, fmt, n_frames, p, taps, state, scratch, pcm, audio, stream);
 }
 
 }  // namespace sdrg

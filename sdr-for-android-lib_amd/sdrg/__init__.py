@@ -27,7 +27,9 @@ LIB_PATH = os.environ.get("SDRG_LIB_PATH") or os.path.join(PKG, "lib", "libsdrg.
 
 # include/sdrg.h
 CF32, CS8, CU8, CS16 = 0, 1, 2, 3
-STAGE_SPECTRUM, STAGE_STATS, STAGE_SSB, STAGE_ALL = 1, 2, 4, 7
+STAGE_SPECTRUM, STAGE_STATS, STAGE_SSB, STAGE_HOT_PATH = 1, 2, 4, 7
+STAGE_SPECTRAL_PULSE, STAGE_AUDIO_PULSE, STAGE_ALL = 8, 16, 31
+PULSE_SPECTRAL, PULSE_AUDIO = 0, 1
 STATUS = {0: "SDRG_OK", -1: "SDRG_E_INVALID", -2: "SDRG_E_UNSUPPORTED", -3: "SDRG_E_NOMEM", -4: "SDRG_E_HIP",
           -5: "SDRG_E_NODEVICE"}
 BYTES_PER_SAMPLE = {CF32: 8, CS8: 2, CU8: 2, CS16: 4}
@@ -55,6 +57,23 @@ RECORD_DTYPE = np.dtype(
     align=True,
 )
 
+PULSE_OUTPUT_DTYPE = np.dtype(
+    [
+        ("strength", "<f4"),
+        ("live_etat", "<i4"),
+        ("level", "<i4"),
+        ("locked", "<i4"),
+        ("period_s", "<f4"),
+        ("est_freq_hz", "<f4"),
+        ("est_freq_hz_rounded", "<i8"),
+        ("input", "<f4"),
+        ("n_energy", "<i4"),
+        ("n_rois", "<i4"),
+        ("overflow", "<i4"),
+    ],
+    align=True,
+)
+
 # Every entry point include/sdrg.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "sdrg_abi_version", "sdrg_last_error", "sdrg_ssb_pcm_len", "sdrg_ssb_design", "sdrg_engine_create", "sdrg_engine_destroy",
@@ -63,6 +82,12 @@ EXPORTS = [
     "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_process_host",
     "sdrg_engine_set_callbacks", "sdrg_engine_set_profiling", "sdrg_engine_get_timings",
     "sdrg_engine_get_timing_stats", "sdrg_engine_reset_timing_stats",
+    "sdrg_engine_set_spectral_pulse_config", "sdrg_engine_set_audio_pulse_config", "sdrg_engine_pulse_outputs",
+    "sdrg_engine_get_pulse_outputs",
+    "sdrg_pulse_config_default", "sdrg_pulse_bank_create", "sdrg_pulse_bank_destroy", "sdrg_pulse_bank_configure",
+    "sdrg_pulse_bank_get_config", "sdrg_pulse_bank_reset", "sdrg_pulse_bank_process_spectral_device",
+    "sdrg_pulse_bank_process_audio_device", "sdrg_pulse_bank_process_spectral_host",
+    "sdrg_pulse_bank_process_audio_host", "sdrg_pulse_bank_synchronize", "sdrg_pulse_bank_set_stream",
 ]
 
 
@@ -84,6 +109,23 @@ class _Config(ctypes.Structure):
     ]
 
 
+class PulseConfig(ctypes.Structure):
+    """sdrg_pulse_config: SpectralPulseDetector::Config / AudioPulseDetector::Config (include/sdrg.h)."""
+    _fields_ = [(k, ctypes.c_float) for k in ("fs_energy", "z_default_s", "t_target_init", "dt_tol_s", "snr_min",
+                                              "snr_rhythm", "snr_strong", "dispersion_max")] + [
+        ("sum_n_max", ctypes.c_int32), ("live_window_t", ctypes.c_float), ("live_divisor", ctypes.c_float),
+        ("sample_rate", ctypes.c_float), ("f_min", ctypes.c_float), ("f_max", ctypes.c_float),
+        ("smooth_cutoff", ctypes.c_float), ("noise_ref_far", ctypes.c_int32), ("noise_ref_near", ctypes.c_int32)]
+
+    @classmethod
+    def default(cls, kind: int, **overrides) -> "PulseConfig":
+        c = cls()
+        _check(load().sdrg_pulse_config_default(kind, ctypes.byref(c)), "sdrg_pulse_config_default")
+        for k, v in overrides.items():
+            setattr(c, k, v)
+        return c
+
+
 class _Timings(ctypes.Structure):
     _fields_ = [("spectrum_ms", ctypes.c_float), ("stats_ms", ctypes.c_float), ("ssb_ms", ctypes.c_float),
                 ("total_ms", ctypes.c_float)]
@@ -97,6 +139,8 @@ CB_F = ctypes.CFUNCTYPE(None, _V, _I32, _F)
 CB_J = ctypes.CFUNCTYPE(None, _V, _I32, _I64)
 CB_PCM = ctypes.CFUNCTYPE(None, _V, _I32, ctypes.POINTER(ctypes.c_int16), _I32)
 CB_FF = ctypes.CFUNCTYPE(None, _V, _I32, _F, _F)
+CB_FIJ = ctypes.CFUNCTYPE(None, _V, _I32, _F, _I32, _I64)
+CB_FI = ctypes.CFUNCTYPE(None, _V, _I32, _F, _I32)
 
 
 class _Callbacks(ctypes.Structure):
@@ -112,6 +156,8 @@ class _Callbacks(ctypes.Structure):
         ("max_bin", CB_FF),
         ("best1khz", CB_FF),
         ("noise_level", CB_F),
+        ("spectral_pulse", CB_FIJ),
+        ("audio_pulse", CB_FI),
     ]
 
 
@@ -156,6 +202,22 @@ def load() -> ctypes.CDLL:
         "sdrg_engine_get_timings": (_I32, [P, ctypes.POINTER(_Timings)]),
         "sdrg_engine_get_timing_stats": (_I32, [P, ctypes.POINTER(_Timings), ctypes.POINTER(_I32)]),
         "sdrg_engine_reset_timing_stats": (_I32, [P]),
+        "sdrg_engine_set_spectral_pulse_config": (_I32, [P, ctypes.POINTER(PulseConfig)]),
+        "sdrg_engine_set_audio_pulse_config": (_I32, [P, ctypes.POINTER(PulseConfig)]),
+        "sdrg_engine_pulse_outputs": (_I32, [P, ctypes.POINTER(P), ctypes.POINTER(P)]),
+        "sdrg_engine_get_pulse_outputs": (_I32, [P, P, P]),
+        "sdrg_pulse_config_default": (_I32, [_I32, ctypes.POINTER(PulseConfig)]),
+        "sdrg_pulse_bank_create": (_I32, [_I32, ctypes.POINTER(PulseConfig), _I32, _I32, ctypes.POINTER(P)]),
+        "sdrg_pulse_bank_destroy": (_I32, [P]),
+        "sdrg_pulse_bank_configure": (_I32, [P, ctypes.POINTER(PulseConfig)]),
+        "sdrg_pulse_bank_get_config": (_I32, [P, ctypes.POINTER(PulseConfig)]),
+        "sdrg_pulse_bank_reset": (_I32, [P]),
+        "sdrg_pulse_bank_process_spectral_device": (_I32, [P, P, P, _I32, P]),
+        "sdrg_pulse_bank_process_audio_device": (_I32, [P, P, _I32, _I32, _I32, P]),
+        "sdrg_pulse_bank_process_spectral_host": (_I32, [P, P, P, P]),
+        "sdrg_pulse_bank_process_audio_host": (_I32, [P, P, _I32, _I32, P]),
+        "sdrg_pulse_bank_synchronize": (_I32, [P]),
+        "sdrg_pulse_bank_set_stream": (_I32, [P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -241,7 +303,8 @@ class Engine:
 
     def read(self, fftCallback=None, detectionFlagCallback=None, meanSnrCallback=None, meanSnrSigmaCallback=None,
              peakFrequencyCallback=None, pcmCallback=None, peakAboveNoiseMeanCallback=None, maxBinCallback=None,
-             best1kHzCallback=None, noiseLevelCallback=None) -> None:
+             best1kHzCallback=None, noiseLevelCallback=None, spectralPulseCallback=None,
+             audioPulseCallback=None) -> None:
         """Register per-frame callbacks (JNI read(), SDRBridge.kt:141-154).  Each receives the stream index
         first, then the reference callback's arguments; arrays arrive as numpy copies."""
         def wrap(fn, ctype, conv):
@@ -263,6 +326,8 @@ class Engine:
             wrap(maxBinCallback, CB_FF, ident),
             wrap(best1kHzCallback, CB_FF, ident),
             wrap(noiseLevelCallback, CB_F, ident),
+            wrap(spectralPulseCallback, CB_FIJ, ident),
+            wrap(audioPulseCallback, CB_FI, ident),
         )
         _check(load().sdrg_engine_set_callbacks(self._h, ctypes.byref(self._cbs)), "read")
 
@@ -277,6 +342,28 @@ class Engine:
 
     def reset_state(self) -> None:
         _check(load().sdrg_engine_reset_state(self._h), "reset_state")
+
+    def set_spectral_pulse_config(self, cfg: PulseConfig) -> None:
+        """SpectralPulseDetector::configure for every stream (state kept)."""
+        _check(load().sdrg_engine_set_spectral_pulse_config(self._h, ctypes.byref(cfg)), "set_spectral_pulse_config")
+
+    def setPulseConfig(self, cfg: PulseConfig) -> None:
+        """SSBProcessor::setPulseConfig: fresh AudioPulseDetectors with cfg from the next frame."""
+        _check(load().sdrg_engine_set_audio_pulse_config(self._h, ctypes.byref(cfg)), "setPulseConfig")
+
+    def pulse_outputs(self, spectral: bool = True, audio: bool = True):
+        """Host copies of the last call's pulse-detector outputs (PULSE_OUTPUT_DTYPE arrays, or None)."""
+        sp = np.zeros(self.n_streams, PULSE_OUTPUT_DTYPE) if spectral else None
+        au = np.zeros(self.n_streams, PULSE_OUTPUT_DTYPE) if audio else None
+        ptr = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        _check(load().sdrg_engine_get_pulse_outputs(self._h, ptr(sp), ptr(au)), "get_pulse_outputs")
+        return sp, au
+
+    def pulse_output_ptrs(self):
+        """Device pointers of the last call's pulse outputs (valid until the next call)."""
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _check(load().sdrg_engine_pulse_outputs(self._h, ctypes.byref(a), ctypes.byref(b)), "pulse_outputs")
+        return a.value, b.value
 
     def process(self, iq: np.ndarray, fmt: int = CS8, stages: int = STAGE_ALL, now_ms: int = 0):
         """Host path: iq is [n_streams][samplesPerReading * 2] raw samples. Returns (spectra, records, pcm)."""
@@ -324,6 +411,79 @@ class Engine:
     def close(self) -> None:
         if getattr(self, "_h", None):
             load().sdrg_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PulseBank:
+    """n_streams beacon pulse detectors of one kind (SpectralPulseDetector or AudioPulseDetector) on one GPU."""
+
+    def __init__(self, kind: int, n_streams: int, cfg: PulseConfig | None = None, device: int = 0):
+        L = load()
+        self.kind = kind
+        self.n_streams = n_streams
+        c = cfg if cfg is not None else PulseConfig.default(kind)
+        h = ctypes.c_void_p()
+        _check(L.sdrg_pulse_bank_create(kind, ctypes.byref(c), n_streams, device, ctypes.byref(h)),
+               "sdrg_pulse_bank_create")
+        self._h = h
+
+    def configure(self, cfg: PulseConfig) -> None:
+        _check(load().sdrg_pulse_bank_configure(self._h, ctypes.byref(cfg)), "pulse_bank_configure")
+
+    def config(self) -> PulseConfig:
+        c = PulseConfig()
+        _check(load().sdrg_pulse_bank_get_config(self._h, ctypes.byref(c)), "pulse_bank_get_config")
+        return c
+
+    def reset(self) -> None:
+        _check(load().sdrg_pulse_bank_reset(self._h), "pulse_bank_reset")
+
+    def set_stream(self, hip_stream: int | None) -> None:
+        _check(load().sdrg_pulse_bank_set_stream(self._h, hip_stream), "pulse_bank_set_stream")
+
+    def process_spectral(self, snr_sigma: np.ndarray, freq_hz: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(snr_sigma, np.float32)
+        b = np.ascontiguousarray(freq_hz, np.float32)
+        if a.size != self.n_streams or b.size != self.n_streams:
+            raise SdrgError("one value per stream expected")
+        out = np.zeros(self.n_streams, PULSE_OUTPUT_DTYPE)
+        p = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        _check(load().sdrg_pulse_bank_process_spectral_host(self._h, p(a), p(b), p(out)), "process_spectral_host")
+        return out
+
+    def process_audio(self, block: np.ndarray) -> np.ndarray:
+        """block: [n_streams][n] int16 (or float32) samples, one block per stream."""
+        a = np.ascontiguousarray(block)
+        fmt = 0 if a.dtype == np.int16 else 1
+        if fmt:
+            a = np.ascontiguousarray(a, np.float32)
+        if a.ndim != 2 or a.shape[0] != self.n_streams:
+            raise SdrgError("block must be [n_streams][n]")
+        out = np.zeros(self.n_streams, PULSE_OUTPUT_DTYPE)
+        p = lambda x: x.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        _check(load().sdrg_pulse_bank_process_audio_host(self._h, p(a), fmt, a.shape[1], p(out)), "process_audio_host")
+        return out
+
+    def process_spectral_device(self, snr_ptr: int, freq_ptr: int, stride_bytes: int, out_ptr: int) -> None:
+        _check(load().sdrg_pulse_bank_process_spectral_device(self._h, snr_ptr, freq_ptr, stride_bytes, out_ptr),
+               "process_spectral_device")
+
+    def process_audio_device(self, audio_ptr: int, sample_format: int, n: int, stride: int, out_ptr: int) -> None:
+        _check(load().sdrg_pulse_bank_process_audio_device(self._h, audio_ptr, sample_format, n, stride, out_ptr),
+               "process_audio_device")
+
+    def synchronize(self) -> None:
+        _check(load().sdrg_pulse_bank_synchronize(self._h), "pulse_bank_synchronize")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            load().sdrg_pulse_bank_destroy(self._h)
             self._h = None
 
     def __del__(self):
