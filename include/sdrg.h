@@ -53,7 +53,8 @@ typedef enum sdrg_iq_format {
     SDRG_IQ_CF32 = 0,
     SDRG_IQ_CS8 = 1,
     SDRG_IQ_CU8 = 2,
-    SDRG_IQ_CS16 = 3
+    SDRG_IQ_CS16 = 3,
+    SDRG_IQ_CS12 = 4   /* packed 12-bit (3 bytes per complex sample): sdrg_ingest input only, repacked to CS16 */
 } sdrg_iq_format;
 
 /* Which stages a process call runs (bitmask). */
@@ -222,6 +223,31 @@ int32_t sdrg_pulse_bank_process_audio_host(sdrg_pulse_bank *bank, const void *au
 int32_t sdrg_pulse_bank_synchronize(sdrg_pulse_bank *bank);
 /* Run the device-pointer calls on the caller's HIP stream (a hipStream_t; NULL = the bank's own stream). */
 int32_t sdrg_pulse_bank_set_stream(sdrg_pulse_bank *bank, void *hip_stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * Ingest: exact-N re-chunking of raw device reads (rx_reading_thread, sdr-bridge-java-soapy.cpp:503-575).
+ * Reads of any length are appended per stream (accBuffer); every exact samples_per_reading block becomes a
+ * frame in a per-stream queue of at most queue_max frames, the oldest dropped when full (RX_QUEUE_MAX = 20,
+ * :121, :556-564).  Frames are popped one per stream into a [n_streams][N] batch in the engine format
+ * (sdrg_ingest_output_format: the input format, except CS12 which is repacked to CS16).  Host-only.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct sdrg_ingest sdrg_ingest;
+int32_t sdrg_ingest_create(int32_t n_streams, int32_t samples_per_reading, int32_t in_format, int32_t queue_max,
+                           sdrg_ingest **out);
+int32_t sdrg_ingest_destroy(sdrg_ingest *ing);
+int32_t sdrg_ingest_output_format(const sdrg_ingest *ing);
+/* readStream() returned n_samples complex samples in the input format for `stream` */
+int32_t sdrg_ingest_push(sdrg_ingest *ing, int32_t stream, const void *raw, int64_t n_samples);
+/* queued frames, samples of the partial frame, frames dropped from a full queue so far */
+int32_t sdrg_ingest_status(const sdrg_ingest *ing, int32_t stream, int32_t *queued, int32_t *partial_samples,
+                           int64_t *dropped_frames);
+/* when every stream has a queued frame: pop one per stream into out [n_streams][N] and set *popped = 1;
+ * otherwise *popped = 0 and nothing changes */
+int32_t sdrg_ingest_pop_batch(sdrg_ingest *ing, void *out, int32_t *popped);
+/* one stream's oldest frame (rx_process_thread's pop, :597-603) */
+int32_t sdrg_ingest_pop(sdrg_ingest *ing, int32_t stream, void *out, int32_t *popped);
+/* setSamplesPerReading: cut at n from now on (queued frames of the old size are discarded) */
+int32_t sdrg_ingest_set_samples_per_reading(sdrg_ingest *ing, int32_t n);
 
 typedef struct sdrg_engine sdrg_engine;
 

@@ -26,7 +26,7 @@ PKG = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("SDRG_LIB_PATH") or os.path.join(PKG, "lib", "libsdrg.so")  # override: diagnostic builds
 
 # include/sdrg.h
-CF32, CS8, CU8, CS16 = 0, 1, 2, 3
+CF32, CS8, CU8, CS16, CS12 = 0, 1, 2, 3, 4
 STAGE_SPECTRUM, STAGE_STATS, STAGE_SSB, STAGE_HOT_PATH = 1, 2, 4, 7
 STAGE_SPECTRAL_PULSE, STAGE_AUDIO_PULSE, STAGE_ALL = 8, 16, 31
 PULSE_SPECTRAL, PULSE_AUDIO = 0, 1
@@ -88,6 +88,8 @@ EXPORTS = [
     "sdrg_pulse_bank_get_config", "sdrg_pulse_bank_reset", "sdrg_pulse_bank_process_spectral_device",
     "sdrg_pulse_bank_process_audio_device", "sdrg_pulse_bank_process_spectral_host",
     "sdrg_pulse_bank_process_audio_host", "sdrg_pulse_bank_synchronize", "sdrg_pulse_bank_set_stream",
+    "sdrg_ingest_create", "sdrg_ingest_destroy", "sdrg_ingest_output_format", "sdrg_ingest_push", "sdrg_ingest_status",
+    "sdrg_ingest_pop_batch", "sdrg_ingest_pop", "sdrg_ingest_set_samples_per_reading",
 ]
 
 
@@ -218,6 +220,14 @@ def load() -> ctypes.CDLL:
         "sdrg_pulse_bank_process_audio_host": (_I32, [P, P, _I32, _I32, P]),
         "sdrg_pulse_bank_synchronize": (_I32, [P]),
         "sdrg_pulse_bank_set_stream": (_I32, [P, P]),
+        "sdrg_ingest_create": (_I32, [_I32, _I32, _I32, _I32, ctypes.POINTER(P)]),
+        "sdrg_ingest_destroy": (_I32, [P]),
+        "sdrg_ingest_output_format": (_I32, [P]),
+        "sdrg_ingest_push": (_I32, [P, _I32, P, _I64]),
+        "sdrg_ingest_status": (_I32, [P, _I32, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I64)]),
+        "sdrg_ingest_pop_batch": (_I32, [P, P, ctypes.POINTER(_I32)]),
+        "sdrg_ingest_pop": (_I32, [P, _I32, P, ctypes.POINTER(_I32)]),
+        "sdrg_ingest_set_samples_per_reading": (_I32, [P, _I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -484,6 +494,69 @@ class PulseBank:
     def close(self) -> None:
         if getattr(self, "_h", None):
             load().sdrg_pulse_bank_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+IN_BYTES_PER_SAMPLE = {CF32: 8, CS16: 4, CS8: 2, CU8: 2, CS12: 3}
+
+
+class Ingest:
+    """Exact-N re-chunking of raw reads per stream (rx_reading_thread, sdr-bridge-java-soapy.cpp:503-575)."""
+
+    def __init__(self, n_streams: int, samples_per_reading: int, in_format: int = CS8, queue_max: int = 20):
+        h = ctypes.c_void_p()
+        _check(load().sdrg_ingest_create(n_streams, samples_per_reading, in_format, queue_max, ctypes.byref(h)),
+               "sdrg_ingest_create")
+        self._h = h
+        self.n_streams, self.n, self.in_format = n_streams, samples_per_reading, in_format
+        self.out_format = int(load().sdrg_ingest_output_format(h))
+
+    def push(self, stream: int, raw: np.ndarray) -> None:
+        """raw: the bytes of whole complex samples in the input format (any numpy dtype)."""
+        b = np.ascontiguousarray(raw).view(np.uint8).reshape(-1)
+        bps = IN_BYTES_PER_SAMPLE[self.in_format]
+        if b.size % bps:
+            raise SdrgError("partial sample")
+        _check(load().sdrg_ingest_push(self._h, stream, b.ctypes.data_as(ctypes.c_void_p), b.size // bps),
+               "ingest_push")
+
+    def status(self, stream: int):
+        q, p, d = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        _check(load().sdrg_ingest_status(self._h, stream, ctypes.byref(q), ctypes.byref(p), ctypes.byref(d)),
+               "ingest_status")
+        return q.value, p.value, d.value
+
+    def _frame_dtype(self):
+        return NUMPY_DTYPE[self.out_format]
+
+    def pop_batch(self):
+        """[n_streams][N*2] frames in the output format, or None when some stream has no frame yet."""
+        out = np.empty((self.n_streams, 2 * self.n), self._frame_dtype())
+        got = ctypes.c_int32()
+        _check(load().sdrg_ingest_pop_batch(self._h, out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(got)),
+               "ingest_pop_batch")
+        return out if got.value else None
+
+    def pop(self, stream: int):
+        out = np.empty(2 * self.n, self._frame_dtype())
+        got = ctypes.c_int32()
+        _check(load().sdrg_ingest_pop(self._h, stream, out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(got)),
+               "ingest_pop")
+        return out if got.value else None
+
+    def set_samples_per_reading(self, n: int) -> None:
+        _check(load().sdrg_ingest_set_samples_per_reading(self._h, n), "ingest_set_samples_per_reading")
+        self.n = n
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            load().sdrg_ingest_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -272,3 +272,37 @@ def test_full_size_batch_properties(S, O):
     assert torch.equal(d_spec, d_spec2) and torch.equal(d_pcm, d_pcm2)
     eng.close()
     eng2.close()
+
+
+def test_ingest_cs12_reads_to_engine(S, O):
+    """§8(f) ingest: packed CS12 reads of random lengths -> exact-N frames (repacked to CS16) -> engine; the
+    spectrum within the FFT tolerance and the PCM bit-exact against the oracle on the same CS16 frames."""
+    rng = np.random.default_rng(1212)
+    n, fs, B, F = 4096, 2_000_000, 8, 3
+    ing = S.Ingest(B, n, S.CS12)
+    # a CS16 tone scaled to 12 bits, packed as CS12 (I = v & 0xfff in b0 | b1 low nibble, Q in b1 high | b2)
+    tone = O.synth_frames(B * F, n, O.CS16, tone_hz=1500.0, fs=fs, amp=8000.0, seed=77).reshape(B, F * 2 * n)
+    v12 = (tone.astype(np.int32) >> 4) & 0xFFF
+    i, q = v12[:, 0::2], v12[:, 1::2]
+    packed = np.stack([i & 0xFF, ((i >> 8) & 0xF) | ((q & 0xF) << 4), q >> 4], axis=-1).astype(np.uint8)
+    packed = packed.reshape(B, -1)
+    for b in range(B):
+        off = 0
+        while off < F * n:
+            k = int(min(rng.integers(1, 3000), F * n - off))
+            ing.push(b, packed[b, 3 * off: 3 * (off + k)])
+            off += k
+    eng = engine(S, n, fs, B)
+    sst = [O.SsbState() for _ in range(B)]
+    for f in range(F):
+        frames = ing.pop_batch()
+        assert frames is not None and frames.dtype == np.int16
+        spec, rec, pcm = eng.process(frames, fmt=S.CS16, now_ms=1000 + f)
+        for b in range(B):
+            iq = O.unpack(O.CS16, frames[b], n)
+            assert spectrum_ok(spec[b], O.power_shifted(iq, use_f64=True)).all()
+            np.testing.assert_array_equal(pcm[b], sst[b].process(iq, fs, 1))
+            # the repacked values are the 12-bit samples << 4
+            np.testing.assert_array_equal(frames[b] >> 4, (tone[b, f * 2 * n:(f + 1) * 2 * n] >> 4))
+    assert ing.pop_batch() is None
+    eng.close()
