@@ -425,23 +425,35 @@ hipError_t launch_n(const void *iq, int fmt, int n_frames, const float *tw, floa
 // ================================================================================================
 // N = 16384, the benchmark size: persistent kernel, two 512-thread workgroups per CU (4 waves per SIMD),
 // each looping over frames blockIdx.x, + gridDim.x, ...  Stockham plan 32 x 32 x 16 with the twiddles in LDS:
-//   pass 1 twiddle w_1024^(r k), k = j mod 32           : P1[r][k]                     (8 KiB table)
-//   pass 2 twiddle w_16384^(r k), k = j = 32 k_hi + k_lo : P1[2r][k_hi] * A2[r][k_lo]    (3.75 KiB table)
-// (w_16384^(32 r k_hi) = w_512^(r k_hi) = w_1024^(2 r k_hi); one extra complex multiply per pass-2 twiddle
-// instead of 128 KiB of twiddle reads per frame from L2).  The next frame's raw samples are loaded into
-// registers before this frame's |X|^2 stores, so the in-order vmcnt wait at the top of the next iteration
-// does not also wait for the stores.  LDS per workgroup: 66 KiB half-frame exchange + 11.75 KiB tables.
-// Measured (tools/fftlab, 4096 CS8 frames): ~126 us vs 137-150 us for the generic kernel at this size.
+//   pass 1 twiddle w_1024^(r k), k = j mod 32 : P1[r][k]  (8 KiB table)
+//   pass 2 twiddle w_16384^(r j), j = 2t + b  : (w^j)^r, w^j = P1[2][j / 32] * A2[j mod 32]  (w_16384^(32 k) =
+//     w_1024^(2 k)); the 15 powers by repeated products (error ~r ulp, far inside the parity bound): 2 LDS reads
+//     and 30 complex multiplies per thread instead of 30 table reads + 30 multiplies to compose factors.
+// The next frame's raw samples are loaded into registers before this frame's |X|^2 stores, so the in-order
+// vmcnt wait at the top of the next iteration does not also wait for the stores; the stores are
+// non-temporal (the spectra are written once, not re-read by this kernel).  LDS per workgroup: 66 KiB
+// half-frame exchange + 8.25 KiB tables.
+// Measured (tools/fftlab, 4096 CS8 frames, tools/fftlab/run_variants.sh): ~107 us; the composed-factor
+// twiddles with plain stores ~126 us, the generic kernel at this size 137-150 us.
 // ================================================================================================
 namespace k16 {
+
+// Lab-only ablations (tools/fftlab builds with -DSDRG_K16_ABLATE=mask; results are wrong when set):
+// 1 pass-1 twiddles off, 2 pass-2 twiddles off, 4 exchanges off, 8 DFTs off, 16 stores off
+#ifndef SDRG_K16_ABLATE
+#define SDRG_K16_ABLATE 0
+#endif
+constexpr int ABL = SDRG_K16_ABLATE;
 
 constexpr int LOG2N = 14, N = 1 << LOG2N, T = N / E, HALF = N / 2;
 constexpr int XCH_F2 = HALF + HALF / 32;  // padded half-frame exchange buffer, f2 slots
 constexpr int P1_F2 = 32 * 32;            // P1[r][k] = w_1024^(r k), r, k < 32
-constexpr int A2_F4 = 15 * 16;            // A2[r-1][m] = (w_16384^(r 2m), w_16384^(r (2m+1))), r = 1..15
+constexpr int A2_F4 = 16;                 // A2[m] = (w_16384^(2m), w_16384^(2m+1)), m < 16
 constexpr int TAB_FLOATS = 2 * P1_F2 + 4 * A2_F4;
 constexpr int LDS_BYTES = XCH_F2 * 8 + P1_F2 * 8 + A2_F4 * 16;
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
+
+typedef float f2s __attribute__((ext_vector_type(2)));
 
 // raw samples x[t + 512 r] of frame f into registers (zero-extended 16/32-bit words)
 template <int FMT>
@@ -466,9 +478,7 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
     __syncthreads();
     constexpr int BPS = bytes_per_sample<FMT>();
     constexpr float S = power_scale<FMT>();
-    const f2 *p1_row = p1 + (t & 31);     // pass 1: P1[r][k], k = t mod 32
-    const f2 *b_row = p1 + (t >> 4);      // pass 2: P1[2r][k_hi], k_hi = t / 16
-    const float4 *a_row = a2 + (t & 15);  // pass 2: A2[r][m], m = t mod 16
+    const f2 *p1_row = p1 + (t & 31);  // pass 1: P1[r][k], k = t mod 32
 
     constexpr bool STAGE = FMT != SDRG_IQ_CF32;  // CF32 (8 B/sample) loads at the top of the iteration
     uint32_t raw[E];
@@ -487,31 +497,47 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
             for (int r = 0; r < E; ++r) v[r] = load_unscaled<FMT>(rs, t * BPS, r * (N / 32) * BPS);
         }
         const int next = frame + gridDim.x;
-        dft<32>(v);
-        exchange<LOG2N, 32, 1, 32, false>(xch, v);
+        if constexpr (!(ABL & 8)) dft<32>(v);
+        if constexpr (!(ABL & 4)) exchange<LOG2N, 32, 1, 32, false>(xch, v);
         // ---- pass 1: radix 32, NS = 32 ----
+        if constexpr (!(ABL & 1)) {
 #pragma unroll
-        for (int r = 1; r < 32; ++r) v[r] = cmul_v(v[r], p1_row[r * 32]);
-        dft<32>(v);
-        exchange<LOG2N, 32, 32, 16, true>(xch, v);
+            for (int r = 1; r < 32; ++r) v[r] = cmul_v(v[r], p1_row[r * 32]);
+        }
+        if constexpr (!(ABL & 8)) dft<32>(v);
+        if constexpr (!(ABL & 4)) exchange<LOG2N, 32, 32, 16, true>(xch, v);
         // ---- pass 2: radix 16, NS = 1024, butterflies j = 2t + b held as v[16 b + r] ----
+        if constexpr (!(ABL & 2)) {
+            f2 wa, wb;  // w_16384^j for j = 2t, 2t + 1
+            {
+                const f2 bw = p1[2 * 32 + (t >> 4)];
+                const float4 aw = a2[t & 15];
+                wa = cmul_v(bw, f2{aw.x, aw.y});
+                wb = cmul_v(bw, f2{aw.z, aw.w});
+            }
+            f2 pa = wa, pb = wb;
 #pragma unroll
-        for (int r = 1; r < 16; ++r) {
-            const f2 bw = b_row[2 * r * 32];
-            const float4 aw = a_row[(r - 1) * 16];
-            v[r] = cmul_v(v[r], cmul_v(bw, f2{aw.x, aw.y}));
-            v[16 + r] = cmul_v(v[16 + r], cmul_v(bw, f2{aw.z, aw.w}));
+            for (int r = 1; r < 16; ++r) {
+                if (r > 1) {
+                    pa = cmul_v(pa, wa);
+                    pb = cmul_v(pb, wb);
+                }
+                v[r] = cmul_v(v[r], pa);
+                v[16 + r] = cmul_v(v[16 + r], pb);
+            }
         }
         f2 x0[16], x1[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) { x0[r] = v[r]; x1[r] = v[16 + r]; }
-        dft<16>(x0);
-        dft<16>(x1);
+        if constexpr (!(ABL & 8)) {
+            dft<16>(x0);
+            dft<16>(x1);
+        }
         // ---- |X|^2 at the fftshifted index: outputs j + 1024 r, j = 2t, 2t + 1 ----
-        float2 pw[16];
+        f2s pw[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-            pw[r] = make_float2((x0[r].x * x0[r].x + x0[r].y * x0[r].y) * S, (x1[r].x * x1[r].x + x1[r].y * x1[r].y) * S);
+            pw[r] = f2s{(x0[r].x * x0[r].x + x0[r].y * x0[r].y) * S, (x1[r].x * x1[r].x + x1[r].y * x1[r].y) * S};
         if constexpr (STAGE) {
             if (next < n_frames) {
                 issue_raw<FMT>(iq, next, t, raw);
@@ -521,8 +547,16 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
             }
         }
         float *o = spectra + (size_t)frame * N + 2 * t;
+        if constexpr (ABL & 16) {  // keep the values live without the stores
+            float acc = 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) *reinterpret_cast<float2 *>(o + ((r * 1024 + N / 2) & (N - 1))) = pw[r];
+            for (int r = 0; r < 16; ++r) acc += pw[r].x + pw[r].y;
+            if (acc == 1.2345f) o[0] = acc;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                __builtin_nontemporal_store(pw[r], reinterpret_cast<f2s *>(o + ((r * 1024 + N / 2) & (N - 1))));
+        }
     }
 }
 
@@ -535,13 +569,12 @@ void fill_tables(float *out) {
             out[2 * (r * 32 + k) + 1] = (float)sin(a);
         }
     float *a2 = out + 2 * P1_F2;
-    for (int r = 1; r < 16; r++)
-        for (int m = 0; m < 16; m++)
-            for (int b = 0; b < 2; b++) {
-                const double a = -2.0 * M_PI * (double)(r * (2 * m + b)) / 16384.0;
-                a2[4 * ((r - 1) * 16 + m) + 2 * b] = (float)cos(a);
-                a2[4 * ((r - 1) * 16 + m) + 2 * b + 1] = (float)sin(a);
-            }
+    for (int m = 0; m < 16; m++)
+        for (int b = 0; b < 2; b++) {
+            const double a = -2.0 * M_PI * (double)(2 * m + b) / 16384.0;
+            a2[4 * m + 2 * b] = (float)cos(a);
+            a2[4 * m + 2 * b + 1] = (float)sin(a);
+        }
 }
 
 int device_cus() {

@@ -514,6 +514,20 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
             const int c = it - 2;
             if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 2) || lane < PG)) {
                 const int lim = min(CH, S - c * CH);
+#ifdef SDRG_DIAG_LPF_NOLDS  // diagnostic build only: the recurrence on register data, no LDS traffic
+                if (true) {
+                    float v[CH];
+#pragma unroll
+                    for (int q = 0; q < CH; q++) v[q] = (float)(q + c) * 1e-3f;
+#pragma unroll
+                    for (int q = 0; q < CH; q++) {
+                        const f2v p1 = c1 * z1, p2 = c2 * z2;
+                        const float y = (((v[q] + p1.x) + p2.x) + p1.y) + p2.y;
+                        z2 = z1;
+                        z1 = y;
+                    }
+                } else
+#endif
                 if (lim == CH) {
                     row_pipeline(&L.a[c & 1][my_s * ROW], &L.y[c & 3][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll

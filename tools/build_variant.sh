@@ -8,5 +8,8 @@ HIP="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-
 $HIP -c $D/csrc/spectrum.hip -o $B/spectrum.o
 $HIP -ffp-contract=off -c $D/csrc/stats.hip -o $B/stats.o
 $HIP -ffp-contract=off -fno-slp-vectorize -c $D/csrc/ssb.hip -o $B/ssb.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/lib/libsdrg_$NAME.so $B/spectrum.o $B/stats.o $B/ssb.o $D/build/design.o $D/build/engine.o $D/build/compat.o -lm
+$HIP -ffp-contract=off -c $D/csrc/pulse.hip -o $B/pulse.o
+make -s -C $D  # host objects
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/lib/libsdrg_$NAME.so $B/spectrum.o $B/stats.o $B/ssb.o $B/pulse.o \
+    $D/build/design.o $D/build/engine.o $D/build/pulse_bank.o $D/build/ingest.o $D/build/compat.o -lm
 echo built $D/lib/libsdrg_$NAME.so
