@@ -5,7 +5,7 @@
 export TMPDIR=/tmp
 TAG=${1:-r1}
 STEPS=${STEPS:-20}
-python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { echo "build failed"; exit 1; }
+# (the library is built in-tree on the CPU side before the call)
 timeout -k 10 300 python bench.py --steps 50 --warmup 5 > gpurun_out/bench_$TAG.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench_$TAG.log; exit 1; }
 echo "bench: $(tail -1 gpurun_out/bench_$TAG.log | cut -c1-200)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline > gpurun_out/prof_bench_$TAG.log 2>&1 || { echo "rocprof stats failed"; exit 1; }

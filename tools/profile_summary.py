@@ -19,7 +19,8 @@ TAG = sys.argv[1] if len(sys.argv) > 1 else "r1"
 OUT = "profiles"
 os.makedirs(OUT, exist_ok=True)
 ENGINE = ("spectrum16k_kernel", "spectrum_kernel", "stats_kernel", "ssb_pipe_kernel", "four_step_a", "four_step_b", "ssb_chain_kernel",
-          "ssb_fir_kernel", "ssb_eq_kernel")
+          "ssb_fir_kernel", "ssb_eq_kernel", "spectral_pulse_kernel", "audio_pulse_kernel", "audio_front_kernel",
+          "pulse_reset_kernel")
 
 
 def short(name: str) -> str:
