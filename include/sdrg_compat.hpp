@@ -76,5 +76,78 @@ void processSSB_opt(std::vector<std::complex<float>> iq, uint32_t sampleRate, bo
 // Status of the last processSSB_opt call.
 int32_t lastSsbStatus();
 
+// SpectralPulseDetector (src/dsp/spectral_pulse_detector.h:19-79) and AudioPulseDetector
+// (src/ssb/audio_pulse_detector.h:15-104): same public interface; each object owns a one-stream
+// sdrg_pulse_bank, so its state machine runs in the GPU kernels (csrc/pulse.hip).
+enum class PulseLevel { NONE = 0, LOW = 1, MEDIUM = 2, STRONG = 3 };
+
+class SpectralPulseDetector {
+public:
+    using PulseLevel = compat::PulseLevel;
+    struct Config {  // spectral_pulse_detector.h:23-35
+        float fsEnergy = 20.f, zDefaultS = 0.666f, tTargetInit = 1.75f, dtTolS = 0.150f;
+        float snrMin = 1.5f, snrRhythm = 2.5f, snrStrong = 4.0f, dispersionMax = 1.3f;
+        int sumNMax = 7;
+        float liveWindowT = 4.0f, liveDivisor = 3.0f;
+    };
+    SpectralPulseDetector() : SpectralPulseDetector(Config{}) {}
+    explicit SpectralPulseDetector(const Config &cfg);
+    ~SpectralPulseDetector();
+    SpectralPulseDetector(const SpectralPulseDetector &) = delete;
+    SpectralPulseDetector &operator=(const SpectralPulseDetector &) = delete;
+
+    void configure(const Config &cfg);
+    PulseLevel process(float snrSigma, float freqHz);
+    PulseLevel pulseDetected() const { return static_cast<PulseLevel>(out_.level); }
+    float lastPulseStrength() const { return out_.strength; }
+    bool isLocked() const { return out_.locked != 0; }
+    float lockedPeriodS() const { return out_.period_s; }
+    int liveEtat() const { return out_.live_etat; }
+    float estimatedFreqHz() const { return out_.est_freq_hz; }
+    void reset();
+    int32_t lastStatus() const { return status_; }
+
+private:
+    sdrg_pulse_bank *bank_ = nullptr;
+    sdrg_pulse_output out_{};
+    float t_target_init_ = 1.75f;
+    int32_t status_ = SDRG_OK;
+};
+
+class AudioPulseDetector {
+public:
+    using PulseLevel = compat::PulseLevel;
+    struct Config {  // audio_pulse_detector.h:19-37
+        float sampleRate = 48000.f, fMin = 1500.f, fMax = 4000.f, fsEnergy = 100.f, smoothCutoff = 5.f;
+        float zDefaultS = 0.666f, tTargetInit = 1.75f, dtTolS = 0.150f;
+        float snrMin = 1.0f, snrRhythm = 1.1f, snrStrong = 2.0f, dispersionMax = 1.3f;
+        int sumNMax = 7;
+        float liveWindowT = 4.0f, liveDivisor = 3.0f;
+        int noiseRefFar = 80, noiseRefNear = 40;
+    };
+    AudioPulseDetector() : AudioPulseDetector(Config{}) {}
+    explicit AudioPulseDetector(const Config &cfg);
+    ~AudioPulseDetector();
+    AudioPulseDetector(const AudioPulseDetector &) = delete;
+    AudioPulseDetector &operator=(const AudioPulseDetector &) = delete;
+
+    PulseLevel process(const std::vector<float> &audio);
+    PulseLevel process(const std::vector<int16_t> &pcm);
+    PulseLevel pulseDetected() const { return static_cast<PulseLevel>(out_.level); }
+    float lastPulseStrength() const { return out_.strength; }
+    bool isLocked() const { return out_.locked != 0; }
+    float lockedPeriodS() const { return out_.period_s; }
+    int liveEtat() const { return out_.live_etat; }
+    void reset();
+    int32_t lastStatus() const { return status_; }
+
+private:
+    PulseLevel run(const void *samples, int fmt, size_t n);
+    sdrg_pulse_bank *bank_ = nullptr;
+    sdrg_pulse_output out_{};
+    float t_target_init_ = 1.75f;
+    int32_t status_ = SDRG_OK;
+};
+
 }  // namespace compat
 }  // namespace sdrg

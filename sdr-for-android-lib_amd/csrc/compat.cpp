@@ -127,5 +127,115 @@ void processSSB_opt(std::vector<std::complex<float>> iq, uint32_t sampleRate, bo
     if (g_ssb_status) pcmOut.clear();
 }
 
+// ---- pulse detectors ------------------------------------------------------------------------------
+namespace {
+
+sdrg_pulse_config spectral_cfg(const SpectralPulseDetector::Config &c) {
+    sdrg_pulse_config p;
+    sdrg_pulse_config_default(SDRG_PULSE_SPECTRAL, &p);
+    p.fs_energy = c.fsEnergy;
+    p.z_default_s = c.zDefaultS;
+    p.t_target_init = c.tTargetInit;
+    p.dt_tol_s = c.dtTolS;
+    p.snr_min = c.snrMin;
+    p.snr_rhythm = c.snrRhythm;
+    p.snr_strong = c.snrStrong;
+    p.dispersion_max = c.dispersionMax;
+    p.sum_n_max = c.sumNMax;
+    p.live_window_t = c.liveWindowT;
+    p.live_divisor = c.liveDivisor;
+    return p;
+}
+
+sdrg_pulse_config audio_cfg(const AudioPulseDetector::Config &c) {
+    sdrg_pulse_config p;
+    sdrg_pulse_config_default(SDRG_PULSE_AUDIO, &p);
+    p.sample_rate = c.sampleRate;
+    p.f_min = c.fMin;
+    p.f_max = c.fMax;
+    p.fs_energy = c.fsEnergy;
+    p.smooth_cutoff = c.smoothCutoff;
+    p.z_default_s = c.zDefaultS;
+    p.t_target_init = c.tTargetInit;
+    p.dt_tol_s = c.dtTolS;
+    p.snr_min = c.snrMin;
+    p.snr_rhythm = c.snrRhythm;
+    p.snr_strong = c.snrStrong;
+    p.dispersion_max = c.dispersionMax;
+    p.sum_n_max = c.sumNMax;
+    p.live_window_t = c.liveWindowT;
+    p.live_divisor = c.liveDivisor;
+    p.noise_ref_far = c.noiseRefFar;
+    p.noise_ref_near = c.noiseRefNear;
+    return p;
+}
+
+void fresh_output(sdrg_pulse_output &o, float t_target_init) {
+    std::memset(&o, 0, sizeof(o));
+    o.period_s = t_target_init;
+}
+
+}  // namespace
+
+SpectralPulseDetector::SpectralPulseDetector(const Config &cfg) : t_target_init_(cfg.tTargetInit) {
+    const sdrg_pulse_config p = spectral_cfg(cfg);
+    status_ = sdrg_pulse_bank_create(SDRG_PULSE_SPECTRAL, &p, 1, 0, &bank_);
+    if (status_) bank_ = nullptr;
+    fresh_output(out_, t_target_init_);
+}
+
+SpectralPulseDetector::~SpectralPulseDetector() {
+    if (bank_) sdrg_pulse_bank_destroy(bank_);
+}
+
+// configure (spectral_pulse_detector.cpp:6-8): the config only; tTarget_ and the history are kept
+void SpectralPulseDetector::configure(const Config &cfg) {
+    const sdrg_pulse_config p = spectral_cfg(cfg);
+    if (bank_) status_ = sdrg_pulse_bank_configure(bank_, &p);
+}
+
+SpectralPulseDetector::PulseLevel SpectralPulseDetector::process(float snrSigma, float freqHz) {
+    if (!bank_) return pulseDetected();
+    status_ = sdrg_pulse_bank_process_spectral_host(bank_, &snrSigma, &freqHz, &out_);
+    return pulseDetected();
+}
+
+void SpectralPulseDetector::reset() {
+    if (bank_) status_ = sdrg_pulse_bank_reset(bank_);
+    sdrg_pulse_config c;
+    if (bank_ && sdrg_pulse_bank_get_config(bank_, &c) == SDRG_OK) t_target_init_ = c.t_target_init;
+    fresh_output(out_, t_target_init_);
+}
+
+AudioPulseDetector::AudioPulseDetector(const Config &cfg) : t_target_init_(cfg.tTargetInit) {
+    const sdrg_pulse_config p = audio_cfg(cfg);
+    status_ = sdrg_pulse_bank_create(SDRG_PULSE_AUDIO, &p, 1, 0, &bank_);
+    if (status_) bank_ = nullptr;
+    fresh_output(out_, t_target_init_);
+}
+
+AudioPulseDetector::~AudioPulseDetector() {
+    if (bank_) sdrg_pulse_bank_destroy(bank_);
+}
+
+AudioPulseDetector::PulseLevel AudioPulseDetector::run(const void *samples, int fmt, size_t n) {
+    if (!bank_) return pulseDetected();
+    status_ = sdrg_pulse_bank_process_audio_host(bank_, samples, fmt, (int32_t)n, &out_);
+    return pulseDetected();
+}
+
+AudioPulseDetector::PulseLevel AudioPulseDetector::process(const std::vector<float> &audio) {
+    return run(audio.data(), 1, audio.size());
+}
+
+AudioPulseDetector::PulseLevel AudioPulseDetector::process(const std::vector<int16_t> &pcm) {
+    return run(pcm.data(), 0, pcm.size());
+}
+
+void AudioPulseDetector::reset() {
+    if (bank_) status_ = sdrg_pulse_bank_reset(bank_);
+    fresh_output(out_, t_target_init_);
+}
+
 }  // namespace compat
 }  // namespace sdrg

@@ -1,0 +1,169 @@
+// sdrg_jni_bridge.hpp — the SDRBridge JNI surface of the reference (src/sdr-bridge-java-soapy.cpp:625-1171)
+// over the engine's C ABI, written once against a JNI "traits" type so the same logic runs under the real
+// JNIEnv (sdrg_jni.cpp, built with the Android NDK's jni.h) and under a recording fake in the tests
+// (tests/cpp/jni_bridge_test.cpp) — there is no JVM in this image.
+//
+// What it replaces, per reference function:
+//   applyConfig(9 SDRConfig fields)  :1073-1141  -> sdrg_engine_create / _apply_config (+ the spectral pulse
+//                                                    detector's fsEnergy, done by the engine)
+//   read(12 callbacks)               :625-764    -> global refs + "invoke" method IDs with the reference's
+//                                                    signatures; frames then arrive through onFrame()
+//   soapyCallback(buf, len)          :424-493    -> onFrame(): one engine call for FFT + stats + spectral pulse
+//   SSB worker loop                  ssb_processor.cpp:80-115 -> the same engine call (SSB + audio pulse);
+//                                                    pcm and audioPulse callbacks after soapyCallback's
+//   stopReading / close              :766-876    -> callbacks dropped / global refs deleted, engine destroyed
+//   setFrequency / setSampleRate / setSamplesPerReading / setFrequencyFocusRange / setSoundMode /
+//   setRefresh*Ms                    :878-1071   -> engine setters / apply_config at the next frame
+//   setPulseConfig                   :1143-1161  -> no-op, as in the reference
+//   getAmbientAudioEnergy            :1163-1166  -> the audio pulse detector's lastPulseStrength()
+// Device I/O (initDongle, getDriver, tuner gains and ranges) stays with SoapySDR and is not part of this.
+#pragma once
+
+#include <algorithm>
+#include <complex>
+#include <cstdint>
+#include <vector>
+
+#include "../../include/sdrg.h"
+
+namespace sdrg {
+namespace jni {
+
+// J must provide: types Env, Obj, Mid; NewGlobalRef, DeleteGlobalRef, MethodOf(env, obj, sig) ("invoke"),
+// ClearException(env); CallF / CallI / CallJ / CallFF / CallFI / CallFIJ / CallFloats / CallShorts.
+template <class J>
+class Bridge {
+public:
+    using Env = typename J::Env;
+    using Obj = typename J::Obj;
+    using Mid = typename J::Mid;
+    enum Callback {
+        FFT, DETECTION_FLAG, MEAN_SNR, MEAN_SNR_SIGMA, PEAK_FREQUENCY, PCM, AUDIO_PULSE, PEAK_ABOVE_NOISE_MEAN,
+        MAX_BIN, BEST_1KHZ, SPECTRAL_PULSE, NOISE_LEVEL, N_CALLBACKS
+    };
+    static constexpr const char *kSignature[N_CALLBACKS] = {"([F)V", "(I)V", "(F)V", "(F)V", "(J)V", "([S)V",
+                                                             "(FI)V", "(F)V", "(FF)V", "(FF)V", "(FIJ)V", "(F)V"};
+
+    ~Bridge() {
+        if (eng_) sdrg_engine_destroy(eng_);
+    }
+
+    bool applyConfig(Env *, int64_t centerFrequency, int64_t sampleRate, int32_t samplesPerReading,
+                     int32_t freqFocusRangeKhz, int32_t gain, int64_t refreshFFTMs, int64_t refreshPeakMs,
+                     int64_t refreshSignalStrengthMs, int32_t soundMode) {
+        cfg_ = sdrg_config{centerFrequency, sampleRate, samplesPerReading, freqFocusRangeKhz, gain, soundMode,
+                           refreshFFTMs, refreshPeakMs, refreshSignalStrengthMs};
+        status_ = eng_ ? sdrg_engine_apply_config(eng_, &cfg_) : sdrg_engine_create(&cfg_, 1, 0, &eng_);
+        if (status_ != SDRG_OK && !eng_) return false;
+        return status_ == SDRG_OK;  // the reference returns false only when a device call throws (:1115-1118)
+    }
+
+    // read(): the 12 callback objects in the reference's parameter order (:625-640)
+    void read(Env *env, const Obj (&cbs)[N_CALLBACKS]) {
+        dropCallbacks(env);
+        for (int i = 0; i < N_CALLBACKS; i++) {
+            if (!cbs[i]) continue;
+            cb_[i].obj = J::NewGlobalRef(env, cbs[i]);
+            cb_[i].mid = J::MethodOf(env, cbs[i], kSignature[i]);
+        }
+        reading_ = true;
+    }
+
+    // One exact-N frame of CF32 samples (the rx_process_thread's chunk, :590-615); now_ms is the clock the
+    // reference reads from steady_clock for its 300 ms tracking latch (fft_process.cpp:333-361).
+    void onFrame(Env *env, const std::complex<float> *buf, uint32_t len, int64_t now_ms) {
+        if (!eng_ || !reading_ || !buf || len == 0) return;
+        if ((uint32_t)cfg_.samples_per_reading != len) {  // the reference processes whatever len it is handed
+            cfg_.samples_per_reading = (int32_t)len;
+            if ((status_ = sdrg_engine_apply_config(eng_, &cfg_)) != SDRG_OK) return;
+        }
+        spec_.resize(len);
+        pcm_.resize((size_t)std::max(0, sdrg_engine_pcm_len(eng_)));
+        status_ = sdrg_engine_process_host(eng_, buf, SDRG_IQ_CF32, SDRG_STAGE_ALL, spec_.data(), &rec_,
+                                           pcm_.empty() ? nullptr : pcm_.data(), now_ms);
+        if (status_ != SDRG_OK) return;  // nothing throws across JNI: the frame is dropped
+        if ((status_ = sdrg_engine_get_pulse_outputs(eng_, &spectral_, &audio_)) != SDRG_OK) return;
+        // soapyCallback (:458-488)
+        if (has(FFT)) J::CallFloats(env, cb_[FFT].obj, cb_[FFT].mid, spec_.data(), (int32_t)len);
+        if (has(DETECTION_FLAG)) J::CallI(env, cb_[DETECTION_FLAG].obj, cb_[DETECTION_FLAG].mid, rec_.detection_flag);
+        if (has(MEAN_SNR)) J::CallF(env, cb_[MEAN_SNR].obj, cb_[MEAN_SNR].mid, rec_.mean_snr_db);
+        if (has(MEAN_SNR_SIGMA)) J::CallF(env, cb_[MEAN_SNR_SIGMA].obj, cb_[MEAN_SNR_SIGMA].mid, rec_.mean_snr_sigma);
+        if (has(PEAK_FREQUENCY)) J::CallJ(env, cb_[PEAK_FREQUENCY].obj, cb_[PEAK_FREQUENCY].mid, rec_.tracking_frequency);
+        if (has(PEAK_ABOVE_NOISE_MEAN))
+            J::CallF(env, cb_[PEAK_ABOVE_NOISE_MEAN].obj, cb_[PEAK_ABOVE_NOISE_MEAN].mid, rec_.peak_above_noise_mean_db);
+        if (has(MAX_BIN)) J::CallFF(env, cb_[MAX_BIN].obj, cb_[MAX_BIN].mid, rec_.max_bin_snr_db, rec_.max_bin_snr_sigma);
+        if (has(BEST_1KHZ))
+            J::CallFF(env, cb_[BEST_1KHZ].obj, cb_[BEST_1KHZ].mid, rec_.best1khz_snr_db, rec_.best1khz_snr_sigma);
+        if (has(NOISE_LEVEL)) J::CallF(env, cb_[NOISE_LEVEL].obj, cb_[NOISE_LEVEL].mid, rec_.per_bin_mean);
+        if (has(SPECTRAL_PULSE))
+            J::CallFIJ(env, cb_[SPECTRAL_PULSE].obj, cb_[SPECTRAL_PULSE].mid, spectral_.input, spectral_.live_etat,
+                       spectral_.est_freq_hz_rounded);
+        // SSB worker (ssb_processor.cpp:105-113): pcm only when the frame produced samples, pulse always
+        if (has(PCM) && !pcm_.empty()) J::CallShorts(env, cb_[PCM].obj, cb_[PCM].mid, pcm_.data(), (int32_t)pcm_.size());
+        if (has(AUDIO_PULSE)) J::CallFI(env, cb_[AUDIO_PULSE].obj, cb_[AUDIO_PULSE].mid, audio_.strength, audio_.live_etat);
+        J::ClearException(env);
+    }
+
+    void stopReading(Env *) { reading_ = false; }
+
+    void close(Env *env) {
+        reading_ = false;
+        dropCallbacks(env);  // every global ref, noiseLevel's included (the reference leaks that one, :826-874)
+        if (eng_) sdrg_engine_destroy(eng_);
+        eng_ = nullptr;
+    }
+
+    void setFrequency(Env *, int64_t hz) {
+        cfg_.center_frequency = hz;
+        if (eng_) status_ = sdrg_engine_set_frequency(eng_, hz);  // raises isCenterFrequencyChanged (:907)
+    }
+    void setSampleRate(Env *, int64_t fs) { reconfigure([&] { cfg_.sample_rate = fs; }); }
+    void setSamplesPerReading(Env *, int32_t n) { reconfigure([&] { cfg_.samples_per_reading = n; }); }
+    void setFrequencyFocusRange(Env *, int32_t khz) {
+        cfg_.freq_focus_range_khz = khz;
+        if (eng_) status_ = sdrg_engine_set_frequency_focus_range(eng_, khz);
+    }
+    void setSoundMode(Env *, int32_t mode) {
+        cfg_.sound_mode = mode;
+        if (eng_) status_ = sdrg_engine_set_sound_mode(eng_, mode);
+    }
+    void setRefreshFFTMs(Env *, int64_t v) { cfg_.refresh_fft_ms = v; }
+    void setRefreshPeakMs(Env *, int64_t v) { cfg_.refresh_peak_ms = v; }
+    void setRefreshSignalStrengthMs(Env *, int64_t v) { cfg_.refresh_signal_strength_ms = v; }
+    void setPulseConfig(Env *) {}  // legacy parameters ignored, defaults kept (:1156-1160)
+    float getAmbientAudioEnergy(Env *) const { return audio_.strength; }
+
+    int32_t lastStatus() const { return status_; }
+    const sdrg_config &config() const { return cfg_; }
+
+private:
+    struct Cb {
+        Obj obj{};
+        Mid mid{};
+    };
+    bool has(int i) const { return cb_[i].obj && cb_[i].mid; }
+    void dropCallbacks(Env *env) {
+        for (auto &c : cb_) {
+            if (c.obj) J::DeleteGlobalRef(env, c.obj);
+            c = Cb{};
+        }
+    }
+    template <class F>
+    void reconfigure(F &&change) {
+        change();
+        if (eng_) status_ = sdrg_engine_apply_config(eng_, &cfg_);
+    }
+
+    sdrg_engine *eng_ = nullptr;
+    sdrg_config cfg_{};
+    Cb cb_[N_CALLBACKS];
+    bool reading_ = false;
+    int32_t status_ = SDRG_OK;
+    std::vector<float> spec_;
+    std::vector<int16_t> pcm_;
+    sdrg_frame_record rec_{};
+    sdrg_pulse_output spectral_{}, audio_{};
+};
+
+}  // namespace jni
+}  // namespace sdrg

@@ -1,0 +1,164 @@
+// jni_bridge_test.cpp — drives sdrg::jni::Bridge (sdr-for-android-lib_amd/jni/sdrg_jni_bridge.hpp) through a
+// recording fake of the JNI calls it makes, the way Kotlin's SDRBridge and the reference's rx threads drive
+// the JNI exports (applyConfig, read(12 callbacks), frames, setters, stopReading, close), and checks every
+// callback's arguments against a second engine driven directly through the C ABI on the same frames:
+// the order is soapyCallback's (sdr-bridge-java-soapy.cpp:458-488) then the SSB worker's
+// (ssb_processor.cpp:105-113), and every value is bit-identical.  Prints "OK ..." and exits 0 on success.
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sdrg_jni_bridge.hpp"
+
+namespace {
+
+struct FakeObj {
+    int id;
+};
+struct Call {
+    int cb;
+    std::string sig;
+    std::vector<double> args;   // scalars (float/int/long) as doubles, exactly representable here
+    std::vector<float> floats;  // ([F)V payload
+    std::vector<int16_t> shorts;
+};
+struct FakeEnv {
+    std::vector<Call> log;
+    int global_refs = 0;
+};
+
+struct FakeJni {
+    using Env = FakeEnv;
+    using Obj = FakeObj *;
+    using Mid = const char *;
+    static Obj NewGlobalRef(Env *e, Obj o) { e->global_refs++; return o; }
+    static void DeleteGlobalRef(Env *e, Obj) { e->global_refs--; }
+    static Mid MethodOf(Env *, Obj, const char *sig) { return sig; }
+    static void ClearException(Env *) {}
+    static void push(Env *e, Obj o, Mid m, std::vector<double> a) { e->log.push_back({o->id, m, std::move(a), {}, {}}); }
+    static void CallF(Env *e, Obj o, Mid m, float a) { push(e, o, m, {a}); }
+    static void CallI(Env *e, Obj o, Mid m, int32_t a) { push(e, o, m, {(double)a}); }
+    static void CallJ(Env *e, Obj o, Mid m, int64_t a) { push(e, o, m, {(double)a}); }
+    static void CallFF(Env *e, Obj o, Mid m, float a, float b) { push(e, o, m, {a, b}); }
+    static void CallFI(Env *e, Obj o, Mid m, float a, int32_t b) { push(e, o, m, {a, (double)b}); }
+    static void CallFIJ(Env *e, Obj o, Mid m, float a, int32_t b, int64_t c) { push(e, o, m, {a, (double)b, (double)c}); }
+    static void CallFloats(Env *e, Obj o, Mid m, const float *p, int32_t n) {
+        e->log.push_back({o->id, m, {}, std::vector<float>(p, p + n), {}});
+    }
+    static void CallShorts(Env *e, Obj o, Mid m, const int16_t *p, int32_t n) {
+        e->log.push_back({o->id, m, {}, {}, std::vector<int16_t>(p, p + n)});
+    }
+};
+
+using B = sdrg::jni::Bridge<FakeJni>;
+
+int fails = 0;
+#define CHECK(c, ...)                                  \
+    do {                                               \
+        if (!(c)) {                                    \
+            std::fprintf(stderr, "FAIL %s: ", #c);     \
+            std::fprintf(stderr, __VA_ARGS__);         \
+            std::fprintf(stderr, "\n");                \
+            if (++fails > 20) return 1;                \
+        }                                              \
+    } while (0)
+
+bool same_f(double got, float want) { return (float)got == want || (std::isnan(got) && std::isnan(want)); }
+
+}  // namespace
+
+int main() {
+    const int n = 4096, frames = 180;
+    const int64_t fs = 2000000, cf = 100000000;
+    FakeEnv env;
+    B bridge;
+    if (!bridge.applyConfig(&env, cf, fs, n, 5, 10, 50, 200, 30, 1)) {
+        std::fprintf(stderr, "applyConfig failed: %s\n", sdrg_last_error());
+        return 2;
+    }
+    FakeObj objs[B::N_CALLBACKS];
+    B::Obj cbs[B::N_CALLBACKS];
+    for (int i = 0; i < B::N_CALLBACKS; i++) {
+        objs[i].id = i;
+        cbs[i] = &objs[i];
+    }
+    bridge.read(&env, cbs);
+    CHECK(env.global_refs == B::N_CALLBACKS, "global refs %d", env.global_refs);
+
+    // the same stream through the C ABI
+    sdrg_config c{cf, fs, n, 5, 10, 1, 50, 200, 30};
+    sdrg_engine *ref = nullptr;
+    if (sdrg_engine_create(&c, 1, 0, &ref)) return 3;
+    std::vector<float> spec(n);
+    std::vector<int16_t> pcm((size_t)sdrg_engine_pcm_len(ref));
+    sdrg_frame_record rec;
+    sdrg_pulse_output sp, ap;
+
+    std::vector<std::complex<float>> buf(n);
+    uint64_t x = 12345;
+    for (int f = 0; f < frames; f++) {
+        if (f == 60) {  // setFrequency mid-stream, on both
+            bridge.setFrequency(&env, cf + 1000);
+            sdrg_engine_set_frequency(ref, cf + 1000);
+        }
+        if (f == 120) {
+            bridge.setSoundMode(&env, 2);
+            sdrg_engine_set_sound_mode(ref, 2);
+        }
+        for (int i = 0; i < n; i++) {  // keyed +2 kHz carrier over pseudo-random noise
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            const double t = (double)(f * n + i) / fs;
+            const double a = (std::fmod(t, 0.45) < 0.08) ? 0.3 : 0.02;
+            const double ph = 2 * M_PI * 2000.0 * t;
+            buf[i] = {(float)(a * std::cos(ph) + ((double)(x & 0xffff) / 65536.0 - 0.5) * 0.05),
+                      (float)(a * std::sin(ph) + ((double)((x >> 16) & 0xffff) / 65536.0 - 0.5) * 0.05)};
+        }
+        env.log.clear();
+        const int64_t now = 1000 + 2 * f;
+        bridge.onFrame(&env, buf.data(), n, now);
+        CHECK(bridge.lastStatus() == 0, "frame %d status %d", f, bridge.lastStatus());
+        if (sdrg_engine_process_host(ref, buf.data(), SDRG_IQ_CF32, SDRG_STAGE_ALL, spec.data(), &rec, pcm.data(), now))
+            return 4;
+        if (sdrg_engine_get_pulse_outputs(ref, &sp, &ap)) return 5;
+        // expected sequence
+        const int order[] = {B::FFT, B::DETECTION_FLAG, B::MEAN_SNR, B::MEAN_SNR_SIGMA, B::PEAK_FREQUENCY,
+                             B::PEAK_ABOVE_NOISE_MEAN, B::MAX_BIN, B::BEST_1KHZ, B::NOISE_LEVEL, B::SPECTRAL_PULSE,
+                             B::PCM, B::AUDIO_PULSE};
+        CHECK(env.log.size() == 12, "frame %d: %zu calls", f, env.log.size());
+        if (env.log.size() != 12) continue;
+        for (int k = 0; k < 12; k++) {
+            const Call &cl = env.log[k];
+            CHECK(cl.cb == order[k], "frame %d call %d is callback %d", f, k, cl.cb);
+            CHECK(cl.sig == B::kSignature[cl.cb], "signature %s", cl.sig.c_str());
+        }
+        CHECK(env.log[0].floats.size() == (size_t)n && std::memcmp(env.log[0].floats.data(), spec.data(), 4 * n) == 0,
+              "fft payload frame %d", f);
+        CHECK(env.log[1].args[0] == rec.detection_flag, "detection");
+        CHECK(same_f(env.log[2].args[0], rec.mean_snr_db), "meanSnr");
+        CHECK(same_f(env.log[3].args[0], rec.mean_snr_sigma), "meanSnrSigma");
+        CHECK(env.log[4].args[0] == (double)rec.tracking_frequency, "peakFrequency");
+        CHECK(same_f(env.log[5].args[0], rec.peak_above_noise_mean_db), "peakAboveNoiseMean");
+        CHECK(same_f(env.log[6].args[0], rec.max_bin_snr_db) && same_f(env.log[6].args[1], rec.max_bin_snr_sigma), "maxBin");
+        CHECK(same_f(env.log[7].args[0], rec.best1khz_snr_db) && same_f(env.log[7].args[1], rec.best1khz_snr_sigma), "best1kHz");
+        CHECK(same_f(env.log[8].args[0], rec.per_bin_mean), "noiseLevel");
+        CHECK(same_f(env.log[9].args[0], rec.best1khz_snr_sigma) && env.log[9].args[1] == sp.live_etat &&
+                  env.log[9].args[2] == (double)sp.est_freq_hz_rounded, "spectralPulse frame %d", f);
+        CHECK(env.log[10].shorts == pcm, "pcm frame %d", f);
+        CHECK(same_f(env.log[11].args[0], ap.strength) && env.log[11].args[1] == ap.live_etat, "audioPulse");
+    }
+    CHECK(bridge.getAmbientAudioEnergy(&env) == ap.strength, "ambient energy");
+    bridge.stopReading(&env);
+    env.log.clear();
+    bridge.onFrame(&env, buf.data(), n, 5000);
+    CHECK(env.log.empty(), "callbacks after stopReading");
+    bridge.close(&env);
+    CHECK(env.global_refs == 0, "global refs after close %d", env.global_refs);
+    sdrg_engine_destroy(ref);
+    if (fails) return 1;
+    std::printf("OK %d frames, %d callbacks each, spectral live %d, audio live %d\n", frames, 12, sp.live_etat,
+                ap.live_etat);
+    return 0;
+}

@@ -90,3 +90,13 @@ def test_invalid_configs_rejected_before_device():
     with pytest.raises(sdrg.SdrgError) as ei:
         sdrg.Engine(sdrg.SDRConfig(samplesPerReading=0), 1)
     assert "UNSUPPORTED" in str(ei.value)
+
+
+def test_jni_bridge_and_dropins_compile(tmp_path):
+    """The JNI glue template (with the test's JNI fake) and the C++ drop-in programs compile against the
+    public headers (no GPU needed to build; the GPU tests run them)."""
+    inc = os.path.join(ROOT, "include")
+    jni = os.path.join(ROOT, "sdr-for-android-lib_amd", "jni")
+    for src in ("jni_bridge_test.cpp", "compat_main.cpp", "compat_pulse.cpp"):
+        subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", f"-I{inc}", f"-I{jni}",
+                        os.path.join(ROOT, "tests", "cpp", src)], check=True)

@@ -42,3 +42,34 @@ def test_cpp_dropins_match_oracle(tmp_path):
         for i, k in enumerate(fields):
             assert abs(rec[i] - float(want[k])) <= 2e-4 + 2e-5 * abs(float(want[k])), (f, k, rec[i], want[k])
         np.testing.assert_array_equal(pcm, sst.process(iqs[f], fs, mode))
+
+
+def test_cpp_pulse_dropins_match_reference_fixtures(tmp_path):
+    """SpectralPulseDetector / AudioPulseDetector drop-ins, written like the bridge uses them, against the
+    reference fixtures (bit-exact getters)."""
+    import pulse_inputs as PI
+    from conftest import load_golden
+    exe = tmp_path / "compat_pulse"
+    inc = os.path.join(ROOT, "include")
+    libdir = os.path.join(ROOT, "sdr-for-android-lib_amd", "lib")
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-I{inc}", os.path.join(ROOT, "tests", "cpp", "compat_pulse.cpp"),
+                    "-o", str(exe), f"-L{libdir}", "-lsdrg", f"-Wl,-rpath,{libdir}"], check=True)
+    dt = np.dtype([("strength", "<f4"), ("live_etat", "<i4"), ("level", "<i4"), ("locked", "<i4"),
+                   ("period_s", "<f4"), ("est_freq_hz", "<f4")])
+    g = load_golden("pulse_spectral")
+    name, fs, n, kw, _ = PI.SPECTRAL_CASES[0]
+    x, f = PI.spectral_case(n=n, fs_energy=fs, **kw)
+    (tmp_path / "s.bin").write_bytes(np.stack([x, f], axis=1).astype(np.float32).tobytes())
+    subprocess.run([str(exe), "spectral", repr(fs), str(tmp_path / "s.bin"), str(tmp_path / "so.bin")], check=True)
+    got = np.frombuffer((tmp_path / "so.bin").read_bytes(), dt)
+    for k in dt.names:
+        a, b = np.ascontiguousarray(g[name][k]), np.ascontiguousarray(got[k])
+        assert a.tobytes() == b.tobytes(), k
+    ga = load_golden("pulse_audio")
+    name, n, block, kw = PI.AUDIO_CASES[0]
+    s = PI.audio_case(n=n, **kw)
+    (tmp_path / "a.bin").write_bytes(s.tobytes())
+    subprocess.run([str(exe), "audio", str(block), str(tmp_path / "a.bin"), str(tmp_path / "ao.bin")], check=True)
+    got = np.frombuffer((tmp_path / "ao.bin").read_bytes(), dt)
+    for k in ("strength", "live_etat", "level", "locked", "period_s"):
+        assert np.ascontiguousarray(ga[name][k]).tobytes() == np.ascontiguousarray(got[k]).tobytes(), k
