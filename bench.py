@@ -146,13 +146,18 @@ def main() -> int:
     stages = {"all": sdrg.STAGE_ALL, "hot": sdrg.STAGE_HOT_PATH, "spectrum": sdrg.STAGE_SPECTRUM, "ssb": sdrg.STAGE_SSB,
               "spectrum+stats": sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS}[args.stages]
 
+    gathered = torch.empty((world * streams, rec.shape[1]), dtype=torch.uint8, device=dev) if rank == 0 else None
+    if world > 1:
+        # the engine enqueues on torch's stream, so the RCCL gather is ordered after each step on the GPU
+        # without a host synchronisation, and the next step's kernels follow the gather
+        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
     def step():
         eng.process_device(iq.data_ptr(), sdrg.CS8, stages, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(),
                            now[0])
         now[0] += 8  # 16384 samples @ 2 Msps = 8.192 ms per frame
         if world > 1:
-            eng.synchronize()
-            shard.gather_records(rec, world, rank, dst=0)  # the one collective: records to rank 0 (RCCL)
+            shard.gather_records(rec, world, rank, dst=0, out=gathered)  # the one collective: records to rank 0
 
     eng.set_profiling(True)
     for _ in range(args.warmup):

@@ -321,6 +321,10 @@ int32_t sdrg_engine_process_device(sdrg_engine *eng, const void *iq, int32_t for
                                    float *spectra, sdrg_frame_record *records, int16_t *pcm,
                                    int64_t now_ms);
 int32_t sdrg_engine_synchronize(sdrg_engine *eng);
+/* Enqueue the engine's work on the caller's HIP stream (a hipStream_t; NULL = the engine's own stream): the
+ * SSB fork/join happens relative to it, so consumers on that stream (e.g. an RCCL gather of the records)
+ * are ordered after each call without a host synchronisation.  Synchronises the previous stream first. */
+int32_t sdrg_engine_set_stream(sdrg_engine *eng, void *hip_stream);
 
 /* Same from host memory (PCIe-inclusive): copies iq in, runs, copies outputs back, synchronises,
  * then invokes the registered callbacks per stream in soapyCallback order.  Any output may be NULL. */

@@ -76,6 +76,7 @@ struct sdrg_engine {
     int n_streams = 0;
     int device = 0;
     hipStream_t s_main = nullptr, s_ssb = nullptr;
+    hipStream_t s_own = nullptr;  // the engine's own main stream (s_main is it, or the caller's via set_stream)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // profiling: a ring of event sets so consecutive calls are timed without host synchronisation
     static constexpr int RING = 64;
@@ -523,9 +524,10 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         sdrg_engine_destroy(e);
         return code;
     };
-    if (hipStreamCreateWithFlags(&e->s_main, hipStreamNonBlocking) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&e->s_own, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&e->s_ssb, hipStreamNonBlocking) != hipSuccess)
         return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
+    e->s_main = e->s_own;
     hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join};
     for (auto p : evs)
         if (hipEventCreateWithFlags(p, hipEventDisableTiming) != hipSuccess)
@@ -555,7 +557,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     }
     if (e->spec_bank_live) pulse_bank_release(&e->spec_bank);
     if (e->audio_bank_live) pulse_bank_release(&e->audio_bank);
-    if (e->s_main) (void)hipStreamDestroy(e->s_main);
+    if (e->s_own) (void)hipStreamDestroy(e->s_own);
     if (e->s_ssb) (void)hipStreamDestroy(e->s_ssb);
     delete e;
     return SDRG_OK;
@@ -621,6 +623,14 @@ int32_t sdrg_engine_reset_state(sdrg_engine *e) {
     e->cf_changed_pending = false;
     e->spec_bank.reset_pending = true;
     e->audio_bank.reset_pending = true;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_stream(sdrg_engine *e, void *hip_stream) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->s_main));  // work already enqueued stays ordered before the switch
+    e->s_main = hip_stream ? static_cast<hipStream_t>(hip_stream) : e->s_own;
     return SDRG_OK;
 }
 

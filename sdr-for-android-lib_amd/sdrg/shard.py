@@ -15,17 +15,25 @@ def stream_range(rank: int, world: int, streams_per_rank: int) -> tuple[int, int
     return rank * streams_per_rank, (rank + 1) * streams_per_rank
 
 
-def gather_records(records, world: int, rank: int, dst: int = 0, group=None):
+def gather_records(records, world: int, rank: int, dst: int = 0, group=None, out=None):
     """Gather each rank's [B, record_bytes] uint8 record tensor to `dst`.
 
     Returns the [world*B, record_bytes] concatenation (global stream order) on `dst`, None elsewhere.  The
     tensor must live where the process group's backend expects it (HIP memory for nccl/RCCL, host for gloo).
+    `out` (on dst): a preallocated [world*B, record_bytes] tensor to gather into (no per-step allocation);
+    with RCCL the gather is ordered on the current stream, so no host synchronisation is needed.
     """
     import torch
     import torch.distributed as dist
 
     if world == 1:
         return records
-    bufs = [torch.empty_like(records) for _ in range(world)] if rank == dst else None
+    if rank == dst:
+        if out is None:
+            out = torch.empty((world * records.shape[0],) + tuple(records.shape[1:]), dtype=records.dtype,
+                              device=records.device)
+        bufs = list(out.chunk(world, dim=0))
+    else:
+        bufs = None
     dist.gather(records, bufs, dst=dst, group=group)
-    return torch.cat(bufs, dim=0) if rank == dst else None
+    return out if rank == dst else None

@@ -262,14 +262,17 @@ def test_full_size_batch_properties(S, O):
     for b in rng.choice(B, 12, replace=False):
         iq = O.unpack(O.CS8, raw[b], n)
         np.testing.assert_array_equal(pcm[b], O.SsbState().process(iq, fs, 1), err_msg=f"stream {b}")
-    # determinism: a second engine reproduces every bit
+    # determinism: a second engine, enqueued on torch's stream (sdrg_engine_set_stream), reproduces every bit
     eng2 = engine(S, n, fs, B)
+    eng2.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     d_spec2 = torch.empty_like(d_spec)
     d_pcm2 = torch.empty_like(d_pcm)
-    eng2.process_device(d_iq.data_ptr(), O.CS8, S.STAGE_ALL, d_spec2.data_ptr(), d_rec.data_ptr(),
+    d_rec2 = torch.zeros_like(d_rec)
+    eng2.process_device(d_iq.data_ptr(), O.CS8, S.STAGE_ALL, d_spec2.data_ptr(), d_rec2.data_ptr(),
                         d_pcm2.data_ptr(), 1000)
-    eng2.synchronize()
-    assert torch.equal(d_spec, d_spec2) and torch.equal(d_pcm, d_pcm2)
+    same = torch.equal(d_spec, d_spec2) and torch.equal(d_pcm, d_pcm2)  # ordered on torch's stream, no sync
+    assert same
+    eng2.set_stream(None)
     eng.close()
     eng2.close()
 

@@ -41,9 +41,12 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     first, last = shard.stream_range(rank, world, B)
     got = []
-    for recs in _records(O, first, last):
+    out = None
+    for k, recs in enumerate(_records(O, first, last)):
         t = torch.from_numpy(recs.view(np.uint8).reshape(B, -1).copy())
-        g = shard.gather_records(t, world, rank)
+        if rank == 0 and k > 0 and out is None:  # later steps gather into a preallocated buffer (bench.py)
+            out = torch.empty((world * B, t.shape[1]), dtype=torch.uint8)
+        g = shard.gather_records(t, world, rank, out=out)
         if rank == 0:
             got.append(g.numpy().copy())
     dist.barrier()
