@@ -148,9 +148,12 @@ def main() -> int:
 
     gathered = torch.empty((world * streams, rec.shape[1]), dtype=torch.uint8, device=dev) if rank == 0 else None
     if world > 1:
-        # the engine enqueues on torch's stream, so the RCCL gather is ordered after each step on the GPU
-        # without a host synchronisation, and the next step's kernels follow the gather
-        eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        # the engine enqueues on a torch stream that is current for the collectives too, so the RCCL gather is
+        # ordered after each step on the GPU without a host synchronisation, and the next step's kernels
+        # follow the gather (a real stream: the legacy default stream has no handle to pass)
+        work_stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(work_stream)
+        eng.set_stream(work_stream.cuda_stream)
 
     def step():
         eng.process_device(iq.data_ptr(), sdrg.CS8, stages, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(),

@@ -264,13 +264,16 @@ def test_full_size_batch_properties(S, O):
         np.testing.assert_array_equal(pcm[b], O.SsbState().process(iq, fs, 1), err_msg=f"stream {b}")
     # determinism: a second engine, enqueued on torch's stream (sdrg_engine_set_stream), reproduces every bit
     eng2 = engine(S, n, fs, B)
-    eng2.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    side = torch.cuda.Stream(dev)
+    eng2.set_stream(side.cuda_stream)
     d_spec2 = torch.empty_like(d_spec)
     d_pcm2 = torch.empty_like(d_pcm)
     d_rec2 = torch.zeros_like(d_rec)
-    eng2.process_device(d_iq.data_ptr(), O.CS8, S.STAGE_ALL, d_spec2.data_ptr(), d_rec2.data_ptr(),
-                        d_pcm2.data_ptr(), 1000)
-    same = torch.equal(d_spec, d_spec2) and torch.equal(d_pcm, d_pcm2)  # ordered on torch's stream, no sync
+    side.wait_stream(torch.cuda.current_stream(dev))  # the allocations above
+    with torch.cuda.stream(side):
+        eng2.process_device(d_iq.data_ptr(), O.CS8, S.STAGE_ALL, d_spec2.data_ptr(), d_rec2.data_ptr(),
+                            d_pcm2.data_ptr(), 1000)
+        same = torch.equal(d_spec, d_spec2) and torch.equal(d_pcm, d_pcm2)  # ordered on `side`, no host sync
     assert same
     eng2.set_stream(None)
     eng.close()
