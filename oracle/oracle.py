@@ -332,24 +332,44 @@ class PulseDetector:
 REF_PULSE = os.path.join(HERE, "_ref", "ref_pulse")
 
 
-def ref_pulse_spectral(snr_sigma: np.ndarray, freq_hz: np.ndarray, fs_energy: float, reconf=None) -> np.ndarray:
-    """The reference's own SpectralPulseDetector (oracle/_ref/ref_pulse, container only)."""
+# reference Config field name -> sdrg_pulse_config field name
+PULSE_CFG_NAMES = {"fsEnergy": "fs_energy", "zDefaultS": "z_default_s", "tTargetInit": "t_target_init",
+                   "dtTolS": "dt_tol_s", "snrMin": "snr_min", "snrRhythm": "snr_rhythm", "snrStrong": "snr_strong",
+                   "dispersionMax": "dispersion_max", "sumNMax": "sum_n_max", "liveWindowT": "live_window_t",
+                   "liveDivisor": "live_divisor", "sampleRate": "sample_rate", "fMin": "f_min", "fMax": "f_max",
+                   "smoothCutoff": "smooth_cutoff", "noiseRefFar": "noise_ref_far", "noiseRefNear": "noise_ref_near"}
+
+
+def pulse_overrides(ref_names: dict) -> dict:
+    """Reference Config overrides -> sdrg_pulse_config field overrides."""
+    return {PULSE_CFG_NAMES[k]: v for k, v in ref_names.items()}
+
+
+def _kv(overrides: dict | None):
+    return [f"{k}={repr(float(np.float32(v))) if isinstance(v, float) else v}" for k, v in (overrides or {}).items()]
+
+
+def ref_pulse_spectral(snr_sigma: np.ndarray, freq_hz: np.ndarray, fs_energy: float, reconf=None,
+                       overrides: dict | None = None) -> np.ndarray:
+    """The reference's own SpectralPulseDetector (oracle/_ref/ref_pulse, container only); overrides use the
+    reference Config field names."""
     inp = np.stack([np.asarray(snr_sigma, np.float32), np.asarray(freq_hz, np.float32)], axis=1)
     args = [REF_PULSE, "spectral", repr(float(np.float32(fs_energy)))]
     if reconf is not None:
         args += [str(int(reconf[0])), repr(float(np.float32(reconf[1])))]
+    args += _kv(overrides)
     out = subprocess.run(args, input=inp.tobytes(), capture_output=True, check=True).stdout
     return np.frombuffer(out, PULSE_OUTPUT_DTYPE).copy()
 
 
-def ref_pulse_audio(samples: np.ndarray, block: int) -> np.ndarray:
+def ref_pulse_audio(samples: np.ndarray, block: int, overrides: dict | None = None) -> np.ndarray:
     """The reference's own AudioPulseDetector over int16 / float32 samples in blocks (container only)."""
     a = np.ascontiguousarray(samples)
     fmt = 0 if a.dtype == np.int16 else 1
     if fmt:
         a = a.astype(np.float32)
-    out = subprocess.run([REF_PULSE, "audio", str(fmt), str(block)], input=a.tobytes(), capture_output=True,
-                         check=True).stdout
+    out = subprocess.run([REF_PULSE, "audio", str(fmt), str(block)] + _kv(overrides), input=a.tobytes(),
+                         capture_output=True, check=True).stdout
     return np.frombuffer(out, PULSE_OUTPUT_DTYPE).copy()
 
 

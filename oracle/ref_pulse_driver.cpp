@@ -10,11 +10,15 @@
 //       stdin: float32 pairs (snrSigma, freqHz), one per frame.  Builds SpectralPulseDetector with the default
 //       Config but fsEnergy = <fs_energy> (what applyConfig does, sdr-bridge-java-soapy.cpp:1130-1138); before
 //       frame <k> calls configure() with fsEnergy = <fs_energy2>.  stdout: one sdrg_pulse_output per frame.
-//   ref_pulse audio <fmt> <block>
+//   ref_pulse audio <fmt> <block> [key=value ...]
 //       stdin: int16 (fmt 0) or float32 (fmt 1) samples; AudioPulseDetector with the default Config (what
 //       SSBProcessor uses, setPulseConfig being a no-op in the bridge) processes them in blocks of <block>
 //       samples (the last block may be shorter).  stdout: one sdrg_pulse_output per block.
+//   Both kinds take optional Config overrides as key=value (the reference Config field names), e.g.
+//   snrStrong=3.5 liveDivisor=2 (spectral: after fs_energy / the reconfigure pair).
 #include <cmath>
+#include <string>
+#include <type_traits>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -27,6 +31,26 @@
 
 static void emit(const sdrg_pulse_output &o) { std::fwrite(&o, sizeof(o), 1, stdout); }
 
+// key=value Config overrides (field names of the reference Config structs)
+template <class C>
+static bool set_field(C &c, const char *kv) {
+    const char *eq = std::strchr(kv, '=');
+    if (!eq) return false;
+    const std::string k(kv, eq - kv);
+    const float v = std::strtof(eq + 1, nullptr);
+    const int iv = std::atoi(eq + 1);
+#define F(name) if (k == #name) { c.name = v; return true; }
+#define I(name) if (k == #name) { c.name = iv; return true; }
+    F(fsEnergy) F(zDefaultS) F(tTargetInit) F(dtTolS) F(snrMin) F(snrRhythm) F(snrStrong) F(dispersionMax)
+    I(sumNMax) F(liveWindowT) F(liveDivisor)
+    if constexpr (std::is_same_v<C, AudioPulseDetector::Config>) {
+        F(sampleRate) F(fMin) F(fMax) F(smoothCutoff) I(noiseRefFar) I(noiseRefNear)
+    }
+#undef F
+#undef I
+    return false;
+}
+
 int main(int argc, char **argv) {
     if (argc < 3) {
         std::fprintf(stderr, "usage: ref_pulse spectral <fs> [<k> <fs2>] | audio <fmt> <block>\n");
@@ -35,14 +59,21 @@ int main(int argc, char **argv) {
     if (!std::strcmp(argv[1], "spectral")) {
         SpectralPulseDetector::Config cfg;
         cfg.fsEnergy = std::strtof(argv[2], nullptr);
-        SpectralPulseDetector det;
-        det.configure(cfg);
-        const long k_re = argc > 4 ? std::strtol(argv[3], nullptr, 10) : -1;
-        const float fs2 = argc > 4 ? std::strtof(argv[4], nullptr) : 0.f;
+        int a = 3;
+        long k_re = -1;
+        float fs2 = 0.f;
+        if (argc > 4 && !std::strchr(argv[3], '=')) {
+            k_re = std::strtol(argv[3], nullptr, 10);
+            fs2 = std::strtof(argv[4], nullptr);
+            a = 5;
+        }
+        for (; a < argc; a++)
+            if (!set_field(cfg, argv[a])) { std::fprintf(stderr, "bad override %s\n", argv[a]); return 2; }
+        SpectralPulseDetector det(cfg);
         float in[2];
         for (long k = 0; std::fread(in, sizeof(float), 2, stdin) == 2; k++) {
             if (k == k_re) {
-                SpectralPulseDetector::Config c2;
+                SpectralPulseDetector::Config c2 = cfg;
                 c2.fsEnergy = fs2;
                 det.configure(c2);
             }
@@ -64,7 +95,10 @@ int main(int argc, char **argv) {
     if (!std::strcmp(argv[1], "audio") && argc >= 4) {
         const int fmt = std::atoi(argv[2]);
         const size_t block = (size_t)std::atol(argv[3]);
-        AudioPulseDetector det;
+        AudioPulseDetector::Config cfg;
+        for (int a = 4; a < argc; a++)
+            if (!set_field(cfg, argv[a])) { std::fprintf(stderr, "bad override %s\n", argv[a]); return 2; }
+        AudioPulseDetector det(cfg);
         const size_t es = fmt == 0 ? 2 : 4;
         std::vector<char> buf(block * es);
         for (;;) {

@@ -30,11 +30,19 @@ def main() -> None:
         x, f = PI.spectral_case(n=n, fs_energy=fs, **kw)
         spec[name] = O.ref_pulse_spectral(x, f, fs, reconf)
         spec[name + "__digest"] = np.array(PI.digest(x, f))
+    for name, fs, n, kw, ov in PI.SPECTRAL_CUSTOM_CASES:
+        x, f = PI.spectral_case(n=n, fs_energy=fs, **kw)
+        spec[name] = O.ref_pulse_spectral(x, f, fs, None, ov)
+        spec[name + "__digest"] = np.array(PI.digest(x, f))
     np.savez_compressed(os.path.join(HERE, "pulse_spectral.npz"), **spec)
     aud = {}
     for name, n, block, kw in PI.AUDIO_CASES:
         s = PI.audio_case(n=n, **kw)
         aud[name] = O.ref_pulse_audio(s, block)
+        aud[name + "__digest"] = np.array(PI.digest(s))
+    for name, n, block, kw, ov in PI.AUDIO_CUSTOM_CASES:
+        s = PI.audio_case(n=n, **kw)
+        aud[name] = O.ref_pulse_audio(s, block, ov)
         aud[name + "__digest"] = np.array(PI.digest(s))
     np.savez_compressed(os.path.join(HERE, "pulse_audio.npz"), **aud)
     print("wrote pulse_spectral.npz, pulse_audio.npz")

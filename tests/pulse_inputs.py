@@ -114,3 +114,20 @@ AUDIO_CASES = [
     ("hum_noise_1000", 48000 * 24, 1000, dict(seed=13, amp=0, hum=4000)),
     ("fast_100", 48000 * 12, 100, dict(seed=14, period=0.7, burst=0.08, hum=2500)),
 ]
+
+# Non-default configurations (reference Config field names), pinned against the reference build too.
+SPECTRAL_CUSTOM_CASES = [
+    # name, fs_energy, n_frames, input kwargs, Config overrides
+    ("custom_thresholds", float(FS16K), 2600, dict(seed=31, amp=3.2, jitter=0.08),
+     {"snrMin": 1.2, "snrRhythm": 2.0, "snrStrong": 3.0, "liveDivisor": 2.0, "liveWindowT": 3.0}),
+    ("custom_period", 40.0, 1200, dict(seed=32, period=2.6, width=0.25),
+     {"tTargetInit": 2.5, "dtTolS": 0.25, "zDefaultS": 1.0, "sumNMax": 5, "dispersionMax": 0.9}),
+]
+AUDIO_CUSTOM_CASES = [
+    # name, n_samples, block, input kwargs, Config overrides
+    ("custom_band_noise_ref", 48000 * 16, 394, dict(seed=41, amp=2500, noise=600.0),
+     {"fMin": 1200.0, "fMax": 3000.0, "noiseRefFar": 60, "noiseRefNear": 25, "snrStrong": 1.8, "snrMin": 1.05}),
+    ("custom_rates", 32000 * 16, 512, dict(seed=42, rate=32000.0, period=1.4),
+     {"sampleRate": 32000.0, "fsEnergy": 50.0, "smoothCutoff": 4.0, "tTargetInit": 1.4, "liveDivisor": 2.5}),
+]
+

@@ -192,3 +192,29 @@ def test_engine_pulse_stage_dependencies(S):
     eng.process(iq, fmt=S.CS8, stages=S.STAGE_ALL)
     sp, au = eng.pulse_outputs()
     assert (sp["live_etat"] == 0).all() and (au["live_etat"] == 0).all() and (sp["n_energy"] == 1).all()
+
+
+@pytest.mark.parametrize("case", PI.SPECTRAL_CUSTOM_CASES, ids=[c[0] for c in PI.SPECTRAL_CUSTOM_CASES])
+def test_spectral_bank_custom_config_vs_reference(S, O, case):
+    name, fs, n, kw, ov = case
+    g = load_golden("pulse_spectral")
+    x, f = PI.spectral_case(n=n, fs_energy=fs, **kw)
+    B = 70  # not a multiple of 64
+    bank = S.PulseBank(S.PULSE_SPECTRAL, B, S.PulseConfig.default(S.PULSE_SPECTRAL, fs_energy=fs,
+                                                                  **O.pulse_overrides(ov)))
+    outs = np.stack([bank.process_spectral(np.full(B, x[t]), np.full(B, f[t])) for t in range(n)])
+    for s in (0, 63, 64, B - 1):
+        _same(g[name], outs[:, s], O.PULSE_REF_FIELDS, f"{name} stream {s}")
+
+
+@pytest.mark.parametrize("case", PI.AUDIO_CUSTOM_CASES, ids=[c[0] for c in PI.AUDIO_CUSTOM_CASES])
+def test_audio_bank_custom_config_vs_reference(S, O, case):
+    """Custom band / noise reference / rates, 67 streams (the front-end kernel's last wave partly empty)."""
+    name, n, block, kw, ov = case
+    g = load_golden("pulse_audio")
+    s = PI.audio_case(n=n, **kw)
+    B = 67
+    bank = S.PulseBank(S.PULSE_AUDIO, B, S.PulseConfig.default(S.PULSE_AUDIO, **O.pulse_overrides(ov)))
+    outs = np.stack([bank.process_audio(np.repeat(s[None, k:k + block], B, axis=0)) for k in range(0, n, block)])
+    for st in (0, 63, 64, B - 1):
+        _same(g[name], outs[:, st], ("strength", "live_etat", "level", "locked", "period_s", "input"), f"{name} {st}")

@@ -97,3 +97,25 @@ def test_oracle_matches_reference_live(oracle_mod, seed):
     block = int(rng.choice([97, 394, 480, 1256]))
     _same(O.ref_pulse_audio(s, block), O.PulseDetector(O.PULSE_AUDIO).audio_blocks(s, block),
           ("strength", "live_etat", "level", "locked", "period_s"))
+
+
+@pytest.mark.parametrize("case", PI.SPECTRAL_CUSTOM_CASES, ids=[c[0] for c in PI.SPECTRAL_CUSTOM_CASES])
+def test_spectral_oracle_custom_config_matches_reference(oracle_mod, case):
+    O = oracle_mod
+    name, fs, n, kw, ov = case
+    g = load_golden("pulse_spectral")
+    x, f = PI.spectral_case(n=n, fs_energy=fs, **kw)
+    assert PI.digest(x, f) == str(g[name + "__digest"])
+    d = O.PulseDetector(O.PULSE_SPECTRAL, fs_energy=fs, **O.pulse_overrides(ov))
+    _same(g[name], d.spectral(x, f), O.PULSE_REF_FIELDS)
+
+
+@pytest.mark.parametrize("case", PI.AUDIO_CUSTOM_CASES, ids=[c[0] for c in PI.AUDIO_CUSTOM_CASES])
+def test_audio_oracle_custom_config_matches_reference(oracle_mod, case):
+    O = oracle_mod
+    name, n, block, kw, ov = case
+    g = load_golden("pulse_audio")
+    s = PI.audio_case(n=n, **kw)
+    assert PI.digest(s) == str(g[name + "__digest"])
+    got = O.PulseDetector(O.PULSE_AUDIO, **O.pulse_overrides(ov)).audio_blocks(s, block)
+    _same(g[name], got, ("strength", "live_etat", "level", "locked", "period_s", "input"))
