@@ -325,6 +325,12 @@ int32_t sdrg_engine_synchronize(sdrg_engine *eng);
  * SSB fork/join happens relative to it, so consumers on that stream (e.g. an RCCL gather of the records)
  * are ordered after each call without a host synchronisation.  Synchronises the previous stream first. */
 int32_t sdrg_engine_set_stream(sdrg_engine *eng, void *hip_stream);
+/* Pipelining across calls (default off).  When on, sdrg_engine_process_device forks the SSB stages at the
+ * start of each call and does not join them into the main stream at its end, so a call's SSB pipeline runs
+ * beside the next call's spectrum.  The spectrum / statistics / spectral-pulse outputs are ordered on the
+ * main stream as usual; the PCM and audio-pulse outputs are complete after sdrg_engine_synchronize (or
+ * after the next call's SSB stage starts, which follows them on the SSB stream).  process_host always joins. */
+int32_t sdrg_engine_set_pipelining(sdrg_engine *eng, int32_t on);
 
 /* Same from host memory (PCIe-inclusive): copies iq in, runs, copies outputs back, synchronises,
  * then invokes the registered callbacks per stream in soapyCallback order.  Any output may be NULL. */

@@ -122,6 +122,7 @@ struct sdrg_engine {
     bool spec_bank_live = false, audio_bank_live = false;
     std::vector<sdrg_pulse_output> h_pspec, h_paudio;
     bool cf_changed_pending = false;
+    bool pipelined = false;  // sdrg_engine_set_pipelining: no join of the SSB stream per call
     int upper = 1;
     bool has_cbs = false;
     sdrg_callbacks cbs{};
@@ -311,7 +312,7 @@ int32_t bytes_per_sample(int fmt) {
 }
 
 int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, float *spectra,
-                sdrg_frame_record *records, int16_t *pcm, int64_t now_ms) {
+                sdrg_frame_record *records, int16_t *pcm, int64_t now_ms, bool join) {
     const int n = e->cfg.samples_per_reading;
     const int B = e->n_streams;
     if (!iq) return fail(SDRG_E_INVALID, "null iq");
@@ -394,13 +395,23 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     // workgroups per CU); the SSB pipeline (latency-bound, one workgroup per CU) then runs beside the
     // statistics kernel on a forked stream.  Measured: the same step time as running the spectrum beside
     // the SSB pipeline, with the spectrum kernel's HBM rate not diluted by the SSB workgroups.
+    // Pipelined (sdrg_engine_set_pipelining): the SSB stream forks at the start of the call and is not
+    // joined at its end, so this call's SSB pipeline and the next call's spectrum share the chip as the
+    // other's workgroups retire (steady state measured in tools/overlap_lab.py).
+    const bool early_fork = e->pipelined && !join;
+    if (do_ssb && early_fork) {
+        HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));  // orders the SSB after the caller's producer work
+        HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
+    }
     if (do_spec) {
         HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, e->s_main));
         if (prof) HIP_TRY(hipEventRecord(ev->spec, e->s_main));
     }
     if (do_ssb) {  // fork
-        HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
-        HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
+        if (!early_fork) {
+            HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
+            HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
+        }
         if (prof) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
         // AudioPulseDetector::process(pcm) after processSSB_opt (ssb_processor.cpp:109): its per-sample front
         // end runs inside the SSB kernel on the PCM it produces, the detector right after
@@ -428,7 +439,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         if (prof) HIP_TRY(hipEventRecord(ev->stats, e->s_main));
         e->cf_changed_pending = false;
     }
-    if (do_ssb) HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));  // join
+    if (do_ssb && !early_fork) HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));  // join
     if (prof) {
         HIP_TRY(hipEventRecord(ev->end, e->s_main));
         ev->pending = true;
@@ -626,6 +637,17 @@ int32_t sdrg_engine_reset_state(sdrg_engine *e) {
     return SDRG_OK;
 }
 
+int32_t sdrg_engine_set_pipelining(sdrg_engine *e, int32_t on) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    HIP_TRY(hipSetDevice(e->device));
+    if (e->pipelined && !on) {  // re-join what is in flight so later work on s_main follows it
+        HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
+        HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));
+    }
+    e->pipelined = on != 0;
+    return SDRG_OK;
+}
+
 int32_t sdrg_engine_set_stream(sdrg_engine *e, void *hip_stream) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     HIP_TRY(hipSetDevice(e->device));
@@ -681,12 +703,13 @@ int32_t sdrg_engine_process_device(sdrg_engine *e, const void *iq, int32_t forma
                                    sdrg_frame_record *records, int16_t *pcm, int64_t now_ms) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     HIP_TRY(hipSetDevice(e->device));
-    return enqueue(e, iq, format, stages, spectra, records, pcm, now_ms);
+    return enqueue(e, iq, format, stages, spectra, records, pcm, now_ms, false);
 }
 
 int32_t sdrg_engine_synchronize(sdrg_engine *e) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     HIP_TRY(hipStreamSynchronize(e->s_main));
+    HIP_TRY(hipStreamSynchronize(e->s_ssb));  // not joined into s_main when pipelined
     static const bool stamps = [] {
         const char *v = getenv("SDRG_PIPE_STAMPS");
         return v && v[0] == '1';
@@ -731,7 +754,7 @@ int32_t sdrg_engine_process_host(sdrg_engine *e, const void *iq, int32_t format,
     }
     HIP_TRY(hipMemcpyAsync(e->d_iq_stage, iq, iq_bytes, hipMemcpyHostToDevice, e->s_main));
     int32_t rc = enqueue(e, e->d_iq_stage, format, stages, do_spec ? e->d_spec_stage : nullptr,
-                         do_stats ? e->d_rec_stage : nullptr, do_ssb ? e->d_pcm_stage : nullptr, now_ms);
+                         do_stats ? e->d_rec_stage : nullptr, do_ssb ? e->d_pcm_stage : nullptr, now_ms, true);
     if (rc) return rc;
     float *h_spec = spectra;
     sdrg_frame_record *h_rec = records;

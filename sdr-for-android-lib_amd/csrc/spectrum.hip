@@ -21,6 +21,7 @@
 //   * N = 32768 / 65536 do not fit a CU's LDS and run as a two-kernel four-step FFT.
 // MFMA is not used: there is no dense contraction on this path.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -596,7 +597,12 @@ hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectr
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    const int grid = n_frames < 2 * device_cus() ? n_frames : 2 * device_cus();
+    static const int max_grid = [] {  // lab override (SDRG_SPECTRUM_GRID): persistent workgroups
+        const char *v = getenv("SDRG_SPECTRUM_GRID");
+        const int g = v ? atoi(v) : 0;
+        return g > 0 ? g : 2 * device_cus();
+    }();
+    const int grid = n_frames < max_grid ? n_frames : max_grid;
     hipLaunchKernelGGL(k, dim3(grid), dim3(T), LDS_BYTES, s, iq, spectra, tabs, n_frames);
     return hipGetLastError();
 }

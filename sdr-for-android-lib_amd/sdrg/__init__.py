@@ -80,6 +80,7 @@ EXPORTS = [
     "sdrg_engine_apply_config", "sdrg_engine_set_frequency", "sdrg_engine_set_frequency_focus_range",
     "sdrg_engine_set_sound_mode", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
     "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_set_stream",
+    "sdrg_engine_set_pipelining",
     "sdrg_engine_process_host",
     "sdrg_engine_set_callbacks", "sdrg_engine_set_profiling", "sdrg_engine_get_timings",
     "sdrg_engine_get_timing_stats", "sdrg_engine_reset_timing_stats",
@@ -200,6 +201,7 @@ def load() -> ctypes.CDLL:
         "sdrg_engine_process_device": (_I32, [P, P, _I32, _I32, P, P, P, _I64]),
         "sdrg_engine_synchronize": (_I32, [P]),
         "sdrg_engine_set_stream": (_I32, [P, P]),
+        "sdrg_engine_set_pipelining": (_I32, [P, _I32]),
         "sdrg_engine_process_host": (_I32, [P, P, _I32, _I32, P, P, P, _I64]),
         "sdrg_engine_set_callbacks": (_I32, [P, ctypes.POINTER(_Callbacks)]),
         "sdrg_engine_set_profiling": (_I32, [P, _I32]),
@@ -402,6 +404,10 @@ class Engine:
     def synchronize(self) -> None:
         _check(load().sdrg_engine_synchronize(self._h), "synchronize")
 
+    def set_pipelining(self, on: bool) -> None:
+        """Overlap each call's SSB stages with the next call's spectrum (see include/sdrg.h)."""
+        _check(load().sdrg_engine_set_pipelining(self._h, int(on)), "set_pipelining")
+
     def set_stream(self, hip_stream: int | None) -> None:
         """Enqueue on the caller's HIP stream (e.g. torch.cuda.current_stream().cuda_stream); None = own."""
         _check(load().sdrg_engine_set_stream(self._h, hip_stream), "set_stream")
@@ -459,6 +465,10 @@ class PulseBank:
 
     def reset(self) -> None:
         _check(load().sdrg_pulse_bank_reset(self._h), "pulse_bank_reset")
+
+    def set_pipelining(self, on: bool) -> None:
+        """Overlap each call's SSB stages with the next call's spectrum (see include/sdrg.h)."""
+        _check(load().sdrg_engine_set_pipelining(self._h, int(on)), "set_pipelining")
 
     def set_stream(self, hip_stream: int | None) -> None:
         _check(load().sdrg_pulse_bank_set_stream(self._h, hip_stream), "pulse_bank_set_stream")

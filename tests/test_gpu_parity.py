@@ -312,3 +312,32 @@ def test_ingest_cs12_reads_to_engine(S, O):
             np.testing.assert_array_equal(frames[b] >> 4, (tone[b, f * 2 * n:(f + 1) * 2 * n] >> 4))
     assert ing.pop_batch() is None
     eng.close()
+
+
+def test_pipelined_calls_equal_joined_calls(S, O):
+    """sdrg_engine_set_pipelining: each call's SSB stages overlap the next call's spectrum; after synchronize
+    every output (spectra, records, PCM, both pulse detectors) equals the joined schedule bit for bit."""
+    import torch
+    n, fs, B, F = 16384, 2_000_000, 256, 4
+    dev = torch.device("cuda:0")
+    raws = [torch.from_numpy(np.stack([O.synth_frames(1, n, O.CS8, tone_hz=300.0 * (b % 13) - 1800.0, fs=fs,
+                                                      seed=100 * f + b)[0] for b in range(B)])).to(dev)
+            for f in range(F)]
+    outs = {}
+    for mode in (False, True):
+        eng = engine(S, n, fs, B)
+        eng.set_pipelining(mode)
+        spec = [torch.empty((B, n), dtype=torch.float32, device=dev) for _ in range(F)]
+        rec = [torch.zeros((B, S.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev) for _ in range(F)]
+        pcm = [torch.empty((B, eng.pcm_len), dtype=torch.int16, device=dev) for _ in range(F)]
+        torch.cuda.synchronize()
+        for f in range(F):
+            eng.process_device(raws[f].data_ptr(), O.CS8, S.STAGE_ALL, spec[f].data_ptr(), rec[f].data_ptr(),
+                               pcm[f].data_ptr(), 1000 + 8 * f)
+        eng.synchronize()
+        sp, au = eng.pulse_outputs()
+        outs[mode] = (torch.stack(spec).cpu(), torch.stack(rec).cpu(), torch.stack(pcm).cpu(), sp, au)
+        eng.close()
+    a, b = outs[False], outs[True]
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    assert a[3].tobytes() == b[3].tobytes() and a[4].tobytes() == b[4].tobytes()
