@@ -43,11 +43,25 @@ stats_csv = glob.glob(f"gpurun_out/prof_{TAG}/**/*kernel_stats.csv", recursive=T
 lines = [f"# Round profile {TAG}", ""]
 if stats_csv:
     shutil.copy(stats_csv[0], f"{OUT}/{TAG}_kernel_stats.csv")
-    lines += ["## rocprofv3 --kernel-trace --stats (bench.py --steps 20 --warmup 3, all stages)", "",
+    lines += ["## rocprofv3 --kernel-trace --stats (bench.py --steps 20 --warmup 3 --no-cpu-baseline, defaults)", "",
               "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
     for r in csv.DictReader(open(stats_csv[0])):
         lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                      f"{float(r['MinNs']) / 1e3:.1f} | {float(r['MaxNs']) / 1e3:.1f} | {r['Percentage']} |")
+# per-launch durations of the roofline kernel from the trace: bench.py runs 3 warmup steps, the timed steps,
+# then 10 isolated spectrum-only launches; split them so each can be compared with the bench line's numbers
+trace_csv = glob.glob(f"gpurun_out/prof_{TAG}/**/*kernel_trace.csv", recursive=True)
+if trace_csv:
+    rows = [r for r in csv.DictReader(open(trace_csv[0])) if "spectrum16k_kernel" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+    if len(d) > 13:
+        timed, iso = d[3:-10], d[-10:]
+        lines += ["", "## spectrum16k_kernel launch durations from the kernel trace", "",
+                  f"* timed region ({len(timed)} launches, pipelined with the SSB stages): "
+                  f"avg {sum(timed) / len(timed):.1f} us",
+                  f"* isolated pass after it ({len(iso)} launches, the kernel alone): avg {sum(iso) / len(iso):.1f} us",
+                  "* the bench line's `roofline` / `roofline_isolated` use the same two sets, timed with HIP events"]
 bench = None
 blog = f"gpurun_out/bench_{TAG}.log"
 if os.path.exists(blog):
