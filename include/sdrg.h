@@ -323,7 +323,8 @@ int32_t sdrg_engine_process_device(sdrg_engine *eng, const void *iq, int32_t for
 int32_t sdrg_engine_synchronize(sdrg_engine *eng);
 /* Enqueue the engine's work on the caller's HIP stream (a hipStream_t; NULL = the engine's own stream): the
  * SSB fork/join happens relative to it, so consumers on that stream (e.g. an RCCL gather of the records)
- * are ordered after each call without a host synchronisation.  Synchronises the previous stream first. */
+ * are ordered after each call without a host synchronisation.  Synchronises the previous stream first.
+ * The stream must outlive the engine (or be unset with NULL before it is destroyed). */
 int32_t sdrg_engine_set_stream(sdrg_engine *eng, void *hip_stream);
 /* Pipelining across calls (default off).  When on, sdrg_engine_process_device forks the SSB stages at the
  * start of each call and does not join them into the main stream at its end, so a call's SSB pipeline runs

@@ -535,8 +535,14 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         sdrg_engine_destroy(e);
         return code;
     };
-    if (hipStreamCreateWithFlags(&e->s_own, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->s_ssb, hipStreamNonBlocking) != hipSuccess)
+    // stream priorities (lab: SDRG_STREAM_PRIO = "main,ssb" in hipDeviceGetStreamPriorityRange units; default
+    // both normal)
+    int prio_main = 0, prio_ssb = 0;
+    if (const char *v = getenv("SDRG_STREAM_PRIO")) {
+        if (sscanf(v, "%d,%d", &prio_main, &prio_ssb) != 2) prio_main = prio_ssb = 0;
+    }
+    if (hipStreamCreateWithPriority(&e->s_own, hipStreamNonBlocking, prio_main) != hipSuccess ||
+        hipStreamCreateWithPriority(&e->s_ssb, hipStreamNonBlocking, prio_ssb) != hipSuccess)
         return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
     e->s_main = e->s_own;
     hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join};
@@ -552,8 +558,10 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
 int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (!e) return SDRG_OK;
     (void)hipSetDevice(e->device);
+    // the caller's stream (sdrg_engine_set_stream) must outlive the engine: synchronise it while it is set
     if (e->s_main) (void)hipStreamSynchronize(e->s_main);
     if (e->s_ssb) (void)hipStreamSynchronize(e->s_ssb);
+    e->spec_bank.last_stream = e->audio_bank.last_stream = nullptr;  // drained above
     void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch,
                     e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
@@ -566,8 +574,8 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
         for (hipEvent_t ev : rev)
             if (ev) (void)hipEventDestroy(ev);
     }
-    if (e->spec_bank_live) pulse_bank_release(&e->spec_bank);
-    if (e->audio_bank_live) pulse_bank_release(&e->audio_bank);
+    pulse_bank_release(&e->spec_bank);  // also what a failed lazy init left behind (null-safe)
+    pulse_bank_release(&e->audio_bank);
     if (e->s_own) (void)hipStreamDestroy(e->s_own);
     if (e->s_ssb) (void)hipStreamDestroy(e->s_ssb);
     delete e;
