@@ -32,6 +32,7 @@ import numpy as np  # noqa: E402
 N = 16384
 FS = 2_000_000
 CF = 100_000_000
+NCO_HZ = 250e3  # --ssb-variant nco127: the NCO offset of the BASELINE configs[2] variant
 B = 4096
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 ALG_BYTES_PER_SAMPLE = {"spectrum": 6.0}  # CS8: 2 B in + 4 B fftshifted float32 power out
@@ -118,6 +119,9 @@ def main() -> int:
                          "step is done; sdrg_engine_set_pipelining); 0: each step joins its SSB stream")
     ap.add_argument("--stages", default="all", choices=["all", "hot", "spectrum", "spectrum+stats", "ssb"],
                     help="ablation only: the metric is defined on 'all'")
+    ap.add_argument("--ssb-variant", default="reference", choices=["reference", "nco127"],
+                    help="nco127: the BASELINE configs[2] variant (a build extension, not the reference chain): NCO "
+                         "mixer at +250 kHz + 127-tap FIR (sdrg_engine_set_ssb_variant); a separately labelled line")
     args = ap.parse_args()
 
     import torch
@@ -137,6 +141,9 @@ def main() -> int:
     streams = args.streams
     cfg = sdrg.SDRConfig(centerFrequency=CF, samplesPerReading=N, sampleRate=FS, freqFocusRangeKhz=5, soundMode=1)
     eng = sdrg.Engine(cfg, streams, device=local)
+    variant = args.ssb_variant != "reference"
+    if variant:
+        eng.set_ssb_variant(NCO_HZ, 127)
     iq = synth_device_frames(torch, dev, streams, seed=0x5D12 + rank)
     spec = torch.empty((streams, N), dtype=torch.float32, device=dev)
     rec = torch.zeros((streams, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
@@ -220,9 +227,12 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "f32 (int8 CS8 in, int16 PCM out)",
         "data": "synthetic CS8 CW tones + Gaussian noise, generated on device",
-        "config": {"workload": f"C3: {streams} streams x {N}-pt CS8 frames @2 Msps per GPU; FFT + |X|^2 + fftshift "
-                               "+ signal-strength stats + SSB (DC, LPF, AGC, 255-tap FIR decim 41, EQ, PCM) + spectral and audio "
-                               "pulse detectors",
+        "config": {"workload": (f"C3: {streams} streams x {N}-pt CS8 frames @2 Msps per GPU; FFT + |X|^2 + fftshift "
+                                "+ signal-strength stats + SSB (DC, LPF, AGC, 255-tap FIR decim 41, EQ, PCM) + spectral "
+                                "and audio pulse detectors") if not variant else
+                               (f"C3-variant (BASELINE configs[2], build extension, not the reference chain): {streams} "
+                                f"streams x {N}-pt CS8 frames @2 Msps per GPU; FFT + stats + SSB with NCO mixer "
+                                f"(+{NCO_HZ / 1e3:g} kHz) + 127-tap FIR decim 41 (397 PCM/frame) + pulse detectors"),
                    "streams_per_gpu": streams, "samples_per_frame": N, "sample_rate": FS, "format": "CS8",
                    "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (", RCCL gather of records"
                                                                                          if world > 1 else "")},
@@ -241,9 +251,11 @@ def main() -> int:
                               "measured": "10 launches of the spectrum stage alone after the timed region"},
         "pipelined": bool(args.pipelined),
     }
+    if variant:
+        out["ssb_variant"] = {"nco_hz": NCO_HZ, "fir_taps": 127, "note": "not the reference's chain; no CPU baseline"}
     if args.stages != "all":
         out["ablation_stages"] = args.stages
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.stages == "all":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.stages == "all" and not variant:
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
         except Exception as exc:  # the baseline is informative; never fail the bench line on it

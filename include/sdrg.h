@@ -287,6 +287,24 @@ int32_t sdrg_engine_set_sound_mode(sdrg_engine *eng, int32_t mode);
 /* processSSB_opt's upperSideband argument (default 1, which is what SSBProcessor always passes,
  * ssb_processor.cpp:103; 0 gives the reference's lower-sideband result, Re - Im of {y, y} = 0). */
 int32_t sdrg_engine_set_upper_sideband(sdrg_engine *eng, int32_t upper);
+/* BUILD EXTENSION, not a reference interface (BASELINE.json configs[2], "SSB (USB) NCO + FIR-decimate, 127-tap
+ * FIR"; the reference chain has neither, ssb_demod_opt.cpp:122).  Off by default, and
+ * every reference-parity result above assumes it off.
+ *   nco_hz   : != 0 mixes each stream's IQ with a phase-continuous NCO before the chain: sample t of a call
+ *              becomes Re((I + jQ) e^{-j 2 pi ph / 2^32}), ph = phase + inc t (mod 2^32), inc =
+ *              round(nco_hz / sample_rate * 2^32) mod 2^32; the phasor is hi[ph >> 22] * lo[(ph >> 12) & 1023]
+ *              from two 1024-entry tables of e^{-j 2 pi k / 2^10} and e^{-j 2 pi k / 2^20} rounded to float.
+ *              The signal at +nco_hz lands at 0 Hz, where removeDC, the low-pass, AGC, FIR and EQ then run
+ *              unchanged.  phase starts at 0 and advances by inc * samp_count per call (every stream of the
+ *              engine sees the same calls).  0 = no mixer (the reference chain).
+ *   fir_taps : decimating FIR length, odd in [3, 255] (Hann-sinc of :121-134 at that length); 0 = 255.
+ *              The PCM frame length follows (sdrg_engine_pcm_len).
+ * Takes effect at the next call; restarts the NCO phase; filter state is kept. */
+int32_t sdrg_engine_set_ssb_variant(sdrg_engine *eng, double nco_hz, int32_t fir_taps);
+/* The variant in force: nco_hz, the FIR length the next call uses, the NCO increment and the next call's
+ * starting phase (any pointer may be NULL). */
+int32_t sdrg_engine_get_ssb_variant(const sdrg_engine *eng, double *nco_hz, int32_t *fir_taps,
+                                    uint32_t *nco_increment, uint32_t *nco_phase);
 /* Current configuration (BridgeConfig getters, bridge-config.h:41-51). */
 int32_t sdrg_engine_get_config(const sdrg_engine *eng, sdrg_config *out);
 int32_t sdrg_engine_n_streams(const sdrg_engine *eng);

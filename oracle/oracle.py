@@ -109,6 +109,11 @@ def lib() -> ctypes.CDLL:
             "oracle_fir_taps": (ctypes.c_int, [i64, ctypes.c_int, f32, P]),
             "oracle_ssb_decim": (ctypes.c_int, [u32]),
             "oracle_ssb_pcm_len": (ctypes.c_int, [i64, u32]),
+            "oracle_ssb_pcm_len_n": (ctypes.c_int, [i64, u32, ctypes.c_int]),
+            "oracle_fir_taps_n": (ctypes.c_int, [i64, ctypes.c_int, f32, ctypes.c_int, P]),
+            "oracle_nco_increment": (u32, [ctypes.c_double, u32]),
+            "oracle_nco_mix": (f32, [u32, f32, f32]),
+            "oracle_ssb_set_variant": (None, [P, ctypes.c_double, u32, ctypes.c_int]),
             "oracle_ssb_process": (ctypes.c_int, [P, P, i64, u32, ctypes.c_int, ctypes.c_int, P, P, P]),
             "oracle_run_streams": (ctypes.c_int, [P, ctypes.c_int, i32, i32, i32, u32, u32, i32, ctypes.c_int,
                                                   ctypes.c_int, P, P]),
@@ -223,8 +228,13 @@ def ssb_decim(sample_rate: int) -> int:
     return lib().oracle_ssb_decim(sample_rate)
 
 
-def ssb_pcm_len(n: int, sample_rate: int) -> int:
-    return lib().oracle_ssb_pcm_len(n, sample_rate)
+def ssb_pcm_len(n: int, sample_rate: int, fir_taps: int = 0) -> int:
+    return lib().oracle_ssb_pcm_len_n(n, sample_rate, fir_taps)
+
+
+def nco_increment(hz: float, sample_rate: int) -> int:
+    """NCO variant (build extension, include/sdrg.h): round(hz / fs * 2^32) mod 2^32."""
+    return lib().oracle_nco_increment(hz, sample_rate)
 
 
 class _Taps(ctypes.Structure):
@@ -238,6 +248,12 @@ class SsbState:
         self.buf = np.zeros(lib().oracle_ssb_state_size(), dtype=np.uint8)
         lib().oracle_ssb_state_init(_ptr(self.buf))
         self.frozen = 0
+        self.fir_taps = 0
+
+    def set_variant(self, nco_hz: float, sample_rate: int, fir_taps: int = 0) -> None:
+        """The NCO/short-FIR variant (a build extension; sdrg_engine_set_ssb_variant).  Restarts the phase."""
+        lib().oracle_ssb_set_variant(_ptr(self.buf), nco_hz, sample_rate, fir_taps)
+        self.fir_taps = fir_taps
 
     def process(self, iq: np.ndarray, sample_rate: int, mode: int = 1, upper: bool = True, stages: bool = False):
         iq = np.ascontiguousarray(iq, dtype=np.float32).reshape(-1)
@@ -245,7 +261,7 @@ class SsbState:
         if self.frozen == 0:
             self.frozen = n
         S = self.frozen
-        m = max(ssb_pcm_len(S, sample_rate), 1)
+        m = max(ssb_pcm_len(S, sample_rate, self.fir_taps), 1)
         pcm = np.zeros(m, dtype=np.int16)
         plen = ctypes.c_int32()
         taps = None

@@ -551,6 +551,10 @@ typedef struct oracle_ssb_state {
     int32_t eq_init;                    /* static bool eqInit (:277) */
     float hp[5], hp_z1, hp_z2;
     float bp[5], bp_z1, bp_z2;
+    /* NCO/short-FIR variant (a build extension, include/sdrg.h sdrg_engine_set_ssb_variant; all 0 = the
+     * reference chain) */
+    int32_t nco_on, fir_taps;
+    uint32_t nco_inc, nco_phase;
 } oracle_ssb_state;
 
 ORACLE_API int oracle_ssb_state_size(void) { return (int)sizeof(oracle_ssb_state); }
@@ -607,9 +611,10 @@ ORACLE_API void oracle_biquad_bandpass(float fs, float f0, float Q, float *c) {
     c[3] = a1 / a0; c[4] = a2 / a0;
 }
 
-/* simpleFIRDecimate's tap design (:121-134); returns the tap count N (taps written to h[0..N)). */
-ORACLE_API int oracle_fir_taps(int64_t in_size, int decim, float cutoff_rel, float *h) {
-    int N = 255;
+/* simpleFIRDecimate's tap design (:121-134) at length taps0 (0 = the reference's 255); returns the tap
+ * count N (taps written to h[0..N)). */
+ORACLE_API int oracle_fir_taps_n(int64_t in_size, int decim, float cutoff_rel, int taps0, float *h) {
+    int N = taps0 > 0 ? taps0 : 255;
     if (N > (int)in_size) N = (int)in_size | 1;
     int M = N - 1;
     float fc = cutoff_rel / decim;
@@ -626,17 +631,67 @@ ORACLE_API int oracle_fir_taps(int64_t in_size, int decim, float cutoff_rel, flo
     return N;
 }
 
+ORACLE_API int oracle_fir_taps(int64_t in_size, int decim, float cutoff_rel, float *h) {
+    return oracle_fir_taps_n(in_size, decim, cutoff_rel, 0, h);
+}
+
+/* ---- NCO variant (BUILD EXTENSION: no reference counterpart; include/sdrg.h) ----
+ * A 32-bit phase accumulator; the phasor e^{-j 2 pi ph / 2^32} is the product of two table entries,
+ * hi[ph >> 22] = e^{-j 2 pi a / 2^10} and lo[(ph >> 12) & 1023] = e^{-j 2 pi b / 2^20}, each evaluated in
+ * double and rounded to float.  Written independently of design.cpp / ssb.hip from the sdrg.h contract. */
+ORACLE_API uint32_t oracle_nco_increment(double hz, uint32_t sample_rate) {
+    double turns = hz / (double)sample_rate;
+    turns -= floor(turns);
+    return (uint32_t)(uint64_t)llround(turns * 4294967296.0);
+}
+
+static float nco_hi[2048], nco_lo[2048];
+static int nco_ready = 0;
+
+static void nco_init(void) {
+    if (nco_ready) return;
+    for (int k = 0; k < 1024; k++) {
+        double a = 2.0 * M_PI * (double)k / 1024.0, b = 2.0 * M_PI * (double)k / 1048576.0;
+        nco_hi[2 * k] = (float)cos(a);
+        nco_hi[2 * k + 1] = (float)(-sin(a));
+        nco_lo[2 * k] = (float)cos(b);
+        nco_lo[2 * k + 1] = (float)(-sin(b));
+    }
+    nco_ready = 1;
+}
+
+/* Re((xr + j xi) w(ph)) */
+ORACLE_API float oracle_nco_mix(uint32_t ph, float xr, float xi) {
+    nco_init();
+    const float *h = nco_hi + 2 * (ph >> 22), *l = nco_lo + 2 * ((ph >> 12) & 1023u);
+    float wr = h[0] * l[0] - h[1] * l[1];
+    float wi = h[0] * l[1] + h[1] * l[0];
+    return xr * wr - xi * wi;
+}
+
+/* Select the variant for this stream's chain (nco_hz 0 = no mixer; fir_taps 0 = 255); restarts the phase. */
+ORACLE_API void oracle_ssb_set_variant(oracle_ssb_state *s, double nco_hz, uint32_t sample_rate, int fir_taps) {
+    s->nco_on = nco_hz != 0.0;
+    s->nco_inc = s->nco_on ? oracle_nco_increment(nco_hz, sample_rate) : 0u;
+    s->nco_phase = 0u;
+    s->fir_taps = fir_taps;
+}
+
 ORACLE_API int oracle_ssb_decim(uint32_t sample_rate) {                             /* :273 */
     int d = (int)(sample_rate / 48000.0f);
     return d > 1 ? d : 1;
 }
 
-ORACLE_API int oracle_ssb_pcm_len(int64_t samp_count, uint32_t sample_rate) {
-    int N = 255;
+ORACLE_API int oracle_ssb_pcm_len_n(int64_t samp_count, uint32_t sample_rate, int taps0) {
+    int N = taps0 > 0 ? taps0 : 255;
     if (N > (int)samp_count) N = (int)samp_count | 1;
     const int decim = oracle_ssb_decim(sample_rate);
     if (samp_count < N) return 0;
     return (int)((samp_count - N) / decim + 1);
+}
+
+ORACLE_API int oracle_ssb_pcm_len(int64_t samp_count, uint32_t sample_rate) {
+    return oracle_ssb_pcm_len_n(samp_count, sample_rate, 0);
 }
 
 static float clampf_ref(float v, float lo, float hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
@@ -686,7 +741,9 @@ ORACLE_API int oracle_ssb_process(oracle_ssb_state *s, const float *iq, int64_t 
         const float a0 = s->lpf[0], a1 = s->lpf[1], a2 = s->lpf[2], b1 = s->lpf[3], b2 = s->lpf[4];
         float z1 = s->lpf_z1, z2 = s->lpf_z2;
         for (int64_t i = 0; i < S; i++) {
-            const float re = (i < n) ? iq[2 * i] : 0.0f;
+            float re = (i < n) ? iq[2 * i] : 0.0f;
+            /* variant: the NCO mixer on the present samples; the iq.resize() padding stays 0 */
+            if (s->nco_on) re = (i < n) ? oracle_nco_mix(s->nco_phase + s->nco_inc * (uint32_t)i, iq[2 * i], iq[2 * i + 1]) : 0.0f;
             dc = alpha * dc + one_minus * re;
             const float x = re - dc;
             if (taps && taps->dc_re) taps->dc_re[i] = x;
@@ -718,7 +775,7 @@ ORACLE_API int oracle_ssb_process(oracle_ssb_state *s, const float *iq, int64_t 
     /* simpleFIRDecimate(audio, decim, 0.45f) (:121-143) */
     const int decim = oracle_ssb_decim(sample_rate);
     float h[256];
-    const int N = oracle_fir_taps(S, decim, 0.45f, h);
+    const int N = oracle_fir_taps_n(S, decim, 0.45f, s->fir_taps, h);
     int n_out = 0;
     float *out48 = (float *)malloc(sizeof(float) * (size_t)(S / decim + 4));
     if (!out48) { free(audio); return -3; }
@@ -767,6 +824,7 @@ ORACLE_API int oracle_ssb_process(oracle_ssb_state *s, const float *iq, int64_t 
         pcm_out[i] = (int16_t)(v * 32767.0f);
     }
     *pcm_len = n_out;
+    s->nco_phase += s->nco_inc * (uint32_t)S;
     free(out48);
     free(audio);
     return 0;

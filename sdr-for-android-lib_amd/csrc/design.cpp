@@ -6,6 +6,8 @@
 // coefficients are bit-identical to the reference's x86-64 build (checked by tests/test_engine_host.py
 // against tests/golden/golden_ssb_design.npz, which comes from the reference build).
 #include <math.h>
+
+#include <cmath>
 #include <stdint.h>
 
 #include "design.h"
@@ -64,10 +66,10 @@ void design_bandpass(float fs, float f0, float Q, float c[5]) {
     c[4] = a2 / a0;
 }
 
-// simpleFIRDecimate's Hann-windowed sinc (:121-134); returns the tap count
-int design_fir(int64_t in_size, int decim, float cutoff_rel, float *h) {
-    int N = 255;
-    if (N > (int)in_size) N = (int)in_size | 1;
+// simpleFIRDecimate's Hann-windowed sinc (:121-134); returns the tap count.  taps0: the length asked
+// for (0 = the reference's 255; other values only through the NCO/short-FIR variant, sdrg.h)
+int design_fir(int64_t in_size, int decim, float cutoff_rel, float *h, int taps0) {
+    int N = ssb_taps_for(in_size, taps0);
     int M = N - 1;
     float fc = cutoff_rel / decim;
     for (int n = 0; n < N; n++) {
@@ -88,14 +90,14 @@ int ssb_decim(uint32_t sample_rate) {  // processSSB_opt :273
     return d > 1 ? d : 1;
 }
 
-int ssb_taps_for(int64_t samp_count) {
-    int N = 255;
+int ssb_taps_for(int64_t samp_count, int taps0) {
+    int N = taps0 > 0 ? taps0 : 255;
     if (N > (int)samp_count) N = (int)samp_count | 1;
     return N;
 }
 
-int ssb_pcm_len(int64_t samp_count, uint32_t sample_rate) {
-    const int N = ssb_taps_for(samp_count);
+int ssb_pcm_len(int64_t samp_count, uint32_t sample_rate, int taps0) {
+    const int N = ssb_taps_for(samp_count, taps0);
     if (samp_count < N) return 0;
     return (int)((samp_count - N) / ssb_decim(sample_rate) + 1);
 }
@@ -190,6 +192,29 @@ void design_pulse_sos(float fs, float fc, bool highpass, float c[5]) {
     }
     c[3] = 2.f * (K2 - 1.f) / norm;
     c[4] = (K2 - K / Q + 1.f) / norm;
+}
+
+// NCO of the SSB variant (sdrg.h, sdrg_engine_set_ssb_variant): phase increment per sample of a 32-bit
+// phase accumulator, round(hz / fs * 2^32) modulo 2^32 (negative frequencies wrap)
+uint32_t nco_increment(double hz, uint32_t sample_rate) {
+    const double turns = hz / (double)sample_rate;
+    const double frac = turns - std::floor(turns);  // [0, 1)
+    return (uint32_t)(uint64_t)std::llround(frac * 4294967296.0);  // 2^32 wraps to 0 through the cast
+}
+
+// e^{-j 2 pi ph / 2^32} = hi[ph >> 22] * lo[(ph >> 12) & 1023]: hi[a] = e^{-j 2 pi a / 2^10}, lo[b] =
+// e^{-j 2 pi b / 2^20}, each computed in double and rounded to float; interleaved {re, im}, hi then lo
+void nco_tables(float *tab) {
+    for (int a = 0; a < 1024; a++) {
+        const double t = 2.0 * M_PI * (double)a / 1024.0;
+        tab[2 * a] = (float)std::cos(t);
+        tab[2 * a + 1] = (float)-std::sin(t);
+    }
+    for (int b = 0; b < 1024; b++) {
+        const double t = 2.0 * M_PI * (double)b / 1048576.0;
+        tab[2048 + 2 * b] = (float)std::cos(t);
+        tab[2048 + 2 * b + 1] = (float)-std::sin(t);
+    }
 }
 
 }  // namespace sdrg

@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <vector>
 
@@ -59,9 +60,9 @@ struct SsbControl {
     float lpf[5] = {0, 0, 0, 0, 0};
     bool eq_init = false;
     float hp[5] = {0, 0, 0, 0, 0}, bp[5] = {0, 0, 0, 0, 0};
-    // FIR taps currently uploaded (depend on samp_count and decim)
+    // FIR taps currently uploaded (depend on samp_count, decim and the variant's tap count)
     int64_t taps_samp = -1;
-    int taps_decim = -1, n_taps = 0;
+    int taps_decim = -1, taps_req = -1, n_taps = 0;
 };
 
 struct EvSet {
@@ -123,6 +124,11 @@ struct sdrg_engine {
     std::vector<sdrg_pulse_output> h_pspec, h_paudio;
     bool cf_changed_pending = false;
     bool pipelined = false;  // sdrg_engine_set_pipelining: no join of the SSB stream per call
+    // NCO/short-FIR SSB variant (sdrg_engine_set_ssb_variant; a build extension, off by default)
+    double nco_hz = 0.0;
+    int fir_taps = 0;            // 0: the reference's 255
+    uint32_t nco_phase = 0;      // phase of the next call's first sample (advances by inc * samp_count)
+    float *d_nco_tab = nullptr;  // nco_tables(), uploaded once
     int upper = 1;
     bool has_cbs = false;
     sdrg_callbacks cbs{};
@@ -238,9 +244,12 @@ int32_t prepare_ssb(sdrg_engine *e, SsbParams *p) {
         c.rf_init = true;
     }
     const int decim = ssb_decim(fs);
-    if (c.taps_samp != c.samp_count || c.taps_decim != decim || !e->d_taps) {
+    if (c.taps_samp != c.samp_count || c.taps_decim != decim || c.taps_req != e->fir_taps || !e->d_taps) {
+        // an earlier call's SSB kernels may still read the taps and the chunk table (non-blocking streams)
+        HIP_TRY(hipStreamSynchronize(e->s_ssb));
         float h[256];
-        c.n_taps = design_fir(c.samp_count, decim, 0.45f, h);
+        c.n_taps = design_fir(c.samp_count, decim, 0.45f, h, e->fir_taps);
+        c.taps_req = e->fir_taps;
         if (!e->d_taps) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_taps), 256 * sizeof(float)));
         HIP_TRY(hipMemcpy(e->d_taps, h, sizeof(float) * (size_t)c.n_taps, hipMemcpyHostToDevice));
         c.taps_samp = c.samp_count;
@@ -248,7 +257,7 @@ int32_t prepare_ssb(sdrg_engine *e, SsbParams *p) {
         // FIR output ranges per pipeline chunk (the kernel then needs no integer division):
         // overlapping: D*o <= t1-1 and D*o + NT - 1 >= t0 ; completed: t0 <= D*o + NT - 1 < t1
         const int CH = ssb_pipe_chunk(), D = decim, NT = c.n_taps;
-        const int S = (int)c.samp_count, PL = ssb_pcm_len(c.samp_count, fs);
+        const int S = (int)c.samp_count, PL = ssb_pcm_len(c.samp_count, fs, e->fir_taps);
         const int nch = (S + CH - 1) / CH;
         std::vector<int> tab(4 * (size_t)nch);
         int ov_lo = 0, ov_hi = -1, dn_lo = 0, dn_hi = -1;
@@ -278,7 +287,7 @@ int32_t prepare_ssb(sdrg_engine *e, SsbParams *p) {
     p->upper = e->upper;  // SSBProcessor always asks for the upper sideband (ssb_processor.cpp:103)
     p->decim = decim;
     p->n_taps = c.n_taps;
-    p->pcm_len = ssb_pcm_len(c.samp_count, fs);
+    p->pcm_len = ssb_pcm_len(c.samp_count, fs, e->fir_taps);
     p->agc_target = c.agc_target;
     p->agc_fast = c.agc_fast;
     p->agc_slow = c.agc_slow;
@@ -287,6 +296,19 @@ int32_t prepare_ssb(sdrg_engine *e, SsbParams *p) {
     memcpy(p->lpf, c.lpf, sizeof(p->lpf));
     memcpy(p->hp, c.hp, sizeof(p->hp));
     memcpy(p->bp, c.bp, sizeof(p->bp));
+    if (e->nco_hz != 0.0) {
+        if (!e->d_nco_tab) {
+            std::vector<float> tab(4096);
+            nco_tables(tab.data());
+            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_nco_tab), sizeof(float) * tab.size()));
+            HIP_TRY(hipMemcpy(e->d_nco_tab, tab.data(), sizeof(float) * tab.size(), hipMemcpyHostToDevice));
+        }
+        p->nco_on = 1;
+        p->nco_inc = nco_increment(e->nco_hz, fs);
+        p->nco_phase = e->nco_phase;
+        p->nco_tab = e->d_nco_tab;
+        e->nco_phase += p->nco_inc * (uint32_t)c.samp_count;  // phase-continuous across calls
+    }
     return SDRG_OK;
 }
 
@@ -562,7 +584,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (e->s_main) (void)hipStreamSynchronize(e->s_main);
     if (e->s_ssb) (void)hipStreamSynchronize(e->s_ssb);
     e->spec_bank.last_stream = e->audio_bank.last_stream = nullptr;  // drained above
-    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch,
+    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_nco_tab, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch,
                     e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -618,6 +640,29 @@ int32_t sdrg_engine_set_upper_sideband(sdrg_engine *e, int32_t upper) {
     return SDRG_OK;
 }
 
+int32_t sdrg_engine_set_ssb_variant(sdrg_engine *e, double nco_hz, int32_t fir_taps) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if (fir_taps != 0 && (fir_taps < 3 || fir_taps > 255 || (fir_taps & 1) == 0))
+        return fail(SDRG_E_INVALID, "fir_taps must be 0 or odd in [3, 255], got %d", fir_taps);
+    if (!std::isfinite(nco_hz)) return fail(SDRG_E_INVALID, "nco_hz must be finite");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->s_ssb));  // in-flight SSB kernels read the taps being replaced
+    e->nco_hz = nco_hz;
+    e->fir_taps = fir_taps;
+    e->nco_phase = 0;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_get_ssb_variant(const sdrg_engine *e, double *nco_hz, int32_t *fir_taps,
+                                    uint32_t *nco_increment_out, uint32_t *nco_phase) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if (nco_hz) *nco_hz = e->nco_hz;
+    if (fir_taps) *fir_taps = ssb_taps_for(ssb_frozen_or(e), e->fir_taps);
+    if (nco_increment_out) *nco_increment_out = e->nco_hz != 0.0 ? nco_increment(e->nco_hz, (uint32_t)e->cfg.sample_rate) : 0;
+    if (nco_phase) *nco_phase = e->nco_phase;
+    return SDRG_OK;
+}
+
 int32_t sdrg_engine_get_config(const sdrg_engine *e, sdrg_config *out) {
     if (!e || !out) return fail(SDRG_E_INVALID, "null argument");
     *out = e->cfg;
@@ -628,7 +673,7 @@ int32_t sdrg_engine_n_streams(const sdrg_engine *e) { return e ? e->n_streams : 
 
 int32_t sdrg_engine_pcm_len(const sdrg_engine *e) {
     if (!e) return 0;
-    return ssb_pcm_len(ssb_frozen_or(e), (uint32_t)e->cfg.sample_rate);
+    return ssb_pcm_len(ssb_frozen_or(e), (uint32_t)e->cfg.sample_rate, e->fir_taps);
 }
 
 int32_t sdrg_engine_reset_state(sdrg_engine *e) {
@@ -639,6 +684,7 @@ int32_t sdrg_engine_reset_state(sdrg_engine *e) {
     HIP_TRY(hipMemset(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
     HIP_TRY(hipMemset(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
     e->ssb = SsbControl{};
+    e->nco_phase = 0;
     e->cf_changed_pending = false;
     e->spec_bank.reset_pending = true;
     e->audio_bank.reset_pending = true;
@@ -756,7 +802,7 @@ int32_t sdrg_engine_process_host(sdrg_engine *e, const void *iq, int32_t format,
     int pcm_len = 0;
     if (do_ssb) {
         // pcm length is known before the call: frozen (or about-to-be frozen) size and current fs
-        pcm_len = ssb_pcm_len(ssb_frozen_or(e), (uint32_t)e->cfg.sample_rate);
+        pcm_len = ssb_pcm_len(ssb_frozen_or(e), (uint32_t)e->cfg.sample_rate, e->fir_taps);
         int32_t rc = ensure_device(&e->d_pcm_stage, &e->pcm_stage_elems, (size_t)B * (pcm_len > 0 ? pcm_len : 1));
         if (rc) return rc;
     }

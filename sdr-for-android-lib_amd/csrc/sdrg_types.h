@@ -72,6 +72,12 @@ struct SsbParams {
     float lpf[5];              // a0 a1 a2 b1 b2 of rfFilter
     float hp[5];
     float bp[5];
+    // NCO/short-FIR variant (a build extension, sdrg_engine_set_ssb_variant): when nco_on, sample t of the
+    // frame is the real part of (I + jQ) e^{-j 2 pi ph / 2^32}, ph = nco_phase + nco_inc * t (mod 2^32),
+    // with the phasor from the two-level table nco_tab (design.cpp nco_tables); samples past n_in stay 0
+    int32_t nco_on;
+    uint32_t nco_inc, nco_phase;
+    const float *nco_tab;      // device [2][1024] {re, im}
 };
 
 // ------------------------------------------------------------------------------------------------

@@ -101,6 +101,37 @@ __device__ __forceinline__ void unpack_i8(const uint4 *u, float (&x)[8]) {
     }
 }
 
+// Q parts of 8 consecutive samples held in raw form in u[] (the NCO variant's loader).
+template <int FMT>
+__device__ __forceinline__ void unpack_q8(const uint4 *u, float (&x)[8]) {
+    if constexpr (FMT == SDRG_IQ_CS8 || FMT == SDRG_IQ_CU8) {
+        const uint32_t w[4] = {u[0].x, u[0].y, u[0].z, u[0].w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if constexpr (FMT == SDRG_IQ_CS8) {
+                x[2 * q] = (float)(int8_t)((w[q] >> 8) & 0xff) * (1.0f / 128.0f);
+                x[2 * q + 1] = (float)(int8_t)(w[q] >> 24) * (1.0f / 128.0f);
+            } else {
+                x[2 * q] = ((float)((w[q] >> 8) & 0xff) - 127.4f) * (1.0f / 128.0f);
+                x[2 * q + 1] = ((float)(w[q] >> 24) - 127.4f) * (1.0f / 128.0f);
+            }
+        }
+    } else if constexpr (FMT == SDRG_IQ_CS16) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t w[4] = {u[h].x, u[h].y, u[h].z, u[h].w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) x[4 * h + q] = (float)(int16_t)(w[q] >> 16) * (1.0f / 32768.0f);
+        }
+    } else {
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            x[2 * h] = __uint_as_float(u[h].y);
+            x[2 * h + 1] = __uint_as_float(u[h].w);
+        }
+    }
+}
+
 template <int FMT>
 __device__ __forceinline__ float load_i1(const char *frame, int n) {
     if constexpr (FMT == SDRG_IQ_CS8) return (float)(int8_t)frame[2 * (size_t)n] * (1.0f / 128.0f);
@@ -108,6 +139,27 @@ __device__ __forceinline__ float load_i1(const char *frame, int n) {
     else if constexpr (FMT == SDRG_IQ_CS16)
         return (float)reinterpret_cast<const int16_t *>(frame)[2 * (size_t)n] * (1.0f / 32768.0f);
     else return reinterpret_cast<const float *>(frame)[2 * (size_t)n];
+}
+
+// Imaginary part (Q) of sample n, same unpack conventions as load_i1.
+template <int FMT>
+__device__ __forceinline__ float load_q1(const char *frame, int n) {
+    if constexpr (FMT == SDRG_IQ_CS8) return (float)(int8_t)frame[2 * (size_t)n + 1] * (1.0f / 128.0f);
+    else if constexpr (FMT == SDRG_IQ_CU8) return ((float)(uint8_t)frame[2 * (size_t)n + 1] - 127.4f) * (1.0f / 128.0f);
+    else if constexpr (FMT == SDRG_IQ_CS16)
+        return (float)reinterpret_cast<const int16_t *>(frame)[2 * (size_t)n + 1] * (1.0f / 32768.0f);
+    else return reinterpret_cast<const float *>(frame)[2 * (size_t)n + 1];
+}
+
+// NCO variant: Re((xr + j xi) * w), w = e^{-j 2 pi ph / 2^32} = hi[ph >> 22] * lo[(ph >> 12) & 1023] with the
+// tables of design.cpp nco_tables (tab = hi then lo, {re, im}); complex products in this fixed order,
+// no contraction, so the CPU restatement (oracle/sdrg_oracle.c oracle_nco_mix) rounds identically.
+__device__ __forceinline__ float nco_mix(const float *tab, uint32_t ph, float xr, float xi) {
+    const float2 h = reinterpret_cast<const float2 *>(tab)[ph >> 22];
+    const float2 l = reinterpret_cast<const float2 *>(tab)[1024 + ((ph >> 12) & 1023)];
+    const float wr = h.x * l.x - h.y * l.y;
+    const float wi = h.x * l.y + h.y * l.x;
+    return xr * wr - xi * wi;
 }
 
 template <int FMT>
@@ -158,7 +210,8 @@ __global__ __launch_bounds__(WAVE) void ssb_chain_kernel(const char *__restrict_
 
     const int S = p.samp_count;
     const int live = p.n_in < S ? p.n_in : S;  // samples present; the rest is iq.resize() zero padding
-    const int n8 = (reinterpret_cast<uintptr_t>(frame) & 15) == 0 ? (live & ~7) : 0;  // 16-B loads need alignment
+    // 16-B loads need alignment; the NCO variant (which also needs Q) runs sample by sample
+    const int n8 = (!p.nco_on && (reinterpret_cast<uintptr_t>(frame) & 15) == 0) ? (live & ~7) : 0;
     int n = 0;
     for (; n < n8; n += 8) {
         float x[8];
@@ -168,6 +221,11 @@ __global__ __launch_bounds__(WAVE) void ssb_chain_kernel(const char *__restrict_
         for (int q = 0; q < 8; q++) y[q] = c.step(x[q]);
         *reinterpret_cast<float4 *>(out + n) = make_float4(y[0], y[1], y[2], y[3]);
         *reinterpret_cast<float4 *>(out + n + 4) = make_float4(y[4], y[5], y[6], y[7]);
+    }
+    if (p.nco_on) {
+        for (; n < live; n++)
+            out[n] = c.step(nco_mix(p.nco_tab, p.nco_phase + p.nco_inc * (uint32_t)n, load_i1<FMT>(frame, n),
+                                    load_q1<FMT>(frame, n)));
     }
     for (; n < live; n++) out[n] = c.step(load_i1<FMT>(frame, n));
     for (; n < S; n++) out[n] = c.step(0.0f);
@@ -300,6 +358,8 @@ struct PipeLds {
     // 0..3 floats so that any 32-tap window is read with aligned ds_read_b128
     float taps_sh[4][TAPS_ROW];
 };
+// NCO variant only, in dynamic LDS: the phasor tables, then the current chunk's CH phasors {re, im}
+constexpr int NCO_LDS_BYTES = (2 * 1024 * 2 + 2 * CH) * 4;
 
 // Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup release/acquire, which makes
 // every wave drain ALL its outstanding memory operations (s_waitcnt vmcnt(0)) first - the loader's
@@ -417,6 +477,7 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                                                           unsigned long long *__restrict__ stamps, int prio_mask,
                                                           int skip_mask, unsigned long long role_map, AudioFront af) {
     __shared__ PipeLds L;
+    extern __shared__ __attribute__((aligned(16))) float nco_lds[];  // NCO_LDS_BYTES when p.nco_on
     const int tid = threadIdx.x;
     const int hw_wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // runs on SIMD hw_wave % 4
     const int wave = (int)((role_map >> (4 * hw_wave)) & 15);     // the role it plays (PipeWave)
@@ -431,6 +492,8 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
         const int k = j + sh - CH;  // copy sh holds taps_pad[j + sh] at index j
         L.taps_sh[sh][j] = (k >= 0 && k < NT) ? taps[k] : 0.0f;
     }
+    if (p.nco_on)
+        for (int i = tid; i < 2 * 1024 * 2; i += PIPE_T) nco_lds[i] = p.nco_tab[i];
 
     const int my_s = lane & (PG - 1);  // serial roles: lane = 16 x copy + stream (all 64 lanes run; lanes < PG store)
     const float demod_k = p.upper ? 2.0f : 0.0f;  // demodSSB(y, y) = y + y or y - y (:89-94) as y * k
@@ -597,11 +660,24 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                 const int c = it;
                 if (c < nch) {
                     const int sl = lane >> 2, part = lane & 3;
+                    float *chunk_w = nco_lds + 2 * 1024 * 2;
+                    if (p.nco_on) {
+                        // every stream of the engine is at the same phase, so the chunk needs CH phasors, not
+                        // PG x CH: lane j forms sample c*CH + j's (the table product of nco_mix with x = 1, 0:
+                        // Re(w) = 1*wr - 0*wi = wr exactly, and likewise Im), written to LDS for the whole wave
+                        static_assert(CH == 64, "one phasor per lane");
+                        const uint32_t ph = p.nco_phase + p.nco_inc * (uint32_t)(c * CH + lane);
+                        const float2 h = reinterpret_cast<const float2 *>(nco_lds)[ph >> 22];
+                        const float2 l = reinterpret_cast<const float2 *>(nco_lds)[1024 + ((ph >> 12) & 1023)];
+                        reinterpret_cast<float2 *>(chunk_w)[lane] = make_float2(h.x * l.x - h.y * l.y, h.x * l.y + h.y * l.x);
+                        // this wave reads what its own lanes wrote: LDS ops of one wave complete in order
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    }
 #pragma unroll
                     for (int g8 = 0; g8 < CH / 32; ++g8) {
                         const int within = part * (CH / 4) + g8 * 8;
                         const int t = c * CH + within;
-                        float x[8];
+                        float x[8], xq[8];
                         if constexpr (DMA) {
                             constexpr int U4 = 8 * (int)bytes_per_sample<FMT>() / 16;  // 16-B pieces per 8 samples
                             const int off = ((c % BC) * CH + within) * (int)bytes_per_sample<FMT>();
@@ -610,10 +686,24 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
 #pragma unroll
                             for (int q = 0; q < U4; q++) u[q] = L.raw[(c / BC) % NRAW][(piece + q) * 64 + sl * 4 + quarter];
                             unpack_i8<FMT>(u, x);
+                            if (p.nco_on) unpack_q8<FMT>(u, xq);
                         } else {
                             if (s0 + sl < n_frames) {
                                 const char *frame = iq + (size_t)(s0 + sl) * p.n_in * bps;
                                 load_i8_masked<FMT>(frame, t, n_live, x);
+                                if (p.nco_on) {
+#pragma unroll
+                                    for (int q = 0; q < 8; q++) xq[q] = (t + q < n_live) ? load_q1<FMT>(frame, t + q) : 0.0f;
+                                }
+                            }
+                        }
+                        if (p.nco_on) {  // the NCO variant: Re(x w) as nco_mix, then the frame's zero padding
+                            const float4 *w4 = reinterpret_cast<const float4 *>(chunk_w + 2 * within);
+#pragma unroll
+                            for (int h = 0; h < 4; h++) {
+                                const float4 w = w4[h];  // phasors of samples within + 2h, + 2h + 1
+                                x[2 * h] = x[2 * h] * w.x - xq[2 * h] * w.y;
+                                x[2 * h + 1] = x[2 * h + 1] * w.z - xq[2 * h + 1] * w.w;
                             }
                         }
 #pragma unroll
@@ -860,7 +950,8 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
     const int4 *chunk_out = reinterpret_cast<const int4 *>(chunk_table);
     if (chunk_out && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels()) {
         const dim3 grid((n_frames + PG - 1) / PG);
-        const size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
+        size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
+        if (p.nco_on && pad < (size_t)NCO_LDS_BYTES) pad = NCO_LDS_BYTES;  // the dynamic part holds the NCO tables
         const int bps = fmt == SDRG_IQ_CF32 ? 8 : fmt == SDRG_IQ_CS16 ? 4 : 2;
         const int bc = 512 / (CH * bps) > 0 ? 512 / (CH * bps) : 1;  // batch_chunks<FMT>()
         const int n_live = p.n_in < p.samp_count ? p.n_in : p.samp_count;

@@ -80,7 +80,7 @@ EXPORTS = [
     "sdrg_engine_apply_config", "sdrg_engine_set_frequency", "sdrg_engine_set_frequency_focus_range",
     "sdrg_engine_set_sound_mode", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
     "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_set_stream",
-    "sdrg_engine_set_pipelining",
+    "sdrg_engine_set_pipelining", "sdrg_engine_set_ssb_variant", "sdrg_engine_get_ssb_variant",
     "sdrg_engine_process_host",
     "sdrg_engine_set_callbacks", "sdrg_engine_set_profiling", "sdrg_engine_get_timings",
     "sdrg_engine_get_timing_stats", "sdrg_engine_reset_timing_stats",
@@ -202,6 +202,8 @@ def load() -> ctypes.CDLL:
         "sdrg_engine_synchronize": (_I32, [P]),
         "sdrg_engine_set_stream": (_I32, [P, P]),
         "sdrg_engine_set_pipelining": (_I32, [P, _I32]),
+        "sdrg_engine_set_ssb_variant": (_I32, [P, ctypes.c_double, _I32]),
+        "sdrg_engine_get_ssb_variant": (_I32, [P, P, P, P, P]),
         "sdrg_engine_process_host": (_I32, [P, P, _I32, _I32, P, P, P, _I64]),
         "sdrg_engine_set_callbacks": (_I32, [P, ctypes.POINTER(_Callbacks)]),
         "sdrg_engine_set_profiling": (_I32, [P, _I32]),
@@ -408,6 +410,17 @@ class Engine:
         """Overlap each call's SSB stages with the next call's spectrum (see include/sdrg.h)."""
         _check(load().sdrg_engine_set_pipelining(self._h, int(on)), "set_pipelining")
 
+    def set_ssb_variant(self, nco_hz: float = 0.0, fir_taps: int = 0) -> None:
+        """BUILD EXTENSION (not a reference interface): NCO mixer at nco_hz before the SSB chain and a
+        fir_taps-long decimating FIR (0 = the reference's 255).  (0, 0) is the reference chain."""
+        _check(load().sdrg_engine_set_ssb_variant(self._h, float(nco_hz), int(fir_taps)), "set_ssb_variant")
+
+    def ssb_variant(self) -> dict:
+        hz, taps, inc, ph = ctypes.c_double(), ctypes.c_int32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(load().sdrg_engine_get_ssb_variant(self._h, ctypes.byref(hz), ctypes.byref(taps), ctypes.byref(inc),
+                                                  ctypes.byref(ph)), "get_ssb_variant")
+        return {"nco_hz": hz.value, "fir_taps": taps.value, "nco_increment": inc.value, "nco_phase": ph.value}
+
     def set_stream(self, hip_stream: int | None) -> None:
         """Enqueue on the caller's HIP stream (e.g. torch.cuda.current_stream().cuda_stream); None = own."""
         _check(load().sdrg_engine_set_stream(self._h, hip_stream), "set_stream")
@@ -465,10 +478,6 @@ class PulseBank:
 
     def reset(self) -> None:
         _check(load().sdrg_pulse_bank_reset(self._h), "pulse_bank_reset")
-
-    def set_pipelining(self, on: bool) -> None:
-        """Overlap each call's SSB stages with the next call's spectrum (see include/sdrg.h)."""
-        _check(load().sdrg_engine_set_pipelining(self._h, int(on)), "set_pipelining")
 
     def set_stream(self, hip_stream: int | None) -> None:
         _check(load().sdrg_pulse_bank_set_stream(self._h, hip_stream), "pulse_bank_set_stream")
