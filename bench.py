@@ -122,6 +122,9 @@ def main() -> int:
     ap.add_argument("--ssb-variant", default="reference", choices=["reference", "nco127"],
                     help="nco127: the BASELINE configs[2] variant (a build extension, not the reference chain): NCO "
                          "mixer at +250 kHz + 127-tap FIR (sdrg_engine_set_ssb_variant); a separately labelled line")
+    ap.add_argument("--gather", default="records", choices=["records", "records+focus"],
+                    help="N > 1: what each step gathers to rank 0 over RCCL: the 72-B frame records (default), or "
+                         "also each frame's focus-window spectrum slice (sdrg.shard.gather_focus)")
     args = ap.parse_args()
 
     import torch
@@ -157,6 +160,10 @@ def main() -> int:
               "spectrum+stats": sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS}[args.stages]
 
     gathered = torch.empty((world * streams, rec.shape[1]), dtype=torch.uint8, device=dev) if rank == 0 else None
+    focus = args.gather == "records+focus"
+    f_lo, f_n = sdrg.focus_window(FS, N, 5)
+    f_stage = torch.empty((streams, f_n), dtype=torch.float32, device=dev) if focus else None
+    f_out = torch.empty((world * streams, f_n), dtype=torch.float32, device=dev) if focus and rank == 0 else None
     if world > 1:
         # the engine enqueues on a torch stream that is current for the collectives too, so the RCCL gather is
         # ordered after each step on the GPU without a host synchronisation, and the next step's kernels
@@ -171,6 +178,8 @@ def main() -> int:
         now[0] += 8  # 16384 samples @ 2 Msps = 8.192 ms per frame
         if world > 1:
             shard.gather_records(rec, world, rank, dst=0, out=gathered)  # the one collective: records to rank 0
+            if focus:
+                shard.gather_focus(spec, f_lo, f_n, world, rank, dst=0, out=f_out, staging=f_stage)
 
     if args.pipelined:
         eng.set_pipelining(True)
@@ -234,8 +243,9 @@ def main() -> int:
                                 f"streams x {N}-pt CS8 frames @2 Msps per GPU; FFT + stats + SSB with NCO mixer "
                                 f"(+{NCO_HZ / 1e3:g} kHz) + 127-tap FIR decim 41 (397 PCM/frame) + pulse detectors"),
                    "streams_per_gpu": streams, "samples_per_frame": N, "sample_rate": FS, "format": "CS8",
-                   "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (", RCCL gather of records"
-                                                                                         if world > 1 else "")},
+                   "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (
+                       (", RCCL gather of records" + (f" + {f_n}-bin focus spectra" if focus else ""))
+                       if world > 1 else "")},
         "kernel_ms": {k: round(v, 4) for k, v in ts.items() if k != "count"},
         "roofline": {"kernel": "spectrum16k_kernel (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

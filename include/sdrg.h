@@ -261,6 +261,12 @@ const char *sdrg_last_error(void);      /* thread-local message for the last fai
  * (ssb_demod_opt.cpp:121-143, :273). */
 int32_t sdrg_ssb_pcm_len(int32_t n, int64_t sample_rate);
 
+/* The focus window of evaluateSignalStrength (fft_process.cpp:124-140) in the fftshifted spectrum the engine
+ * writes: bins [*first_bin, *first_bin + *n_bins) hold offsets -focus_khz .. +focus_khz kHz around the
+ * centre.  *n_bins = 0 when the window is empty (focus wider than the band, :218-247).  Host-only; used to
+ * gather only the spectrum slice a consumer looks at (sdrg/shard.py gather_focus). */
+int32_t sdrg_focus_window(int64_t sample_rate, int32_t n, int32_t focus_khz, int32_t *first_bin, int32_t *n_bins);
+
 /* The SSB filter design the engine uses for a configuration, from the reference's own expressions:
  * rfFilter low-pass (iir2InitLowpass at (float)fs with the sound mode's fc/Q, ssb_demod_opt.cpp:60-73, :262),
  * HP/BP biquads (:148-175, :278-279) and the FIR taps (:121-134).  lpf/hp/bp: {a0, a1, a2, b1, b2};

@@ -514,6 +514,15 @@ int32_t sdrg_ssb_pcm_len(int32_t n, int64_t sample_rate) {
     return ssb_pcm_len(n, (uint32_t)sample_rate);
 }
 
+int32_t sdrg_focus_window(int64_t sample_rate, int32_t n, int32_t focus_khz, int32_t *first_bin, int32_t *n_bins) {
+    if (!first_bin || !n_bins) return fail(SDRG_E_INVALID, "null output");
+    if (n <= 0 || (uint32_t)sample_rate == 0 || focus_khz < 0) return fail(SDRG_E_INVALID, "bad geometry arguments");
+    const StatsGeometry g = stats_geometry((uint32_t)sample_rate, 0, n, focus_khz);
+    *first_bin = g.focus_lo;
+    *n_bins = g.focus_len > 0 ? g.focus_len : 0;
+    return SDRG_OK;
+}
+
 int32_t sdrg_ssb_design(int32_t samp_count, int64_t sample_rate, int32_t sound_mode, float *lpf, float *hp,
                         float *bp, float *taps, int32_t *n_taps) {
     if (samp_count <= 0 || (uint32_t)sample_rate == 0) return fail(SDRG_E_INVALID, "bad samp_count/sample_rate");

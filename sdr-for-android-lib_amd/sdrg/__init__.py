@@ -76,7 +76,7 @@ PULSE_OUTPUT_DTYPE = np.dtype(
 
 # Every entry point include/sdrg.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "sdrg_abi_version", "sdrg_last_error", "sdrg_ssb_pcm_len", "sdrg_ssb_design", "sdrg_engine_create", "sdrg_engine_destroy",
+    "sdrg_abi_version", "sdrg_last_error", "sdrg_ssb_pcm_len", "sdrg_focus_window", "sdrg_ssb_design", "sdrg_engine_create", "sdrg_engine_destroy",
     "sdrg_engine_apply_config", "sdrg_engine_set_frequency", "sdrg_engine_set_frequency_focus_range",
     "sdrg_engine_set_sound_mode", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
     "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_set_stream",
@@ -203,6 +203,7 @@ def load() -> ctypes.CDLL:
         "sdrg_engine_set_stream": (_I32, [P, P]),
         "sdrg_engine_set_pipelining": (_I32, [P, _I32]),
         "sdrg_engine_set_ssb_variant": (_I32, [P, ctypes.c_double, _I32]),
+        "sdrg_focus_window": (_I32, [_I64, _I32, _I32, P, P]),
         "sdrg_engine_get_ssb_variant": (_I32, [P, P, P, P, P]),
         "sdrg_engine_process_host": (_I32, [P, P, _I32, _I32, P, P, P, _I64]),
         "sdrg_engine_set_callbacks": (_I32, [P, ctypes.POINTER(_Callbacks)]),
@@ -251,6 +252,13 @@ def _check(rc: int, what: str) -> None:
 
 def ssb_pcm_len(n: int, sample_rate: int) -> int:
     return int(load().sdrg_ssb_pcm_len(n, sample_rate))
+
+
+def focus_window(sample_rate: int, n: int, focus_khz: int) -> tuple[int, int]:
+    """(first_bin, n_bins) of evaluateSignalStrength's focus window in the fftshifted spectrum (host-side)."""
+    lo, nb = ctypes.c_int32(), ctypes.c_int32()
+    _check(load().sdrg_focus_window(sample_rate, n, focus_khz, ctypes.byref(lo), ctypes.byref(nb)), "focus_window")
+    return lo.value, nb.value
 
 
 def ssb_design(samp_count: int, sample_rate: int, sound_mode: int = 1) -> dict:

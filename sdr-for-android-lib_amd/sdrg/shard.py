@@ -3,7 +3,9 @@
 Frames are independent and the per-stream state (FFTProcessor members, processSSB_opt statics) is small,
 so the path shards by stream with no data-path collective: rank r owns streams [r*B, (r+1)*B) and runs its
 own engine on its own GPU (weak scaling).  The one collective is the per-step gather of the 72-byte frame
-records to rank 0; spectra and PCM stay on the GPU that produced them.
+records to rank 0; spectra and PCM stay on the GPU that produced them.  A consumer that
+wants spectra on rank 0 gathers the focus-window slice of each frame (gather_focus: 82 bins of 16384 at
+2 MHz / 5 kHz, 0.5 % of the bytes) rather than the 268 MB of full spectra per GPU per step.
 """
 from __future__ import annotations
 
@@ -37,3 +39,19 @@ def gather_records(records, world: int, rank: int, dst: int = 0, group=None, out
         bufs = None
     dist.gather(records, bufs, dst=dst, group=group)
     return out if rank == dst else None
+
+
+def gather_focus(spectra, first_bin: int, n_bins: int, world: int, rank: int, dst: int = 0, group=None, out=None,
+                 staging=None):
+    """Gather each rank's focus-window spectrum slice [B, n_bins] (bins [first_bin, first_bin + n_bins) of the
+    [B, N] fftshifted spectra, sdrg.focus_window) to `dst` as [world*B, n_bins] float32, global stream order.
+
+    `staging` (optional, every rank): a preallocated contiguous [B, n_bins] tensor for the slice; `out` (on dst):
+    the preallocated result.  Returns the result on dst, None elsewhere (world == 1: the slice itself)."""
+    import torch
+
+    sl = spectra[:, first_bin:first_bin + n_bins]
+    if staging is None:
+        staging = torch.empty((spectra.shape[0], n_bins), dtype=spectra.dtype, device=spectra.device)
+    staging.copy_(sl)
+    return gather_records(staging, world, rank, dst=dst, group=group, out=out)

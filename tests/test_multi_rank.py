@@ -1,6 +1,7 @@
 """world_size-2 test of the sharded multi-GPU path on CPU (gloo): each rank owns a contiguous block of streams
 and runs them for three steps (the per-rank engine is stood in for by the oracle here: no GPU in this suite);
-the records gathered to rank 0 must equal a single-process run over all streams bit for bit."""
+the records gathered to rank 0 must equal a single-process run over all streams bit for bit, and so must the
+focus-window spectrum slices gathered beside them (shard.gather_focus)."""
 import os
 import socket
 import sys
@@ -13,16 +14,20 @@ from conftest import ROOT
 N, FS, CF, FOCUS, B, STEPS = 4096, 2_500_000, 100_000_000, 5, 3, 3
 
 
-def _records(O, first, last):
+def _records(O, first, last, spectra=None):
     raw = O.synth_frames((last) * STEPS, N, O.CS8, tone_hz=1200.0, fs=FS)
     states = {s: O.FftState(CF, FS, N, FOCUS) for s in range(first, last)}
     out = []
     for step in range(STEPS):
         recs = []
+        specs = []
         for s in range(first, last):
             iq = O.unpack(O.CS8, raw[s * STEPS + step], N)
-            _, rec = states[s].process(iq, 1000 + 10 * step)
+            spec, rec = states[s].process(iq, 1000 + 10 * step)
             recs.append(rec)
+            specs.append(np.asarray(spec, np.float32).copy())
+        if spectra is not None:
+            spectra.append(np.stack(specs))
         arr = np.zeros(len(recs), dtype=O.RECORD_DTYPE)  # fields only: the struct's tail padding is unspecified
         for f in O.RECORD_DTYPE.names:
             arr[f] = [r[f] for r in recs]
@@ -36,23 +41,28 @@ def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
     import oracle as O
+    import sdrg
     from sdrg import shard
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     first, last = shard.stream_range(rank, world, B)
-    got = []
+    lo, nb = sdrg.focus_window(FS, N, FOCUS)
+    got, got_focus = [], []
     out = None
-    for k, recs in enumerate(_records(O, first, last)):
+    specs = []
+    for k, recs in enumerate(_records(O, first, last, specs)):
         t = torch.from_numpy(recs.view(np.uint8).reshape(B, -1).copy())
         if rank == 0 and k > 0 and out is None:  # later steps gather into a preallocated buffer (bench.py)
             out = torch.empty((world * B, t.shape[1]), dtype=torch.uint8)
         g = shard.gather_records(t, world, rank, out=out)
+        gf = shard.gather_focus(torch.from_numpy(specs[k]), lo, nb, world, rank)
         if rank == 0:
             got.append(g.numpy().copy())
+            got_focus.append(gf.numpy().copy())
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0:
-        q.put(got)
+        q.put((got, got_focus))
 
 
 def test_sharded_records_equal_single_process(oracle_mod):
@@ -66,14 +76,17 @@ def test_sharded_records_equal_single_process(oracle_mod):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=300)
+    got, got_focus = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want = _records(O, 0, world * B)
-    assert len(got) == STEPS
+    specs = []
+    want = _records(O, 0, world * B, specs)
+    lo, hi = O.window_geometry(FS, N, FOCUS)[:2]
+    assert len(got) == STEPS and len(got_focus) == STEPS
     for step in range(STEPS):
         np.testing.assert_array_equal(got[step], want[step].view(np.uint8).reshape(world * B, -1))
+        np.testing.assert_array_equal(got_focus[step], specs[step][:, lo:hi + 1])
 
 
 def test_stream_range():
