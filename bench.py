@@ -60,7 +60,7 @@ def pmc_traffic(kernel: str, streams: int):
     tools/profile_round.sh + tools/profile_summary.py on this same bench command), or None."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_pmc.json")), key=os.path.getmtime):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_pmc.json"))):  # round tags sort in order
         try:
             d = json.load(open(f))
             t = d["kernels"][kernel]["traffic_bytes"]
