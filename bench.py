@@ -71,6 +71,22 @@ def pmc_traffic(kernel: str, streams: int):
     return best
 
 
+def d2d_copy_gbs(torch, dev, nbytes: int = 1 << 30, reps: int = 10) -> float:
+    """Measured HBM bandwidth: a device-to-device copy of nbytes, (read + write) bytes per second, HIP events."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    t1.record()
+    t1.synchronize()
+    ms = t0.elapsed_time(t1) / reps
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
 def cpu_baseline(threads: int, target_cpu_s: float = 15.0) -> dict:
     """The oracle (our C restatement of the reference path: FFT + stats + SSB + pulse detectors per frame), one fresh stream per
     frame, timed on the host cores with `threads` worker threads (ctypes releases the GIL)."""
@@ -122,9 +138,11 @@ def main() -> int:
     ap.add_argument("--ssb-variant", default="reference", choices=["reference", "nco127"],
                     help="nco127: the BASELINE configs[2] variant (a build extension, not the reference chain): NCO "
                          "mixer at +250 kHz + 127-tap FIR (sdrg_engine_set_ssb_variant); a separately labelled line")
-    ap.add_argument("--gather", default="records", choices=["records", "records+focus"],
-                    help="N > 1: what each step gathers to rank 0 over RCCL: the 72-B frame records (default), or "
-                         "also each frame's focus-window spectrum slice (sdrg.shard.gather_focus)")
+    ap.add_argument("--gather", default="records", choices=["records", "records+pcm", "records+focus",
+                                                            "records+pcm+focus"],
+                    help="N > 1: what each step gathers to rank 0 over RCCL: the 72-B frame records (default), plus "
+                         "optionally each frame's PCM (SURVEY 8e) and/or its focus-window spectrum slice "
+                         "(sdrg.shard.gather_focus)")
     args = ap.parse_args()
 
     import torch
@@ -160,7 +178,9 @@ def main() -> int:
               "spectrum+stats": sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS}[args.stages]
 
     gathered = torch.empty((world * streams, rec.shape[1]), dtype=torch.uint8, device=dev) if rank == 0 else None
-    focus = args.gather == "records+focus"
+    focus = "focus" in args.gather
+    gather_pcm = "pcm" in args.gather
+    p_out = torch.empty((world * streams, plen), dtype=torch.int16, device=dev) if gather_pcm and rank == 0 else None
     f_lo, f_n = sdrg.focus_window(FS, N, 5)
     f_stage = torch.empty((streams, f_n), dtype=torch.float32, device=dev) if focus else None
     f_out = torch.empty((world * streams, f_n), dtype=torch.float32, device=dev) if focus and rank == 0 else None
@@ -178,6 +198,8 @@ def main() -> int:
         now[0] += 8  # 16384 samples @ 2 Msps = 8.192 ms per frame
         if world > 1:
             shard.gather_records(rec, world, rank, dst=0, out=gathered)  # the one collective: records to rank 0
+            if gather_pcm:
+                shard.gather_records(pcm, world, rank, dst=0, out=p_out)
             if focus:
                 shard.gather_focus(spec, f_lo, f_n, world, rank, dst=0, out=f_out, staging=f_stage)
 
@@ -210,6 +232,7 @@ def main() -> int:
         eng.process_device(iq.data_ptr(), sdrg.CS8, sdrg.STAGE_SPECTRUM, spec.data_ptr(), None, None, now[0])
     eng.synchronize()
     spec_iso_ms = eng.timing_stats()["spectrum_ms"]
+    d2d = d2d_copy_gbs(torch, dev)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -244,7 +267,8 @@ def main() -> int:
                                 f"(+{NCO_HZ / 1e3:g} kHz) + 127-tap FIR decim 41 (397 PCM/frame) + pulse detectors"),
                    "streams_per_gpu": streams, "samples_per_frame": N, "sample_rate": FS, "format": "CS8",
                    "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (
-                       (", RCCL gather of records" + (f" + {f_n}-bin focus spectra" if focus else ""))
+                       (", RCCL gather of records" + (" + PCM" if gather_pcm else "")
+                        + (f" + {f_n}-bin focus spectra" if focus else ""))
                        if world > 1 else "")},
         "kernel_ms": {k: round(v, 4) for k, v in ts.items() if k != "count"},
         "roofline": {"kernel": "spectrum16k_kernel (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
@@ -259,6 +283,10 @@ def main() -> int:
         "roofline_isolated": {"kernel": "spectrum16k_kernel", "bound": "hbm", "achieved": round(achieved_iso, 1),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_iso / HBM_PEAK_GBS, 4),
                               "measured": "10 launches of the spectrum stage alone after the timed region"},
+        "hbm_measured": {"d2d_copy_GBs": round(d2d, 1), "note": "device-to-device copy of 1 GiB, read + write bytes "
+                                                                "per second (SURVEY 8d's measured peak)",
+                         "frac_timed": round(achieved / d2d, 4) if d2d else None,
+                         "frac_isolated": round(achieved_iso / d2d, 4) if d2d else None},
         "pipelined": bool(args.pipelined),
     }
     if variant:
