@@ -138,11 +138,11 @@ def main() -> int:
     ap.add_argument("--ssb-variant", default="reference", choices=["reference", "nco127"],
                     help="nco127: the BASELINE configs[2] variant (a build extension, not the reference chain): NCO "
                          "mixer at +250 kHz + 127-tap FIR (sdrg_engine_set_ssb_variant); a separately labelled line")
-    ap.add_argument("--gather", default="records", choices=["records", "records+pcm", "records+focus",
-                                                            "records+pcm+focus"],
-                    help="N > 1: what each step gathers to rank 0 over RCCL: the 72-B frame records (default), plus "
-                         "optionally each frame's PCM (SURVEY 8e) and/or its focus-window spectrum slice "
-                         "(sdrg.shard.gather_focus)")
+    ap.add_argument("--gather", default="records+focus", choices=["records", "records+pcm", "records+focus",
+                                                                  "records+pcm+focus"],
+                    help="N > 1: what each step gathers to rank 0 over RCCL: the 72-B frame records (peak indices and "
+                         "statistics) and, by default, each frame's focus-window spectrum slice (sdrg.shard.gather_focus; "
+                         "BASELINE configs[3] gathers spectra + peak indices), optionally each frame's PCM (SURVEY 8e)")
     args = ap.parse_args()
 
     import torch
