@@ -42,16 +42,18 @@ def log(msg: str) -> None:
     print(msg, file=sys.stderr, flush=True)
 
 
-def synth_device_frames(torch, dev, n_streams: int, seed: int):
-    """CS8 CW tone per stream (inside the 5 kHz focus) + Gaussian noise, generated on the GPU."""
+def synth_device_frames(torch, dev, n_streams: int, seed: int, n: int = N, cs16: bool = False):
+    """CW tone per stream (inside the 5 kHz focus) + Gaussian noise, generated on the GPU: CS8 (amplitude 60,
+    noise 4) or CS16 (amplitude 8000, noise 400), SURVEY 8d C1 / C5."""
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
+    amp, sig, lo, hi, dt = (8000.0, 400.0, -32768, 32767, torch.int16) if cs16 else (60.0, 4.0, -128, 127, torch.int8)
     tones = (torch.rand(n_streams, 1, device=dev, generator=g, dtype=torch.float64) * 9000.0 - 4500.0)
-    t = torch.arange(N, device=dev, dtype=torch.float64)[None, :]
+    t = torch.arange(n, device=dev, dtype=torch.float64)[None, :]
     ph = 2 * np.pi * tones * t / FS
-    i = torch.round(60 * torch.cos(ph) + 4 * torch.randn(n_streams, N, device=dev, generator=g, dtype=torch.float64))
-    q = torch.round(60 * torch.sin(ph) + 4 * torch.randn(n_streams, N, device=dev, generator=g, dtype=torch.float64))
-    iq = torch.stack([i, q], dim=2).clamp_(-128, 127).to(torch.int8).reshape(n_streams, 2 * N).contiguous()
+    i = torch.round(amp * torch.cos(ph) + sig * torch.randn(n_streams, n, device=dev, generator=g, dtype=torch.float64))
+    q = torch.round(amp * torch.sin(ph) + sig * torch.randn(n_streams, n, device=dev, generator=g, dtype=torch.float64))
+    iq = torch.stack([i, q], dim=2).clamp_(lo, hi).to(dt).reshape(n_streams, 2 * n).contiguous()
     return iq
 
 
@@ -133,8 +135,13 @@ def main() -> int:
     ap.add_argument("--pipelined", type=int, default=1,
                     help="1 (default): each step's SSB stages run beside the next step's spectrum (all work of every "
                          "step is done; sdrg_engine_set_pipelining); 0: each step joins its SSB stream")
-    ap.add_argument("--stages", default="all", choices=["all", "hot", "spectrum", "spectrum+stats", "ssb"],
-                    help="ablation only: the metric is defined on 'all'")
+    ap.add_argument("--stages", default=None, choices=["all", "hot", "spectrum", "spectrum+stats", "ssb"],
+                    help="ablation only: the metric is defined on 'all' (the c3 default)")
+    ap.add_argument("--config", default="c3", choices=["c3", "c2", "c5"],
+                    help="c3 (default, the metric's workload): BASELINE configs[1]+SSB, every stage; c2: BASELINE "
+                         "configs[1] as written (FFT + power + stats only); c5: BASELINE configs[4] (65536-pt CS16, "
+                         "1024 streams, FFT + stats, --focus kHz); c2 and c5 print separately labelled lines")
+    ap.add_argument("--focus", type=int, default=5, help="c5: freqFocusRangeKhz (SURVEY 8d: 5 and 200)")
     ap.add_argument("--ssb-variant", default="reference", choices=["reference", "nco127"],
                     help="nco127: the BASELINE configs[2] variant (a build extension, not the reference chain): NCO "
                          "mixer at +250 kHz + 127-tap FIR (sdrg_engine_set_ssb_variant); a separately labelled line")
@@ -159,14 +166,22 @@ def main() -> int:
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    streams = args.streams
-    cfg = sdrg.SDRConfig(centerFrequency=CF, samplesPerReading=N, sampleRate=FS, freqFocusRangeKhz=5, soundMode=1)
+    c5 = args.config == "c5"
+    n = 65536 if c5 else N
+    fmt = sdrg.CS16 if c5 else sdrg.CS8
+    fmt_name = "CS16" if c5 else "CS8"
+    focus_khz = args.focus if c5 else 5
+    streams = (1024 if args.streams == B else args.streams) if c5 else args.streams
+    if args.stages is None:
+        args.stages = "all" if args.config == "c3" else "spectrum+stats"
+    cfg = sdrg.SDRConfig(centerFrequency=CF, samplesPerReading=n, sampleRate=FS, freqFocusRangeKhz=focus_khz,
+                         soundMode=1)
     eng = sdrg.Engine(cfg, streams, device=local)
     variant = args.ssb_variant != "reference"
     if variant:
         eng.set_ssb_variant(NCO_HZ, 127)
-    iq = synth_device_frames(torch, dev, streams, seed=0x5D12 + rank)
-    spec = torch.empty((streams, N), dtype=torch.float32, device=dev)
+    iq = synth_device_frames(torch, dev, streams, seed=0x5D12 + rank, n=n, cs16=c5)
+    spec = torch.empty((streams, n), dtype=torch.float32, device=dev)
     rec = torch.zeros((streams, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
     plen = eng.pcm_len
     pcm = torch.empty((streams, plen), dtype=torch.int16, device=dev)
@@ -181,7 +196,7 @@ def main() -> int:
     focus = "focus" in args.gather
     gather_pcm = "pcm" in args.gather
     p_out = torch.empty((world * streams, plen), dtype=torch.int16, device=dev) if gather_pcm and rank == 0 else None
-    f_lo, f_n = sdrg.focus_window(FS, N, 5)
+    f_lo, f_n = sdrg.focus_window(FS, n, focus_khz)
     f_stage = torch.empty((streams, f_n), dtype=torch.float32, device=dev) if focus else None
     f_out = torch.empty((world * streams, f_n), dtype=torch.float32, device=dev) if focus and rank == 0 else None
     if world > 1:
@@ -193,9 +208,8 @@ def main() -> int:
         eng.set_stream(work_stream.cuda_stream)
 
     def step():
-        eng.process_device(iq.data_ptr(), sdrg.CS8, stages, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(),
-                           now[0])
-        now[0] += 8  # 16384 samples @ 2 Msps = 8.192 ms per frame
+        eng.process_device(iq.data_ptr(), fmt, stages, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(), now[0])
+        now[0] += n // 2000  # frame duration in ms at 2 Msps (8 ms for 16384)
         if world > 1:
             shard.gather_records(rec, world, rank, dst=0, out=gathered)  # the one collective: records to rank 0
             if gather_pcm:
@@ -231,7 +245,7 @@ def main() -> int:
     eng.synchronize()
     eng.reset_timing_stats()
     for _ in range(10):
-        eng.process_device(iq.data_ptr(), sdrg.CS8, sdrg.STAGE_SPECTRUM, spec.data_ptr(), None, None, now[0])
+        eng.process_device(iq.data_ptr(), fmt, sdrg.STAGE_SPECTRUM, spec.data_ptr(), None, None, now[0])
     eng.synchronize()
     spec_iso_ms = eng.timing_stats()["spectrum_ms"]
     d2d = d2d_copy_gbs(torch, dev)
@@ -240,13 +254,23 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    samples = args.steps * streams * N * world
+    samples = args.steps * streams * n * world
     value = samples / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
     spec_ms = ts["spectrum_ms"]
-    alg_bytes = ALG_BYTES_PER_SAMPLE["spectrum"] * streams * N
+    alg_bytes = (8.0 if c5 else ALG_BYTES_PER_SAMPLE["spectrum"]) * streams * n  # CS16: 4 B in + 4 B out
     achieved = alg_bytes / (spec_ms * 1e-3) / 1e9 if spec_ms > 0 else 0.0
-    traffic = pmc_traffic("spectrum16k_kernel", streams)
+    kname = "four_step_a + four_step_b" if c5 else "spectrum16k_kernel"
+    traffic = pmc_traffic("spectrum16k_kernel", streams) if args.config == "c3" else None
+    workload = {
+        "c3": (f"C3: {streams} streams x {n}-pt CS8 frames @2 Msps per GPU; FFT + |X|^2 + fftshift "
+               "+ signal-strength stats + SSB (DC, LPF, AGC, 255-tap FIR decim 41, EQ, PCM) + spectral "
+               "and audio pulse detectors"),
+        "c2": (f"C2 (BASELINE configs[1]): {streams} streams x {n}-pt CS8 frames @2 Msps per GPU; FFT + |X|^2 + "
+               "fftshift + signal-strength stats (peak, log-magnitude statistics); no SSB"),
+        "c5": (f"C5 (BASELINE configs[4]): {streams} streams x {n}-pt CS16 frames @2 Msps per GPU; four-step FFT + "
+               f"|X|^2 + fftshift + signal-strength stats over a {focus_khz} kHz focus; no SSB"),
+    }[args.config]
     achieved_iso = alg_bytes / (spec_iso_ms * 1e-3) / 1e9 if spec_iso_ms > 0 else 0.0
     out = {
         "metric": "IQ Msamples/s (16384-pt FFT+SSB) at 1/2/4/8 GPUs; % HBM roofline",
@@ -259,21 +283,20 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32 (int8 CS8 in, int16 PCM out)",
-        "data": "synthetic CS8 CW tones + Gaussian noise, generated on device",
-        "config": {"workload": (f"C3: {streams} streams x {N}-pt CS8 frames @2 Msps per GPU; FFT + |X|^2 + fftshift "
-                                "+ signal-strength stats + SSB (DC, LPF, AGC, 255-tap FIR decim 41, EQ, PCM) + spectral "
-                                "and audio pulse detectors") if not variant else
+        "dtype": "f32 (int16 CS16 in)" if c5 else "f32 (int8 CS8 in, int16 PCM out)",
+        "data": f"synthetic {fmt_name} CW tones + Gaussian noise, generated on device",
+        "config": {"workload": workload if not variant else
                                (f"C3-variant (BASELINE configs[2], build extension, not the reference chain): {streams} "
-                                f"streams x {N}-pt CS8 frames @2 Msps per GPU; FFT + stats + SSB with NCO mixer "
+                                f"streams x {n}-pt CS8 frames @2 Msps per GPU; FFT + stats + SSB with NCO mixer "
                                 f"(+{NCO_HZ / 1e3:g} kHz) + 127-tap FIR decim 41 (397 PCM/frame) + pulse detectors"),
-                   "streams_per_gpu": streams, "samples_per_frame": N, "sample_rate": FS, "format": "CS8",
+                   "streams_per_gpu": streams, "samples_per_frame": n, "sample_rate": FS, "format": fmt_name,
+                   "focus_khz": focus_khz,
                    "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (
                        (", RCCL gather of records" + (" + PCM" if gather_pcm else "")
                         + (f" + {f_n}-bin focus spectra" if focus else ""))
                        if world > 1 else "")},
         "kernel_ms": {k: round(v, 4) for k, v in ts.items() if k != "count"},
-        "roofline": {"kernel": "spectrum16k_kernel (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
+        "roofline": {"kernel": f"{kname} (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic[0] if traffic else None,
@@ -282,7 +305,7 @@ def main() -> int:
                      "measured": ("HIP events on the kernel's stream over the timed region"
                                   + (", where each step's SSB pipeline shares the chip with the next step's spectrum"
                                      if pipelined else ""))},
-        "roofline_isolated": {"kernel": "spectrum16k_kernel", "bound": "hbm", "achieved": round(achieved_iso, 1),
+        "roofline_isolated": {"kernel": kname, "bound": "hbm", "achieved": round(achieved_iso, 1),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_iso / HBM_PEAK_GBS, 4),
                               "measured": "10 launches of the spectrum stage alone after the timed region"},
         "hbm_measured": {"d2d_copy_GBs": round(d2d, 1), "note": "device-to-device copy of 1 GiB, read + write bytes "
@@ -293,9 +316,12 @@ def main() -> int:
     }
     if variant:
         out["ssb_variant"] = {"nco_hz": NCO_HZ, "fir_taps": 127, "note": "not the reference's chain; no CPU baseline"}
-    if args.stages != "all":
+    if args.config != "c3":
+        out["labelled_config"] = args.config
+    elif args.stages != "all":
         out["ablation_stages"] = args.stages
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.stages == "all" and not variant:
+    if (rank == 0 and world == 1 and not args.no_cpu_baseline and args.stages == "all" and not variant
+            and args.config == "c3"):
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
         except Exception as exc:  # the baseline is informative; never fail the bench line on it

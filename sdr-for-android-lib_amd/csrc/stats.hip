@@ -63,6 +63,70 @@ __device__ __forceinline__ WinScan scan_window(const float *__restrict__ P, int 
     return r;
 }
 
+// The same sequential loops for up to 11 windows whose bins do not fit the LDS stage at once (e.g. N = 65536
+// with a 200 kHz focus: three windows of 13107 bins).  All 64 lanes copy the next chunk of every window
+// (plus the w bins before it, which the sliding scan subtracts) from HBM into LDS, coalesced; then lane j
+// runs window j's plain sum and lane 32 + j its best-1-kHz sliding scan over that chunk, the two sequential
+// chains of a window on two lanes, in the reference's element order.  Without the staging each dependent
+// step of those chains waited on an HBM load.  Lane j (j < nwin) returns window j's WinScan.
+__device__ WinScan scan_windows_chunked(const float *__restrict__ P, float *buf, int buf_floats, int nwin,
+                                        const int *wlo, const int *whi, int w) {
+    const int lane = threadIdx.x;
+    const int row = buf_floats / nwin;        // floats per window row: w history bins + SC new ones
+    const int SC = row - w;                   // > 0: checked by the caller
+    const int j = lane & 31;
+    const bool sum_lane = lane < nwin, scan_lane = lane >= 32 && j < nwin;
+    const int my_lo = (j < nwin) ? wlo[j] : 0, my_len = (j < nwin) ? whi[j] - wlo[j] + 1 : 0;
+    int max_len = 0;
+    for (int q = 0; q < nwin; q++) max_len = max(max_len, whi[q] - wlo[q] + 1);
+    float s = 0.0f, rs = 0.0f, bv = 0.0f;
+    int best_start = my_lo;
+    const float *mine = buf + j * row + w;  // mine[e - c0] = P[lo + e], e in [c0 - w, c0 + SC)
+    for (int c0 = 0; c0 < max_len; c0 += SC) {
+        for (int q = 0; q < nwin; q++) {
+            const int lo = wlo[q], len = whi[q] - wlo[q] + 1;
+            const int t0 = max(c0 - w, 0), t1 = min(c0 + SC, len);  // elements of window q this chunk needs
+#pragma unroll 16  // 16 loads in flight per lane: a rolled loop would wait out HBM latency per 256 B
+            for (int t = t0 + lane; t < t1; t += WAVE) buf[q * row + w + (t - c0)] = P[lo + t];
+        }
+        __syncthreads();
+        const int end = min(c0 + SC, my_len);
+        if (sum_lane) {
+#pragma unroll 8
+            for (int e = c0; e < end; e++) s += mine[e - c0];
+        } else if (scan_lane && my_len >= w) {
+            int e = c0;
+            for (; e < end && e < w; e++) {  // the first window's sum (:171-172)
+                rs += mine[e - c0];
+                if (e == w - 1) bv = rs;
+            }
+#pragma unroll 4
+            for (; e < end; e++) {  // slide: start st = lo + e - w + 1 (:173-178)
+                rs += mine[e - c0] - mine[e - c0 - w];
+                if (rs > bv) {
+                    bv = rs;
+                    best_start = my_lo + e - w + 1;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const float bv_scan = __shfl(bv, (lane & 31) + 32);
+    const int bs_scan = __shfl(best_start, (lane & 31) + 32);
+    WinScan r;
+    r.sum = s;
+    r.best_start = my_lo;
+    if (my_len <= 0) {
+        r.best1k = 0.0f;
+    } else if (my_len < w) {
+        r.best1k = s / my_len;
+    } else {
+        r.best1k = bv_scan / w;  // as scan_window: RN(max rs / w)
+        r.best_start = bs_scan;
+    }
+    return r;
+}
+
 __device__ __forceinline__ float fmax_ref(float a, float b) { return (a < b) ? b : a; }  // std::max
 
 // Ascending sort of 10 (key, index) pairs by (key, index): odd-even transposition network, registers only.
@@ -154,16 +218,18 @@ __device__ float kth_smallest(const float *vals, int cnt, int k, int *hist, int 
 __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ spectra, StatsGeometry g,
                                                      int64_t now_ms, StatsState *__restrict__ state,
                                                      sdrg_frame_record *__restrict__ records) {
-    extern __shared__ __attribute__((aligned(16))) float dyn[];  // [max_pool] pooled dB / gaps, then [span] staged bins
+    // one dynamic LDS area, used twice: first the staged bins of the window scans, then (after a barrier)
+    // the pooled dB values / gaps of the MAD median
+    extern __shared__ __attribute__((aligned(16))) float dyn[];
     float *pool = dyn;
-    float *stage = dyn + ((g.max_pool + 3) & ~3);
+    float *stage = dyn;
     __shared__ __attribute__((aligned(16))) int hist[256];
     __shared__ int sh_int[2];
     __shared__ int sh_nbottom, sh_best_start;
     __shared__ float w_mean_db[10], w_best1k_db[10];
     __shared__ int w_lo[10], w_hi[10], order[10];
     __shared__ float sh_f[4];
-    __shared__ int sh_geo_lo[10], sh_geo_hi[10];
+    __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
 
     const int lane = threadIdx.x;
     const size_t frame = blockIdx.x;
@@ -190,6 +256,7 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
         // ---- 6.2 focus peak: first maximum of dB, seeded at -130 (fft_process.cpp:142-154) ----
         float best = -130.0f;
         int bidx = 0x7fffffff;
+#pragma unroll 8  // loads in flight (13107-bin focus windows at N = 65536 / 200 kHz)
         for (int i = g.focus_lo + lane; i <= g.focus_hi; i += WAVE) {
             const float d = db_of(P[i]);
             if (d > best) {
@@ -220,11 +287,20 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
             for (int i = lane; i < g.span_len; i += WAVE) stage[i] = P[g.span_lo + i];
             __syncthreads();
         }
+        if (lane == 0) {
+            sh_geo_lo[n_ref] = g.focus_lo;
+            sh_geo_hi[n_ref] = g.focus_hi;
+        }
+        __syncthreads();
+        // windows too wide to stage together: chunked through the same LDS area (all lanes take part)
+        const bool chunked = !staged && STAGE_MAX / (n_ref + 1) - w1k >= 64;
+        WinScan wsc{};
+        if (chunked) wsc = scan_windows_chunked(P, stage, STAGE_MAX, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k);
         if (lane <= n_ref) {
             const bool is_focus = (lane == n_ref);
-            const int lo = is_focus ? g.focus_lo : sh_geo_lo[lane];
-            const int hi = is_focus ? g.focus_hi : sh_geo_hi[lane];
-            const WinScan ws = staged ? scan_window(stage - g.span_lo, lo, hi, w1k) : scan_window(P, lo, hi, w1k);
+            const int lo = sh_geo_lo[lane];
+            const int hi = sh_geo_hi[lane];
+            const WinScan ws = chunked ? wsc : staged ? scan_window(stage - g.span_lo, lo, hi, w1k) : scan_window(P, lo, hi, w1k);
             const int n = hi - lo + 1;
             if (is_focus) {
                 sh_f[0] = db_of(ws.sum / n);  // signalPowerDb (:155)
@@ -290,6 +366,7 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
             int cnt = 0;
             for (int j = 0; j < n_bottom; j++) {
                 const int lo = w_lo[order[j]], hi = w_hi[order[j]];
+#pragma unroll 8
                 for (int i = lo + lane; i <= hi; i += WAVE) {
                     const int q = cnt + (i - lo);
                     if (q < g.max_pool) pool[q] = db_of(P[i]);
@@ -429,8 +506,10 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
                         StatsState *state, sdrg_frame_record *records, hipStream_t stream) {
     if (n_frames <= 0) return hipSuccess;
     if (geo.max_pool > MAX_POOL) return hipErrorInvalidValue;
-    const int staged = (geo.span_len > 0 && geo.span_len <= STAGE_MAX) ? geo.span_len : 0;
-    const size_t lds = sizeof(float) * (size_t)(((geo.max_pool + 3) & ~3) + staged + 4);
+    // the stage area (the staged span, or STAGE_MAX floats for the chunked window scans), reused for the pool
+    const int staged = (geo.span_len > 0 && geo.span_len <= STAGE_MAX) ? geo.span_len : STAGE_MAX;
+    const int pool = (geo.max_pool + 3) & ~3;
+    const size_t lds = sizeof(float) * (size_t)((pool > staged ? pool : staged) + 4);
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(stats_kernel),
