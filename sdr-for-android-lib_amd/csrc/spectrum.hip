@@ -627,9 +627,13 @@ hipError_t launch_fmt(const void *iq, int fmt, int n_frames, const float *tabs, 
 // Each tile runs a Stockham FFT in LDS with 16 values per thread.  Frames go through in waves whose
 // intermediate Y (8 B/sample) stays inside the 256 MiB Infinity Cache between the two kernels.
 // ================================================================================================
-constexpr int TILE_T = 256;  // threads per tile workgroup
+#ifndef SDRG_TILE_A
+#define SDRG_TILE_A 512
+#endif
+constexpr int TILE_A = SDRG_TILE_A;  // threads per kernel-A tile: 32 columns = 128-B rows of CS16 input
+constexpr int TILE_B = 256;          // threads per kernel-B tile
 
-template <int L>
+template <int L, int TILE_T>
 struct TilePlan {
     static constexpr int C = 16 * TILE_T / L;  // columns (rows) per tile so that C*L = 16*T
     static constexpr int LP = L + 1;           // padded column length in LDS
@@ -637,11 +641,32 @@ struct TilePlan {
     static constexpr int RB = 16;
 };
 
+// Twiddles of the four-step kernels from two LDS tables: W_N^m = hi[m >> 8] * lo[m & 255], hi[a] = W_N^(256 a),
+// lo[b] = W_N^b (both copied from the full W_N table at kernel start).  Reading W_N^m straight from the
+// 512 KiB global table touched one cache line per lane per load (strided m), which bounded kernel A by L2
+// line traffic; the LDS product costs one complex multiply.  S: compile-time stride of m (m = i S); when S
+// is a multiple of 256 the lo factor is W^0 = 1 and one lookup suffices.
+template <int S>
+__device__ __forceinline__ f2 tw_lds(const f2 *t_hi, const f2 *t_lo, int i) {
+    if constexpr (S % 256 == 0) {
+        return t_hi[i * (S / 256)];
+    } else {
+        const int m = i * S;
+        return cmul_v(t_hi[m >> 8], t_lo[m & 255]);
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void load_tw_tables(const f2 *__restrict__ tw, f2 *t_hi, f2 *t_lo) {
+    for (int i = threadIdx.x; i < N / 256; i += blockDim.x) t_hi[i] = tw[256 * i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) t_lo[i] = tw[i];
+}
+
 // One Stockham pass over every column of an LDS tile [C][LP]; FIRST reads through load(c, e),
 // LAST writes through store(c, k, v).
-template <int N, int L, int R, int NS, bool FIRST, bool LAST, class Load, class Store>
-__device__ __forceinline__ void tile_pass(f2 *lds, const f2 *__restrict__ tw, Load load, Store store) {
-    using TP = TilePlan<L>;
+template <int N, int L, int R, int NS, bool FIRST, bool LAST, int TILE_T, class Load, class Store>
+__device__ __forceinline__ void tile_pass(f2 *lds, const f2 *t_hi, const f2 *t_lo, Load load, Store store) {
+    using TP = TilePlan<L, TILE_T>;
     constexpr int C = TP::C;
     constexpr int NB = (C * L / R) / TILE_T;
     static_assert(NB >= 1, "tile too small for radix");
@@ -666,7 +691,7 @@ __device__ __forceinline__ void tile_pass(f2 *lds, const f2 *__restrict__ tw, Lo
         if constexpr (NS > 1) {
             const int k = j & (NS - 1);
 #pragma unroll
-            for (int r = 1; r < R; ++r) x[b][r] = cmul_v(x[b][r], tw[(r * k) * (N / (NS * R))]);
+            for (int r = 1; r < R; ++r) x[b][r] = cmul_v(x[b][r], tw_lds<N / (NS * R)>(t_hi, t_lo, r * k));
         }
         dft<R>(x[b]);
         if constexpr (LAST) {
@@ -682,11 +707,14 @@ __device__ __forceinline__ void tile_pass(f2 *lds, const f2 *__restrict__ tw, Lo
 }
 
 template <int LOG2N1, int LOG2N2, int FMT>
-__global__ __launch_bounds__(TILE_T) void four_step_a(const void *__restrict__ iq, f2 *__restrict__ Y,
+__global__ __launch_bounds__(TILE_A) void four_step_a(const void *__restrict__ iq, f2 *__restrict__ Y,
                                                        const f2 *__restrict__ tw) {
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
-    using TP = TilePlan<N1>;
+    using TP = TilePlan<N1, TILE_A>;
     __shared__ __attribute__((aligned(16))) f2 lds[TP::C * TP::LP];
+    __shared__ f2 t_hi[N / 256], t_lo[256];
+    load_tw_tables<N>(tw, t_hi, t_lo);
+    __syncthreads();
     const size_t frame = blockIdx.y;
     const int c0 = blockIdx.x * TP::C;
     const void *src = reinterpret_cast<const char *>(iq) + frame * (size_t)N * bytes_per_sample<FMT>();
@@ -695,27 +723,29 @@ __global__ __launch_bounds__(TILE_T) void four_step_a(const void *__restrict__ i
     auto none = [](int, int, f2) {};
     auto store = [&](int c, int k1, f2 v) {
         const int n2 = c0 + c;
-        y[k1 * N2 + n2] = cmul_v(v, tw[(n2 * k1) & (N - 1)]);
+        y[k1 * N2 + n2] = cmul_v(v, tw_lds<1>(t_hi, t_lo, (n2 * k1) & (N - 1)));
     };
     auto noload = [](int, int) { return f2{0.0f, 0.0f}; };
-    tile_pass<N, N1, TP::RA, 1, true, false>(lds, tw, load, none);
-    tile_pass<N, N1, TP::RB, TP::RA, false, true>(lds, tw, noload, store);
+    tile_pass<N, N1, TP::RA, 1, true, false, TILE_A>(lds, t_hi, t_lo, load, none);
+    tile_pass<N, N1, TP::RB, TP::RA, false, true, TILE_A>(lds, t_hi, t_lo, noload, store);
 }
 
 template <int LOG2N1, int LOG2N2>
-__global__ __launch_bounds__(TILE_T) void four_step_b(const f2 *__restrict__ Y, float *__restrict__ spectra,
+__global__ __launch_bounds__(TILE_B) void four_step_b(const f2 *__restrict__ Y, float *__restrict__ spectra,
                                                        const f2 *__restrict__ tw) {
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
-    using TP = TilePlan<N2>;
+    using TP = TilePlan<N2, TILE_B>;
     __shared__ __attribute__((aligned(16))) f2 lds[TP::C * TP::LP];
+    __shared__ f2 t_hi[N / 256], t_lo[256];
+    load_tw_tables<N>(tw, t_hi, t_lo);  // visible after the staging barrier below
     const size_t frame = blockIdx.y;
     const int r0 = blockIdx.x * TP::C;
     const f2 *y = Y + frame * (size_t)N + (size_t)r0 * N2;
     float *out = spectra + frame * (size_t)N;
     // stage the C rows coalesced
 #pragma unroll
-    for (int i = 0; i < TP::C * N2 / TILE_T; ++i) {
-        const int e = threadIdx.x + i * TILE_T;
+    for (int i = 0; i < TP::C * N2 / TILE_B; ++i) {
+        const int e = threadIdx.x + i * TILE_B;
         lds[(e / N2) * TP::LP + (e % N2)] = y[e];
     }
     __syncthreads();
@@ -725,8 +755,8 @@ __global__ __launch_bounds__(TILE_T) void four_step_b(const f2 *__restrict__ Y, 
         const int k = r0 + rho + N1 * k2;
         out[(k + N / 2) & (N - 1)] = v.x * v.x + v.y * v.y;
     };
-    tile_pass<N, N2, TP::RA, 1, false, false>(lds, tw, noload, none);
-    tile_pass<N, N2, TP::RB, TP::RA, false, true>(lds, tw, noload, store);
+    tile_pass<N, N2, TP::RA, 1, false, false, TILE_B>(lds, t_hi, t_lo, noload, none);
+    tile_pass<N, N2, TP::RB, TP::RA, false, true, TILE_B>(lds, t_hi, t_lo, noload, store);
 }
 
 template <int LOG2N1, int LOG2N2, int FMT>
@@ -738,9 +768,9 @@ hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, floa
     for (int f0 = 0; f0 < n_frames; f0 += wave) {
         const int nf = (n_frames - f0) < wave ? (n_frames - f0) : wave;
         const char *src = reinterpret_cast<const char *>(iq) + (size_t)f0 * N * bytes_per_sample<FMT>();
-        hipLaunchKernelGGL((four_step_a<LOG2N1, LOG2N2, FMT>), dim3(N2 / TilePlan<N1>::C, nf), dim3(TILE_T), 0, s,
-                           src, Y, tw);
-        hipLaunchKernelGGL((four_step_b<LOG2N1, LOG2N2>), dim3(N1 / TilePlan<N2>::C, nf), dim3(TILE_T), 0, s, Y,
+        hipLaunchKernelGGL((four_step_a<LOG2N1, LOG2N2, FMT>), dim3(N2 / TilePlan<N1, TILE_A>::C, nf), dim3(TILE_A), 0,
+                           s, src, Y, tw);
+        hipLaunchKernelGGL((four_step_b<LOG2N1, LOG2N2>), dim3(N1 / TilePlan<N2, TILE_B>::C, nf), dim3(TILE_B), 0, s, Y,
                            spectra + (size_t)f0 * N, tw);
     }
     return hipGetLastError();
