@@ -150,6 +150,9 @@ def main() -> int:
                     help="N > 1: what each step gathers to rank 0 over RCCL: the 72-B frame records (peak indices and "
                          "statistics) and, by default, each frame's focus-window spectrum slice (sdrg.shard.gather_focus; "
                          "BASELINE configs[3] gathers spectra + peak indices), optionally each frame's PCM (SURVEY 8e)")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, gloo backend, the gathers "
+                         "staged through host memory (not a measurement)")
     args = ap.parse_args()
 
     import torch
@@ -160,7 +163,11 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    rehearse = args.rehearse_gloo and world > 1
+    if rehearse:
+        local = 0
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -192,13 +199,16 @@ def main() -> int:
     stages = {"all": sdrg.STAGE_ALL, "hot": sdrg.STAGE_HOT_PATH, "spectrum": sdrg.STAGE_SPECTRUM, "ssb": sdrg.STAGE_SSB,
               "spectrum+stats": sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS}[args.stages]
 
-    gathered = torch.empty((world * streams, rec.shape[1]), dtype=torch.uint8, device=dev) if rank == 0 else None
+    gdev = torch.device("cpu") if rehearse else dev  # gloo gathers host tensors
+    gathered = torch.empty((world * streams, rec.shape[1]), dtype=torch.uint8, device=gdev) if rank == 0 else None
     focus = "focus" in args.gather
     gather_pcm = "pcm" in args.gather
-    p_out = torch.empty((world * streams, plen), dtype=torch.int16, device=dev) if gather_pcm and rank == 0 else None
+    # PCM travels as bytes: neither RCCL nor gloo has a 16-bit integer type
+    p_out = torch.empty((world * streams, 2 * plen), dtype=torch.uint8, device=gdev) if gather_pcm and rank == 0 else None
     f_lo, f_n = sdrg.focus_window(FS, n, focus_khz)
     f_stage = torch.empty((streams, f_n), dtype=torch.float32, device=dev) if focus else None
-    f_out = torch.empty((world * streams, f_n), dtype=torch.float32, device=dev) if focus and rank == 0 else None
+    f_out = torch.empty((world * streams, f_n), dtype=torch.float32, device=gdev) if focus and rank == 0 else None
+    host = (lambda t: t.cpu()) if rehearse else (lambda t: t)
     if world > 1:
         # the engine enqueues on a torch stream that is current for the collectives too, so the RCCL gather is
         # ordered after each step on the GPU without a host synchronisation, and the next step's kernels
@@ -211,11 +221,15 @@ def main() -> int:
         eng.process_device(iq.data_ptr(), fmt, stages, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(), now[0])
         now[0] += n // 2000  # frame duration in ms at 2 Msps (8 ms for 16384)
         if world > 1:
-            shard.gather_records(rec, world, rank, dst=0, out=gathered)  # the one collective: records to rank 0
+            shard.gather_records(host(rec), world, rank, dst=0, out=gathered)  # records (peaks, stats) to rank 0
             if gather_pcm:
-                shard.gather_records(pcm, world, rank, dst=0, out=p_out)
+                shard.gather_records(host(pcm.view(torch.uint8)), world, rank, dst=0, out=p_out)
             if focus:
-                shard.gather_focus(spec, f_lo, f_n, world, rank, dst=0, out=f_out, staging=f_stage)
+                if rehearse:
+                    f_stage.copy_(spec[:, f_lo:f_lo + f_n])
+                    shard.gather_records(f_stage.cpu(), world, rank, dst=0, out=f_out)
+                else:
+                    shard.gather_focus(spec, f_lo, f_n, world, rank, dst=0, out=f_out, staging=f_stage)
 
     # a pipelined call leaves its SSB stream running past the call, so a per-step PCM gather needs the joined schedule
     pipelined = bool(args.pipelined) and not (gather_pcm and world > 1)
@@ -250,7 +264,7 @@ def main() -> int:
     spec_iso_ms = eng.timing_stats()["spectrum_ms"]
     d2d = d2d_copy_gbs(torch, dev)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -314,6 +328,8 @@ def main() -> int:
                          "frac_isolated": round(achieved_iso / d2d, 4) if d2d else None},
         "pipelined": pipelined,
     }
+    if rehearse:
+        out["rehearsal"] = "gloo, every rank on cuda:0: a functional check of the N > 1 path, not a measurement"
     if variant:
         out["ssb_variant"] = {"nco_hz": NCO_HZ, "fir_taps": 127, "note": "not the reference's chain; no CPU baseline"}
     if args.config != "c3":
