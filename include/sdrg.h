@@ -274,6 +274,12 @@ int32_t sdrg_focus_window(int64_t sample_rate, int32_t n, int32_t focus_khz, int
 int32_t sdrg_ssb_design(int32_t samp_count, int64_t sample_rate, int32_t sound_mode, float *lpf, float *hp,
                         float *bp, float *taps, int32_t *n_taps);
 
+/* Page-locked host memory (hipHostMalloc) for sdrg_engine_process_host's buffers: copies to and from it run at
+ * the PCIe rate, while pageable buffers go through the runtime's staging.  The memory
+ * stays valid until sdrg_host_free; any engine may use it. */
+int32_t sdrg_host_alloc(size_t bytes, void **out);
+int32_t sdrg_host_free(void *p);
+
 /* Create an engine for n_streams independent receivers on HIP device `device`.
  * Replaces FFTProcessor() + configure() (fft_process.cpp:8-39) and BridgeConfig::initialize
  * (bridge-config.h:17-38) for each stream. */

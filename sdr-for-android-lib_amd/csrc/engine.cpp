@@ -65,6 +65,39 @@ struct SsbControl {
     int taps_decim = -1, taps_req = -1, n_taps = 0;
 };
 
+// Page-locked host array (hipHostMalloc) for the host path's engine-owned copies: device-to-host copies into
+// pageable memory go through the runtime's staging at a fraction of the PCIe rate.
+template <class T>
+struct PinnedVec {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    PinnedVec() = default;
+    PinnedVec(const PinnedVec &) = delete;
+    PinnedVec &operator=(const PinnedVec &) = delete;
+    ~PinnedVec() {
+        if (p) (void)hipHostFree(p);
+    }
+    bool resize(size_t k) {  // contents are not preserved on growth (every use refills the array)
+        if (k > cap) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = n = 0;
+            if (hipHostMalloc(reinterpret_cast<void **>(&p), sizeof(T) * k, hipHostMallocDefault) != hipSuccess) {
+                p = nullptr;
+                return false;
+            }
+            cap = k;
+        }
+        n = k;
+        return true;
+    }
+    void assign(const T *a, const T *b) {
+        if (resize((size_t)(b - a))) memcpy(p, a, sizeof(T) * (size_t)(b - a));
+    }
+    T *data() { return p; }
+    T &operator[](size_t i) { return p[i]; }
+};
+
 struct EvSet {
     hipEvent_t t0 = nullptr, spec = nullptr, stats = nullptr, ssb0 = nullptr, ssb1 = nullptr, end = nullptr;
     bool has_spec = false, has_stats = false, has_ssb = false, pending = false;
@@ -112,16 +145,16 @@ struct sdrg_engine {
     sdrg_frame_record *d_rec_stage = nullptr;
     int16_t *d_pcm_stage = nullptr;
     size_t pcm_stage_elems = 0;
-    std::vector<float> h_spec;
-    std::vector<sdrg_frame_record> h_rec;
-    std::vector<int16_t> h_pcm;
+    PinnedVec<float> h_spec;
+    PinnedVec<sdrg_frame_record> h_rec;
+    PinnedVec<int16_t> h_pcm;
 
     SsbControl ssb;
     // pulse detectors (created at the first call that runs their stage)
     sdrg_pulse_config spec_pulse_cfg{}, audio_pulse_cfg{};
     sdrg_pulse_bank spec_bank, audio_bank;
     bool spec_bank_live = false, audio_bank_live = false;
-    std::vector<sdrg_pulse_output> h_pspec, h_paudio;
+    PinnedVec<sdrg_pulse_output> h_pspec, h_paudio;
     bool cf_changed_pending = false;
     bool pipelined = false;  // sdrg_engine_set_pipelining: no join of the SSB stream per call
     // NCO/short-FIR SSB variant (sdrg_engine_set_ssb_variant; a build extension, off by default)
@@ -514,6 +547,22 @@ int32_t sdrg_ssb_pcm_len(int32_t n, int64_t sample_rate) {
     return ssb_pcm_len(n, (uint32_t)sample_rate);
 }
 
+int32_t sdrg_host_alloc(size_t bytes, void **out) {
+    if (!out) return fail(SDRG_E_INVALID, "null out");
+    *out = nullptr;
+    if (bytes == 0) return fail(SDRG_E_INVALID, "zero-byte host allocation");
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return fail(SDRG_E_HIP, "hipHostMalloc of %zu bytes failed", bytes);
+    }
+    return SDRG_OK;
+}
+
+int32_t sdrg_host_free(void *p) {
+    if (p) HIP_TRY(hipHostFree(p));
+    return SDRG_OK;
+}
+
 int32_t sdrg_focus_window(int64_t sample_rate, int32_t n, int32_t focus_khz, int32_t *first_bin, int32_t *n_bins) {
     if (!first_bin || !n_bins) return fail(SDRG_E_INVALID, "null output");
     if (n <= 0 || (uint32_t)sample_rate == 0 || focus_khz < 0) return fail(SDRG_E_INVALID, "bad geometry arguments");
@@ -823,9 +872,14 @@ int32_t sdrg_engine_process_host(sdrg_engine *e, const void *iq, int32_t format,
     sdrg_frame_record *h_rec = records;
     int16_t *h_pcm = pcm;
     if (want_cb) {
-        if (do_spec && !h_spec) { e->h_spec.resize((size_t)B * n); h_spec = e->h_spec.data(); }
-        if (do_stats && !h_rec) { e->h_rec.resize(B); h_rec = e->h_rec.data(); }
-        if (do_ssb && !h_pcm) { e->h_pcm.resize((size_t)B * std::max(pcm_len, 1)); h_pcm = e->h_pcm.data(); }
+        if ((do_spec && !e->h_spec.resize((size_t)B * n)) || (do_stats && !e->h_rec.resize(B)) ||
+            (do_ssb && !e->h_pcm.resize((size_t)B * std::max(pcm_len, 1))) ||
+            ((stages & SDRG_STAGE_SPECTRAL_PULSE) && !e->h_pspec.resize(B)) ||
+            ((stages & SDRG_STAGE_AUDIO_PULSE) && !e->h_paudio.resize(B)))
+            return fail(SDRG_E_HIP, "hipHostMalloc failed for the callback copies");
+        if (do_spec && !h_spec) h_spec = e->h_spec.data();
+        if (do_stats && !h_rec) h_rec = e->h_rec.data();
+        if (do_ssb && !h_pcm) h_pcm = e->h_pcm.data();
     }
     if (do_spec && h_spec)
         HIP_TRY(hipMemcpyAsync(h_spec, e->d_spec_stage, sizeof(float) * (size_t)B * n, hipMemcpyDeviceToHost, e->s_main));
@@ -836,12 +890,10 @@ int32_t sdrg_engine_process_host(sdrg_engine *e, const void *iq, int32_t format,
         HIP_TRY(hipMemcpyAsync(h_pcm, e->d_pcm_stage, sizeof(int16_t) * (size_t)B * pcm_len, hipMemcpyDeviceToHost,
                                e->s_main));
     if (want_cb && (stages & SDRG_STAGE_SPECTRAL_PULSE)) {
-        e->h_pspec.resize(B);
         HIP_TRY(hipMemcpyAsync(e->h_pspec.data(), e->spec_bank.d_out, sizeof(sdrg_pulse_output) * (size_t)B,
                                hipMemcpyDeviceToHost, e->s_main));
     }
     if (want_cb && (stages & SDRG_STAGE_AUDIO_PULSE)) {
-        e->h_paudio.resize(B);
         HIP_TRY(hipMemcpyAsync(e->h_paudio.data(), e->audio_bank.d_out, sizeof(sdrg_pulse_output) * (size_t)B,
                                hipMemcpyDeviceToHost, e->s_main));
     }

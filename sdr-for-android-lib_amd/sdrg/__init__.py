@@ -76,7 +76,7 @@ PULSE_OUTPUT_DTYPE = np.dtype(
 
 # Every entry point include/sdrg.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "sdrg_abi_version", "sdrg_last_error", "sdrg_ssb_pcm_len", "sdrg_focus_window", "sdrg_ssb_design", "sdrg_engine_create", "sdrg_engine_destroy",
+    "sdrg_abi_version", "sdrg_last_error", "sdrg_ssb_pcm_len", "sdrg_focus_window", "sdrg_host_alloc", "sdrg_host_free", "sdrg_ssb_design", "sdrg_engine_create", "sdrg_engine_destroy",
     "sdrg_engine_apply_config", "sdrg_engine_set_frequency", "sdrg_engine_set_frequency_focus_range",
     "sdrg_engine_set_sound_mode", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
     "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_set_stream",
@@ -204,6 +204,8 @@ def load() -> ctypes.CDLL:
         "sdrg_engine_set_pipelining": (_I32, [P, _I32]),
         "sdrg_engine_set_ssb_variant": (_I32, [P, ctypes.c_double, _I32]),
         "sdrg_focus_window": (_I32, [_I64, _I32, _I32, P, P]),
+        "sdrg_host_alloc": (_I32, [ctypes.c_size_t, P]),
+        "sdrg_host_free": (_I32, [P]),
         "sdrg_engine_get_ssb_variant": (_I32, [P, P, P, P, P]),
         "sdrg_engine_process_host": (_I32, [P, P, _I32, _I32, P, P, P, _I64]),
         "sdrg_engine_set_callbacks": (_I32, [P, ctypes.POINTER(_Callbacks)]),
@@ -252,6 +254,32 @@ def _check(rc: int, what: str) -> None:
 
 def ssb_pcm_len(n: int, sample_rate: int) -> int:
     return int(load().sdrg_ssb_pcm_len(n, sample_rate))
+
+
+class HostBuffer:
+    """Page-locked host memory (sdrg_host_alloc) viewed as a numpy array, for Engine.process outputs and inputs
+    at the full PCIe rate.  Freed by close() or when garbage-collected."""
+
+    def __init__(self, shape, dtype):
+        self.dtype = np.dtype(dtype)
+        nbytes = int(np.prod(shape)) * self.dtype.itemsize
+        p = ctypes.c_void_p()
+        _check(load().sdrg_host_alloc(max(nbytes, 1), ctypes.byref(p)), "sdrg_host_alloc")
+        self._p = p
+        buf = (ctypes.c_char * max(nbytes, 1)).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=self.dtype, count=int(np.prod(shape))).reshape(shape)
+
+    def close(self) -> None:
+        if getattr(self, "_p", None) is not None and self._p.value:
+            self.array = None
+            load().sdrg_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def focus_window(sample_rate: int, n: int, focus_khz: int) -> tuple[int, int]:
@@ -389,16 +417,29 @@ class Engine:
         _check(load().sdrg_engine_pulse_outputs(self._h, ctypes.byref(a), ctypes.byref(b)), "pulse_outputs")
         return a.value, b.value
 
-    def process(self, iq: np.ndarray, fmt: int = CS8, stages: int = STAGE_ALL, now_ms: int = 0):
-        """Host path: iq is [n_streams][samplesPerReading * 2] raw samples. Returns (spectra, records, pcm)."""
+    def process(self, iq: np.ndarray, fmt: int = CS8, stages: int = STAGE_ALL, now_ms: int = 0, out=None):
+        """Host path: iq is [n_streams][samplesPerReading * 2] raw samples. Returns (spectra, records, pcm).
+
+        out: optional (spectra, records, pcm) arrays to write into (e.g. HostBuffer arrays, page-locked, for the
+        full PCIe rate); entries for stages not run may be None.  By default fresh arrays are allocated."""
         n = self.cfg.samplesPerReading
         iq = np.ascontiguousarray(iq, dtype=NUMPY_DTYPE[fmt])
         if iq.size != self.n_streams * n * 2:
             raise SdrgError(f"iq has {iq.size} values, expected {self.n_streams}x{n}x2")
-        spec = np.empty((self.n_streams, n), np.float32) if stages & STAGE_SPECTRUM else None
-        recs = np.zeros(self.n_streams, RECORD_DTYPE) if stages & STAGE_STATS else None
         plen = self.pcm_len
-        pcm = np.empty((self.n_streams, max(plen, 0)), np.int16) if stages & STAGE_SSB else None
+        if out is not None:
+            spec, recs, pcm = out
+            for a, shape, dt in ((spec, (self.n_streams, n), np.float32), (recs, (self.n_streams,), RECORD_DTYPE),
+                                 (pcm, (self.n_streams, max(plen, 0)), np.int16)):
+                if a is not None and (a.shape != shape or a.dtype != dt or not a.flags.c_contiguous):
+                    raise SdrgError(f"out array {a.shape} {a.dtype}: expected contiguous {shape} {np.dtype(dt)}")
+            if (stages & STAGE_SPECTRUM and spec is None) or (stages & STAGE_STATS and recs is None) or \
+                    (stages & STAGE_SSB and pcm is None):
+                raise SdrgError("out lacks an array for a requested stage")
+        else:
+            spec = np.empty((self.n_streams, n), np.float32) if stages & STAGE_SPECTRUM else None
+            recs = np.zeros(self.n_streams, RECORD_DTYPE) if stages & STAGE_STATS else None
+            pcm = np.empty((self.n_streams, max(plen, 0)), np.int16) if stages & STAGE_SSB else None
         ptr = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
         _check(load().sdrg_engine_process_host(self._h, ptr(iq), fmt, stages, ptr(spec), ptr(recs),
                                                ptr(pcm) if (pcm is not None and plen > 0) else None, now_ms),

@@ -69,3 +69,26 @@ def test_degenerate_frames(S, O, fmt_name):
     frames = [zero, dc, nyq, zero]
     raw = np.stack([np.stack([frames[b], frames[(b + 1) % 4]]) for b in range(4)])  # [4][2 calls][2N]
     _check_calls(S, O, raw, fmt, N, FS)
+
+
+def test_page_locked_host_buffers(S, O):
+    """process(out=...) into sdrg.HostBuffer arrays (sdrg_host_alloc, page-locked) gives the same bytes as the
+    default pageable arrays, with the input also page-locked."""
+    B, n = 8, 4096
+    raw = np.stack([O.synth_frames(1, n, O.CS8, tone_hz=700.0 * b - 2000.0, fs=FS, seed=90 + b)[0] for b in range(B)])
+    e1, e2 = engine(S, n, FS, B), engine(S, n, FS, B)
+    hb = [S.HostBuffer((B, 2 * n), np.int8), S.HostBuffer((B, n), np.float32), S.HostBuffer((B,), S.RECORD_DTYPE),
+          S.HostBuffer((B, e2.pcm_len), np.int16)]
+    hb[0].array[...] = raw
+    for k in range(2):
+        a = e1.process(raw, fmt=O.CS8, now_ms=1000 + 8 * k)
+        b = e2.process(hb[0].array, fmt=O.CS8, now_ms=1000 + 8 * k, out=(hb[1].array, hb[2].array, hb[3].array))
+        assert a[0].tobytes() == b[0].tobytes() and a[2].tobytes() == b[2].tobytes()
+        for f in S.RECORD_DTYPE.names:  # fields: the struct's padding bytes are unspecified
+            assert a[1][f].tobytes() == b[1][f].tobytes(), f
+    with pytest.raises(S.SdrgError):
+        e2.process(raw, fmt=O.CS8, out=(hb[1].array, None, hb[3].array))  # STATS requested, no records array
+    for h in hb:
+        h.close()
+    e1.close()
+    e2.close()
