@@ -303,7 +303,7 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 // go to the EQ role (HP, BP, boost, PCM).  All arithmetic is the reference's, in its order, without
 // contraction: bit-identical PCM.
 //
-// Workgroup = 16 streams x 12 waves, one workgroup per CU (LDS padded past half the CU).  A wave issues
+// Workgroup = 16 streams x 12 waves, one workgroup per CU (84.5 KiB of LDS: two never fit), beside one spectrum workgroup.  A wave issues
 // at most about one VALU instruction per ~10 cycles however idle its SIMD is, while a SIMD serves several
 // waves at that rate (tools/microbench/valu2.hip), so the order-free work is spread over as many waves as
 // keep the heaviest helper's instruction count below the low-pass wave's.  The roles are dealt to the
@@ -343,7 +343,21 @@ constexpr int batch_chunks() {  // chunks per 512-B-per-stream prefetch batch (D
     constexpr int b = 512 / (CH * (FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2));
     return b > 0 ? b : 1;
 }
-constexpr int NRAW = 3;  // raw-IQ batches in LDS: one being unpacked, two in flight
+#ifndef SDRG_PIPE_NRAW  // 2: one batch unpacked, one in flight (3 needs 8 KiB more LDS than co-residency allows)
+#define SDRG_PIPE_NRAW 2
+#endif
+// Co-residency with the spectrum kernel (measured +4-5 % per step, tools/gpu_cores.sh): the pipeline keeps to
+// 80 VGPRs (6 waves per SIMD's worth; 3 x 80 + 2 x 128 <= 512) and 84.5 KiB of LDS (+ 74.3 KiB <= 160 KiB), so
+// one 512-thread spectrum workgroup fits beside it on every CU and the next call's spectrum runs while this
+// call's latency-bound SSB pipeline holds the CUs.  The LDS is dynamic so that the compiler's occupancy model
+// (which otherwise clamps waves-per-EU to what the static LDS allows) honours the 80-VGPR budget.
+#ifndef SDRG_PIPE_DYN_LDS
+#define SDRG_PIPE_DYN_LDS 1
+#endif
+#ifndef SDRG_PIPE_MINW  // waves per SIMD the VGPR budget must allow: 6 -> at most 80 VGPRs
+#define SDRG_PIPE_MINW 6
+#endif
+constexpr int NRAW = SDRG_PIPE_NRAW;  // raw-IQ batches in LDS: one being unpacked, NRAW - 1 in flight
 
 struct PipeLds {
     uint4 raw[NRAW][RAW_U4];  // raw IQ bytes of the prefetch batches (LDS-DMA), [piece][loader lane]
@@ -387,7 +401,10 @@ __device__ __forceinline__ void load_i8_masked(const char *frame, int t, int n_i
 // sub-block i + 1 is read from LDS while sub-block i runs through the recurrence, so the LDS latency is off
 // the recurrence's critical path.  step(v) updates the role's carried state and v in place; the results go
 // to dst when store (lanes that hold a stream's first copy).
-constexpr int SB = 32;
+#ifndef SDRG_PIPE_SB  // 16: two 16-float register sub-blocks fit the 80-VGPR budget without spills (32 spills)
+#define SDRG_PIPE_SB 16
+#endif
+constexpr int SB = SDRG_PIPE_SB;
 template <class Step>
 __device__ __forceinline__ void row_pipeline(const float *src, float *dst, bool store, Step step) {
     constexpr int NSB = CH / SB;
@@ -469,15 +486,21 @@ __device__ __forceinline__ void fir_chunk(PipeLds &L, int c, int t0, int o_lo, i
 }
 
 template <int FMT, bool DMA>
-__global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
+__global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_waves_per_eu(SDRG_PIPE_MINW))) void ssb_pipe_kernel(const char *__restrict__ iq, int n_frames, SsbParams p,
                                                           int nsl_mask, const int4 *__restrict__ chunk_out,
                                                           const float *__restrict__ taps,
                                                           SsbStreamState *__restrict__ state,
                                                           int16_t *__restrict__ pcm,
                                                           unsigned long long *__restrict__ stamps, int prio_mask,
                                                           int skip_mask, unsigned long long role_map, AudioFront af) {
+#if SDRG_PIPE_DYN_LDS  // the whole LDS dynamic: the compiler's occupancy model then sees no LDS limit
+    extern __shared__ __attribute__((aligned(16))) char pipe_dyn[];
+    PipeLds &L = *reinterpret_cast<PipeLds *>(pipe_dyn);
+    float *nco_lds = reinterpret_cast<float *>(pipe_dyn + sizeof(PipeLds));
+#else
     __shared__ PipeLds L;
     extern __shared__ __attribute__((aligned(16))) float nco_lds[];  // NCO_LDS_BYTES when p.nco_on
+#endif
     const int tid = threadIdx.x;
     const int hw_wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // runs on SIMD hw_wave % 4
     const int wave = (int)((role_map >> (4 * hw_wave)) & 15);     // the role it plays (PipeWave)
@@ -521,8 +544,8 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
     };
     if constexpr (DMA) {
         if (wave == W_LOAD && n_batches > 0) issue_batch(0);
-        if (wave == W_LOAD && n_batches > 1) issue_batch(1);
-        if (n_batches > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // batch 0 landed, 1 in flight
+        if (NRAW > 2 && wave == W_LOAD && n_batches > 1) issue_batch(1);
+        if (NRAW > 2 && n_batches > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // batch 0 landed, 1 in flight
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
@@ -649,9 +672,11 @@ __global__ __launch_bounds__(PIPE_T) void ssb_pipe_kernel(const char *__restrict
                 // iteration: wait until at most batch kb + 2's 8 DMAs are outstanding (only this wave's
                 // DMAs are counted by its vmcnt)
                 const int kb = it / BC;
-                if (it % BC == 0 && kb + 2 < n_batches) issue_batch(kb + 2);
+                // batch kb + NRAW - 1 goes into the slot batch kb - 1 left; batch kb + 1 must have landed by
+                // the end of batch kb
+                if (it % BC == 0 && kb + NRAW - 1 < n_batches) issue_batch(kb + NRAW - 1);
                 if (it % BC == BC - 1) {
-                    if (kb + 2 < n_batches) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    if (NRAW > 2 && kb + 2 < n_batches) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
                     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
             }
@@ -952,6 +977,21 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         const dim3 grid((n_frames + PG - 1) / PG);
         size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
         if (p.nco_on && pad < (size_t)NCO_LDS_BYTES) pad = NCO_LDS_BYTES;  // the dynamic part holds the NCO tables
+#if SDRG_PIPE_DYN_LDS
+        pad = sizeof(PipeLds) + (p.nco_on ? NCO_LDS_BYTES : 0);
+        static bool attr_done = false;
+        if (!attr_done) {
+#define SDRG_PIPE_ATTR_SET(F)                                                                                          \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(ssb_pipe_kernel<F, true>),                                  \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(PipeLds) + NCO_LDS_BYTES));     \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(ssb_pipe_kernel<F, false>),                                 \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(PipeLds) + NCO_LDS_BYTES));
+            SDRG_PIPE_ATTR_SET(SDRG_IQ_CS8) SDRG_PIPE_ATTR_SET(SDRG_IQ_CU8) SDRG_PIPE_ATTR_SET(SDRG_IQ_CS16)
+            SDRG_PIPE_ATTR_SET(SDRG_IQ_CF32)
+#undef SDRG_PIPE_ATTR_SET
+            attr_done = true;
+        }
+#endif
         const int bps = fmt == SDRG_IQ_CF32 ? 8 : fmt == SDRG_IQ_CS16 ? 4 : 2;
         const int bc = 512 / (CH * bps) > 0 ? 512 / (CH * bps) : 1;  // batch_chunks<FMT>()
         const int n_live = p.n_in < p.samp_count ? p.n_in : p.samp_count;
