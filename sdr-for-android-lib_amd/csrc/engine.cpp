@@ -459,7 +459,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
     }
     if (do_spec) {
-        HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, e->s_main));
+        HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, e->s_main, do_ssb && early_fork));
         if (prof) HIP_TRY(hipEventRecord(ev->spec, e->s_main));
     }
     if (do_ssb) {  // fork

@@ -21,8 +21,11 @@ size_t spectrum_scratch_floats(int n, int n_frames);
 size_t spectrum_twiddle_floats(int n);
 void spectrum_fill_twiddles(int n, float *out);
 // twiddles: exp(-2 pi i m / N), m in [0, N), float2, computed in double on the host.
+// beside_ssb: the previous call's SSB pipeline is expected to hold the CUs (pipelined calls); the persistent
+// N = 16384 kernel then launches one workgroup per CU, the one that co-resides with it (measured +2-3 % per
+// step over two), instead of two per CU for the chip alone.
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles,
-                           float *spectra, float *scratch, hipStream_t stream);
+                           float *spectra, float *scratch, hipStream_t stream, bool beside_ssb = false);
 
 hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry &geo, int64_t now_ms,
                         StatsState *state, sdrg_frame_record *records, hipStream_t stream);

@@ -588,8 +588,9 @@ int device_cus() {
     return cus;
 }
 
+// wg_per_cu: persistent workgroups per CU (2 alone; 1 when the SSB pipeline shares the CUs, see launch_spectrum)
 template <int FMT>
-hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectra, hipStream_t s) {
+hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectra, hipStream_t s, int wg_per_cu = 2) {
     auto k = spectrum16k_kernel<FMT>;
     static bool attr_set = false;
     if (!attr_set) {
@@ -600,19 +601,21 @@ hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectr
     static const int max_grid = [] {  // lab override (SDRG_SPECTRUM_GRID): persistent workgroups
         const char *v = getenv("SDRG_SPECTRUM_GRID");
         const int g = v ? atoi(v) : 0;
-        return g > 0 ? g : 2 * device_cus();
+        return g > 0 ? g : 0;
     }();
-    const int grid = n_frames < max_grid ? n_frames : max_grid;
+    const int cap = max_grid > 0 ? max_grid : (wg_per_cu == 1 ? 1 : 2) * device_cus();
+    const int grid = n_frames < cap ? n_frames : cap;
     hipLaunchKernelGGL(k, dim3(grid), dim3(T), LDS_BYTES, s, iq, spectra, tabs, n_frames);
     return hipGetLastError();
 }
 
-hipError_t launch_fmt(const void *iq, int fmt, int n_frames, const float *tabs, float *spectra, hipStream_t s) {
+hipError_t launch_fmt(const void *iq, int fmt, int n_frames, const float *tabs, float *spectra, hipStream_t s,
+                      int wg_per_cu) {
     switch (fmt) {
-    case SDRG_IQ_CS8: return launch<SDRG_IQ_CS8>(iq, n_frames, tabs, spectra, s);
-    case SDRG_IQ_CU8: return launch<SDRG_IQ_CU8>(iq, n_frames, tabs, spectra, s);
-    case SDRG_IQ_CS16: return launch<SDRG_IQ_CS16>(iq, n_frames, tabs, spectra, s);
-    case SDRG_IQ_CF32: return launch<SDRG_IQ_CF32>(iq, n_frames, tabs, spectra, s);
+    case SDRG_IQ_CS8: return launch<SDRG_IQ_CS8>(iq, n_frames, tabs, spectra, s, wg_per_cu);
+    case SDRG_IQ_CU8: return launch<SDRG_IQ_CU8>(iq, n_frames, tabs, spectra, s, wg_per_cu);
+    case SDRG_IQ_CS16: return launch<SDRG_IQ_CS16>(iq, n_frames, tabs, spectra, s, wg_per_cu);
+    case SDRG_IQ_CF32: return launch<SDRG_IQ_CF32>(iq, n_frames, tabs, spectra, s, wg_per_cu);
     default: return hipErrorInvalidValue;
     }
 }
@@ -863,12 +866,13 @@ size_t spectrum_scratch_floats(int n, int n_frames) {
 }
 
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles, float *spectra,
-                           float *scratch, hipStream_t stream) {
+                           float *scratch, hipStream_t stream, bool beside_ssb) {
     if (n_frames <= 0) return hipSuccess;
     switch (n) {
     case 32768: return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
     case 65536: return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
-    case 16384: return k16::launch_fmt(iq, fmt, n_frames, twiddles + spectrum_k16_tables_offset(), spectra, stream);
+    case 16384: return k16::launch_fmt(iq, fmt, n_frames, twiddles + spectrum_k16_tables_offset(), spectra, stream,
+                                      beside_ssb ? 1 : 2);
     case 64: return launch_n<6>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 128: return launch_n<7>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 256: return launch_n<8>(iq, fmt, n_frames, twiddles, spectra, stream);
