@@ -249,6 +249,41 @@ int32_t sdrg_ingest_pop(sdrg_ingest *ing, int32_t stream, void *out, int32_t *po
 /* setSamplesPerReading: cut at n from now on (queued frames of the old size are discarded) */
 int32_t sdrg_ingest_set_samples_per_reading(sdrg_ingest *ing, int32_t n);
 
+/* ------------------------------------------------------------------------------------------------
+ * SSBProcessor (src/ssb/ssb_processor.h:24-58, ssb_processor.cpp:26-115): the reference runs the SSB chain on a
+ * worker thread fed by soapyCallback through a queue of at most 3 frames that drops its OLDEST frame when full
+ * (:51-64); per popped frame, processSSB_opt with the frame's sample rate and the current sound mode, then the
+ * PCM callback (only when the frame produced samples), then the audio pulse detector and its callback (:77-115).
+ * This object is that worker over a one-stream engine (SSB + audio-pulse stages), so a consumer that falls behind
+ * drops the same frames as the reference and the filter state continues over the frames that were processed.
+ * Callbacks run on the worker thread.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct sdrg_ssb_processor sdrg_ssb_processor;
+typedef struct sdrg_ssb_callbacks {
+    void *user;
+    void (*pcm)(void *user, const int16_t *pcm, int32_t n);                     /* pcmCallback, ([S)V */
+    void (*pulse)(void *user, float strength, int32_t live_etat);               /* pulseCallback_, (FI)V */
+} sdrg_ssb_callbacks;
+/* queue_max: frames held before the oldest is dropped (0 = the reference's 3). */
+int32_t sdrg_ssb_processor_create(int32_t device, int32_t queue_max, sdrg_ssb_processor **out);
+int32_t sdrg_ssb_processor_destroy(sdrg_ssb_processor *p);   /* stopProcessing + release */
+int32_t sdrg_ssb_processor_start(sdrg_ssb_processor *p, const sdrg_ssb_callbacks *cbs);  /* startProcessing */
+int32_t sdrg_ssb_processor_stop(sdrg_ssb_processor *p);      /* stopProcessing: the worker finishes its frame */
+/* enqueueData: copies the frame (n samples in `format`) with the rate it was read at; ignored when not started. */
+int32_t sdrg_ssb_processor_enqueue(sdrg_ssb_processor *p, const void *iq, int32_t format, int32_t n,
+                                   int64_t sample_rate);
+/* BridgeConfig::getSoundMode() as the worker reads it per frame (:102); default 1. */
+int32_t sdrg_ssb_processor_set_sound_mode(sdrg_ssb_processor *p, int32_t mode);
+/* setPulseConfig (:70-75): a fresh AudioPulseDetector with cfg before the next frame. */
+int32_t sdrg_ssb_processor_set_pulse_config(sdrg_ssb_processor *p, const sdrg_pulse_config *cfg);
+float sdrg_ssb_processor_get_ambient_energy(const sdrg_ssb_processor *p);  /* getAmbientEnergy (ssb_processor.h:34) */
+float sdrg_ssb_processor_get_current_ratio(const sdrg_ssb_processor *p);   /* getCurrentRatio (:35): always 0 */
+/* Wait until the queue is empty and the worker idle (or stopped). */
+int32_t sdrg_ssb_processor_drain(sdrg_ssb_processor *p);
+/* Frames enqueued, dropped from a full queue, processed; status of the last failed frame (0 if none). */
+int32_t sdrg_ssb_processor_counters(const sdrg_ssb_processor *p, int64_t *enqueued, int64_t *dropped,
+                                    int64_t *processed, int32_t *last_status);
+
 typedef struct sdrg_engine sdrg_engine;
 
 /* Library identity. */
@@ -294,6 +329,14 @@ int32_t sdrg_engine_apply_config(sdrg_engine *eng, const sdrg_config *cfg);
 int32_t sdrg_engine_set_frequency(sdrg_engine *eng, int64_t center_frequency);
 /* JNI setFrequencyFocusRange (:1025-1040). */
 int32_t sdrg_engine_set_frequency_focus_range(sdrg_engine *eng, int32_t khz);
+/* JNI setSampleRate (:931-953): BridgeConfig only.  The SSB chain uses the new rate from the next frame (it is
+ * handed BridgeConfig's rate per frame, :441-442); the statistics keep the rate of the last configure() point
+ * (create / applyConfig / setFrequency / setFrequencyFocusRange), as FFTProcessor::config_ does.  The spectral
+ * pulse detector is not reconfigured (only applyConfig does that, :1130-1138). */
+int32_t sdrg_engine_set_sample_rate(sdrg_engine *eng, int64_t sample_rate);
+/* JNI setSamplesPerReading (:1015-1021): BridgeConfig only; the frame size of the following calls (the reader cuts
+ * frames at it, :541-573, and FFTProcessor::process plans whatever length it is handed, fft_process.cpp:42-79). */
+int32_t sdrg_engine_set_samples_per_reading(sdrg_engine *eng, int32_t n);
 /* JNI setSoundMode (:1066-1071). */
 int32_t sdrg_engine_set_sound_mode(sdrg_engine *eng, int32_t mode);
 /* processSSB_opt's upperSideband argument (default 1, which is what SSBProcessor always passes,
@@ -360,8 +403,19 @@ int32_t sdrg_engine_set_stream(sdrg_engine *eng, void *hip_stream);
  * start of each call and does not join them into the main stream at its end, so a call's SSB pipeline runs
  * beside the next call's spectrum.  The spectrum / statistics / spectral-pulse outputs are ordered on the
  * main stream as usual; the PCM and audio-pulse outputs are complete after sdrg_engine_synchronize (or
- * after the next call's SSB stage starts, which follows them on the SSB stream).  process_host always joins. */
+ * after the next call's SSB stage starts, which follows them on the SSB stream).  process_host always joins.
+ * The input buffer stays in use until the SSB stage has read it: see sdrg_engine_input_released below. */
 int32_t sdrg_engine_set_pipelining(sdrg_engine *eng, int32_t on);
+/* The INPUT of a call: the kernels read `iq` asynchronously after sdrg_engine_process_device returns -- the
+ * spectrum on the main stream and the SSB pipeline on its own stream, which in pipelined mode runs on past the
+ * call, beside the next call's spectrum.  The caller must not overwrite or free `iq` until the call has released
+ * it.  input_released: *released = 1 once every kernel of the last call that reads its iq has finished (a
+ * non-blocking query).  wait_input_released: enqueue on `hip_stream` (NULL = the engine's main stream) a wait for
+ * that release, so a refill of the same buffer enqueued there afterwards (e.g. the next frame's host-to-device
+ * copy) cannot overtake the readers -- without a host synchronisation and without joining the SSB stream into the
+ * next call's spectrum (neither call is needed with a fresh buffer per call). */
+int32_t sdrg_engine_input_released(const sdrg_engine *eng, int32_t *released);
+int32_t sdrg_engine_wait_input_released(sdrg_engine *eng, void *hip_stream);
 
 /* Same from host memory (PCIe-inclusive): copies iq in, runs, copies outputs back, synchronises,
  * then invokes the registered callbacks per stream in soapyCallback order.  Any output may be NULL. */

@@ -11,6 +11,7 @@
 
 #include <complex>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "sdrg.h"
@@ -75,6 +76,39 @@ void processSSB_opt(std::vector<std::complex<float>> iq, uint32_t sampleRate, bo
 
 // Status of the last processSSB_opt call.
 int32_t lastSsbStatus();
+
+class AudioPulseDetector;
+
+// SSBProcessor (src/ssb/ssb_processor.h:24-58): the worker thread + 3-deep drop-oldest queue, over
+// sdrg_ssb_processor (frames run through a one-stream engine's SSB + audio-pulse stages).  The sound mode the
+// reference reads from BridgeConfig per frame is set here with setSoundMode.
+using PcmDataCallback = std::function<void(const std::vector<int16_t> &)>;
+class SSBProcessor {
+public:
+    SSBProcessor();
+    ~SSBProcessor();
+    SSBProcessor(const SSBProcessor &) = delete;
+    SSBProcessor &operator=(const SSBProcessor &) = delete;
+
+    void startProcessing(PcmDataCallback pcm_cb);
+    void startProcessing(PcmDataCallback pcm_cb, std::function<void(float, int)> pulse_cb);
+    void stopProcessing();
+    void enqueueData(std::vector<std::complex<float>> &&iq_data, uint32_t sample_rate);
+    void setPulseConfig(const sdrg_pulse_config &cfg);
+    float getAmbientEnergy() const;
+    float getCurrentRatio() const { return 0.f; }
+    void setSoundMode(int mode);
+    int32_t lastStatus() const { return status_; }
+
+private:
+    static void onPcm(void *u, const int16_t *p, int32_t n);
+    static void onPulse(void *u, float strength, int32_t live_etat);
+    sdrg_ssb_processor *proc_ = nullptr;
+    PcmDataCallback pcm_cb_;
+    std::function<void(float, int)> pulse_cb_;
+    std::vector<int16_t> pcm_;
+    int32_t status_ = SDRG_OK;
+};
 
 // SpectralPulseDetector (src/dsp/spectral_pulse_detector.h:19-79) and AudioPulseDetector
 // (src/ssb/audio_pulse_detector.h:15-104): same public interface; each object owns a one-stream

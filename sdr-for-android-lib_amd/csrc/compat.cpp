@@ -58,10 +58,10 @@ void FFTProcessor::process(const std::complex<float> *input_buf, uint32_t input_
 // reference (which re-plans FFTW for whatever length it receives).
 void FFTProcessor::processAt(const std::complex<float> *input_buf, uint32_t input_len, int64_t now_ms) {
     if (!configured_) cfg_ = make_config(0, 2500000, (int)input_len, 5, 1);
-    if ((uint32_t)cfg_.samples_per_reading != input_len) {
+    if ((uint32_t)cfg_.samples_per_reading != input_len) {  // process() takes whatever length it is handed
         cfg_.samples_per_reading = (int32_t)input_len;
         if (eng_) {
-            status_ = sdrg_engine_apply_config(eng_, &cfg_);
+            status_ = sdrg_engine_set_samples_per_reading(eng_, (int32_t)input_len);
             if (status_) return;
         }
     }
@@ -125,6 +125,57 @@ void processSSB_opt(std::vector<std::complex<float>> iq, uint32_t sampleRate, bo
     g_ssb_status = sdrg_engine_process_host(g_ssb, iq.data(), SDRG_IQ_CF32, SDRG_STAGE_SSB, nullptr, nullptr,
                                             pcmOut.empty() ? nullptr : pcmOut.data(), 0);
     if (g_ssb_status) pcmOut.clear();
+}
+
+// ---- SSBProcessor (ssb_processor.cpp:26-115) ------------------------------------------------------------
+SSBProcessor::SSBProcessor() {
+    status_ = sdrg_ssb_processor_create(0, 0, &proc_);
+    if (status_) proc_ = nullptr;
+}
+
+SSBProcessor::~SSBProcessor() {
+    if (proc_) sdrg_ssb_processor_destroy(proc_);  // stopProcessing() first, as the reference's destructor
+}
+
+void SSBProcessor::onPcm(void *u, const int16_t *p, int32_t n) {
+    SSBProcessor *s = static_cast<SSBProcessor *>(u);
+    if (!s->pcm_cb_) return;
+    s->pcm_.assign(p, p + n);
+    s->pcm_cb_(s->pcm_);
+}
+
+void SSBProcessor::onPulse(void *u, float strength, int32_t live_etat) {
+    SSBProcessor *s = static_cast<SSBProcessor *>(u);
+    if (s->pulse_cb_) s->pulse_cb_(strength, live_etat);
+}
+
+void SSBProcessor::startProcessing(PcmDataCallback pcm_cb) { startProcessing(std::move(pcm_cb), nullptr); }
+
+void SSBProcessor::startProcessing(PcmDataCallback pcm_cb, std::function<void(float, int)> pulse_cb) {
+    if (!proc_) return;
+    pcm_cb_ = std::move(pcm_cb);
+    pulse_cb_ = std::move(pulse_cb);
+    const sdrg_ssb_callbacks c{this, &SSBProcessor::onPcm, &SSBProcessor::onPulse};
+    status_ = sdrg_ssb_processor_start(proc_, &c);
+}
+
+void SSBProcessor::stopProcessing() {
+    if (proc_) status_ = sdrg_ssb_processor_stop(proc_);
+}
+
+void SSBProcessor::enqueueData(std::vector<std::complex<float>> &&iq_data, uint32_t sample_rate) {
+    if (!proc_ || iq_data.empty()) return;
+    status_ = sdrg_ssb_processor_enqueue(proc_, iq_data.data(), SDRG_IQ_CF32, (int32_t)iq_data.size(), sample_rate);
+}
+
+void SSBProcessor::setPulseConfig(const sdrg_pulse_config &cfg) {
+    if (proc_) status_ = sdrg_ssb_processor_set_pulse_config(proc_, &cfg);
+}
+
+float SSBProcessor::getAmbientEnergy() const { return proc_ ? sdrg_ssb_processor_get_ambient_energy(proc_) : 0.f; }
+
+void SSBProcessor::setSoundMode(int mode) {
+    if (proc_) status_ = sdrg_ssb_processor_set_sound_mode(proc_, mode);
 }
 
 // ---- pulse detectors ------------------------------------------------------------------------------

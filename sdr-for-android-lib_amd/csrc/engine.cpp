@@ -19,7 +19,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <mutex>
+#include <set>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "design.h"
@@ -40,6 +43,20 @@ int32_t sdrg::fail(int32_t code, const char *fmt, ...) {
     va_end(ap);
     g_last_error = buf;
     return code;
+}
+
+hipError_t sdrg::ensure_dynamic_lds(const void *kernel, int bytes) {
+    static std::mutex mu;
+    static std::set<std::tuple<const void *, int, int>> done;  // (kernel, device, bytes)
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_tuple(kernel, dev, bytes);
+    if (done.count(key)) return hipSuccess;
+    e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.insert(key);
+    return e;
 }
 
 namespace {
@@ -106,12 +123,21 @@ struct EvSet {
 }  // namespace
 
 struct sdrg_engine {
-    sdrg_config cfg{};
+    sdrg_config cfg{};  // BridgeConfig: what the next frame is cut, demodulated and reported with
+    // FFTProcessor::config_ (fft_process.h:88, :20-39): the centre frequency, sample rate and focus the statistics
+    // use, copied from cfg at each configure() point (create, applyConfig, setFrequency, setFrequencyFocusRange).
+    // setSampleRate / setSamplesPerReading / setSoundMode change cfg only (sdr-bridge-java-soapy.cpp:931-1023).
+    uint32_t fft_fc = 0, fft_fs = 0;
+    int32_t fft_focus = 0;
     int n_streams = 0;
     int device = 0;
     hipStream_t s_main = nullptr, s_ssb = nullptr;
     hipStream_t s_own = nullptr;  // the engine's own main stream (s_main is it, or the caller's via set_stream)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // input release: recorded after the last kernel of a call that reads its iq buffer on each stream (the
+    // spectrum on s_main, the SSB pipeline on s_ssb); sdrg_engine_input_released / _wait_input_released
+    hipEvent_t ev_in_main = nullptr, ev_in_ssb = nullptr;
+    bool in_main_recorded = false, in_ssb_recorded = false;
     // profiling: a ring of event sets so consecutive calls are timed without host synchronisation
     static constexpr int RING = 64;
     EvSet ring[RING];
@@ -178,6 +204,13 @@ sdrg_pulse_config spectral_pulse_cfg_for(const sdrg_config &c) {
     return p;
 }
 
+// FFTProcessor::configure(FftProcessorConfig{cf, fs, N, focus}) with the bridge's current values
+void configure_fft(sdrg_engine *e) {
+    e->fft_fc = (uint32_t)e->cfg.center_frequency;
+    e->fft_fs = (uint32_t)e->cfg.sample_rate;
+    e->fft_focus = e->cfg.freq_focus_range_khz;
+}
+
 int32_t validate_config(const sdrg_config *cfg) {
     if (!cfg) return fail(SDRG_E_INVALID, "null config");
     if (cfg->samples_per_reading < 1 || cfg->samples_per_reading > (1 << 20))
@@ -232,6 +265,8 @@ int32_t fold_slot(sdrg_engine *e, int slot) {
         t.stats_ms = ms;
     }
     if (ev.has_ssb) {
+        // pipelined calls never join the SSB stream into ev.end's stream: wait for its own end event
+        HIP_TRY(hipEventSynchronize(ev.ssb1));
         HIP_TRY(hipEventElapsedTime(&ms, ev.ssb0, ev.ssb1));
         t.ssb_ms = ms;
     }
@@ -256,9 +291,11 @@ int32_t fold_all(sdrg_engine *e) {
     return SDRG_OK;
 }
 
-// processSSB_opt's per-call control logic (:223-282) -> kernel parameters
-int32_t prepare_ssb(sdrg_engine *e, SsbParams *p) {
-    SsbControl &c = e->ssb;
+// processSSB_opt's per-call control logic (:223-282) -> kernel parameters.  Works on copies of the engine's
+// SSB control statics (c) and NCO phase (nco_phase) that the caller commits only once the call's launches have
+// succeeded, so a rejected call freezes no frame size and advances no phase.  The taps and chunk table it may
+// upload are keyed by the committed statics: a rejected call's upload is simply redone by the next call.
+int32_t prepare_ssb(sdrg_engine *e, SsbControl &c, uint32_t &nco_phase, SsbParams *p) {
     const uint32_t fs = (uint32_t)e->cfg.sample_rate;
     if (c.samp_count == 0) c.samp_count = e->cfg.samples_per_reading;  // static size_t sampCount = iq.size()
     const int mode = e->cfg.sound_mode;
@@ -338,9 +375,9 @@ int32_t prepare_ssb(sdrg_engine *e, SsbParams *p) {
         }
         p->nco_on = 1;
         p->nco_inc = nco_increment(e->nco_hz, fs);
-        p->nco_phase = e->nco_phase;
+        p->nco_phase = nco_phase;
         p->nco_tab = e->d_nco_tab;
-        e->nco_phase += p->nco_inc * (uint32_t)c.samp_count;  // phase-continuous across calls
+        nco_phase += p->nco_inc * (uint32_t)c.samp_count;  // phase-continuous across calls
     }
     return SDRG_OK;
 }
@@ -410,11 +447,11 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     }
     SsbParams sp;
     if (do_ssb) {
-        int32_t rc = prepare_ssb(e, &sp);
-        if (rc) return rc;
-        if (!pcm && sp.pcm_len > 0) return fail(SDRG_E_INVALID, "null pcm with SSB stage");
-        rc = ensure_device(&e->d_ssb_scratch, &e->ssb_scratch_elems,
-                           (size_t)B * ((size_t)sp.samp_count + (size_t)sp.pcm_len));
+        // frame size and PCM length this call will use (sampCount freezes at the first SSB call, :224-227)
+        const int64_t samp = ssb_frozen_or(e);
+        const int plen = ssb_pcm_len(samp, (uint32_t)e->cfg.sample_rate, e->fir_taps);
+        if (!pcm && plen > 0) return fail(SDRG_E_INVALID, "null pcm with SSB stage");
+        int32_t rc = ensure_device(&e->d_ssb_scratch, &e->ssb_scratch_elems, (size_t)B * ((size_t)samp + (size_t)plen));
         if (rc) return rc;
     }
     if (do_spec) {
@@ -426,10 +463,18 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
 
     StatsGeometry geo{};
     if (do_stats) {
-        geo = stats_geometry((uint32_t)e->cfg.sample_rate, (uint32_t)e->cfg.center_frequency, n,
-                             e->cfg.freq_focus_range_khz);
+        if (e->fft_fs == 0) return fail(SDRG_E_INVALID, "the statistics' sample rate is 0");
+        geo = stats_geometry(e->fft_fs, e->fft_fc, n, e->fft_focus);
         geo.cf_changed = e->cf_changed_pending ? 1 : 0;
         if (geo.max_pool > 16384) return fail(SDRG_E_UNSUPPORTED, "pooled noise bins %d > 16384", geo.max_pool);
+    }
+
+    // last of the checks and allocations: the SSB control statics of this call (committed at the end)
+    SsbControl ssb_next = e->ssb;
+    uint32_t nco_next = e->nco_phase;
+    if (do_ssb) {
+        int32_t rc = prepare_ssb(e, ssb_next, nco_next, &sp);
+        if (rc) return rc;
     }
 
     const bool prof = e->profiling;
@@ -461,6 +506,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     if (do_spec) {
         HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, e->s_main, do_ssb && early_fork));
         if (prof) HIP_TRY(hipEventRecord(ev->spec, e->s_main));
+        HIP_TRY(hipEventRecord(e->ev_in_main, e->s_main));  // the spectrum is the main stream's last iq reader
     }
     if (do_ssb) {  // fork
         if (!early_fork) {
@@ -477,6 +523,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         }
         HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_chunk_table, e->d_ssb, e->d_ssb_scratch, pcm,
                            do_ap ? &af : nullptr, e->s_ssb));
+        HIP_TRY(hipEventRecord(e->ev_in_ssb, e->s_ssb));  // the SSB pipeline has read every raw sample
         if (do_ap) {
             int32_t rc = pulse_bank_audio_detect(&e->audio_bank, e->audio_bank.d_out, e->s_ssb);
             if (rc) return rc;
@@ -492,7 +539,6 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             if (rc) return rc;
         }
         if (prof) HIP_TRY(hipEventRecord(ev->stats, e->s_main));
-        e->cf_changed_pending = false;
     }
     if (do_ssb && !early_fork) HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));  // join
     if (prof) {
@@ -501,6 +547,14 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         e->ring_last = e->ring_next;
         e->ring_next = (e->ring_next + 1) % sdrg_engine::RING;
     }
+    // every launch of the call is enqueued: commit its host-side state
+    if (do_ssb) {
+        e->ssb = ssb_next;
+        e->nco_phase = nco_next;
+    }
+    if (do_stats) e->cf_changed_pending = false;
+    e->in_main_recorded = e->in_main_recorded || do_spec;
+    e->in_ssb_recorded = e->in_ssb_recorded || do_ssb;
     return SDRG_OK;
 }
 
@@ -604,7 +658,8 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
     HIP_TRY(hipGetDeviceProperties(&prop, device));
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(SDRG_E_NODEVICE, "device %d is %s, this build targets gfx950", device, prop.gcnArchName);
-    HIP_TRY(hipSetDevice(device));
+    DeviceScope dscope(device);
+    HIP_TRY(dscope.error());
     sdrg_engine *e = new sdrg_engine();
     e->cfg = *cfg;
     e->spec_pulse_cfg = spectral_pulse_cfg_for(*cfg);
@@ -625,7 +680,8 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         hipStreamCreateWithPriority(&e->s_ssb, hipStreamNonBlocking, prio_ssb) != hipSuccess)
         return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
     e->s_main = e->s_own;
-    hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join};
+    configure_fft(e);
+    hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join, &e->ev_in_main, &e->ev_in_ssb};
     for (auto p : evs)
         if (hipEventCreateWithFlags(p, hipEventDisableTiming) != hipSuccess)
             return cleanup(fail(SDRG_E_HIP, "hipEventCreate failed"));
@@ -637,7 +693,7 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
 
 int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (!e) return SDRG_OK;
-    (void)hipSetDevice(e->device);
+    DeviceScope dscope(e->device);
     // the caller's stream (sdrg_engine_set_stream) must outlive the engine: synchronise it while it is set
     if (e->s_main) (void)hipStreamSynchronize(e->s_main);
     if (e->s_ssb) (void)hipStreamSynchronize(e->s_ssb);
@@ -646,7 +702,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
                     e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
-    hipEvent_t evs[] = {e->ev_fork, e->ev_join};
+    hipEvent_t evs[] = {e->ev_fork, e->ev_join, e->ev_in_main, e->ev_in_ssb};
     for (hipEvent_t ev : evs)
         if (ev) (void)hipEventDestroy(ev);
     for (auto &r : e->ring) {
@@ -667,6 +723,7 @@ int32_t sdrg_engine_apply_config(sdrg_engine *e, const sdrg_config *cfg) {
     int32_t rc = validate_config(cfg);
     if (rc) return rc;
     e->cfg = *cfg;  // applied at the next process call (frame boundary)
+    configure_fft(e);  // fftProcessor.configure (:1123-1128)
     e->spec_pulse_cfg = spectral_pulse_cfg_for(*cfg);
     if (e->spec_bank_live) return pulse_bank_configure(&e->spec_bank, &e->spec_pulse_cfg);
     return SDRG_OK;
@@ -675,7 +732,48 @@ int32_t sdrg_engine_apply_config(sdrg_engine *e, const sdrg_config *cfg) {
 int32_t sdrg_engine_set_frequency(sdrg_engine *e, int64_t center_frequency) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     e->cfg.center_frequency = center_frequency;
+    configure_fft(e);              // :896-901
     e->cf_changed_pending = true;  // :907 isCenterFrequencyChanged = true
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_sample_rate(sdrg_engine *e, int64_t sample_rate) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if ((uint32_t)sample_rate == 0) return fail(SDRG_E_INVALID, "sample_rate must be > 0");
+    e->cfg.sample_rate = sample_rate;  // BridgeConfig only (:931-953): the SSB sees it at the next frame
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_set_samples_per_reading(sdrg_engine *e, int32_t n) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if (n < 1 || n > (1 << 20)) return fail(SDRG_E_UNSUPPORTED, "samples_per_reading %d outside [1, 2^20]", n);
+    e->cfg.samples_per_reading = n;  // BridgeConfig only (:1015-1021): the frames are cut at n from now on
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_input_released(const sdrg_engine *e, int32_t *released) {
+    if (!e || !released) return fail(SDRG_E_INVALID, "null argument");
+    *released = 1;
+    hipEvent_t evs[] = {e->in_main_recorded ? e->ev_in_main : nullptr, e->in_ssb_recorded ? e->ev_in_ssb : nullptr};
+    for (hipEvent_t ev : evs) {
+        if (!ev) continue;
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipErrorNotReady) {
+            *released = 0;
+        } else if (q != hipSuccess) {
+            return fail(SDRG_E_HIP, "hipEventQuery: %s", hipGetErrorString(q));
+        }
+    }
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_wait_input_released(sdrg_engine *e, void *hip_stream) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : e->s_main;
+    if (e->in_main_recorded && s != e->s_main) HIP_TRY(hipStreamWaitEvent(s, e->ev_in_main, 0));
+    if (e->in_ssb_recorded) HIP_TRY(hipStreamWaitEvent(s, e->ev_in_ssb, 0));
     return SDRG_OK;
 }
 
@@ -683,6 +781,7 @@ int32_t sdrg_engine_set_frequency_focus_range(sdrg_engine *e, int32_t khz) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     if (khz < 0) return fail(SDRG_E_INVALID, "focus range must be >= 0");
     e->cfg.freq_focus_range_khz = khz;
+    configure_fft(e);  // :1031-1036
     return SDRG_OK;
 }
 
@@ -703,7 +802,8 @@ int32_t sdrg_engine_set_ssb_variant(sdrg_engine *e, double nco_hz, int32_t fir_t
     if (fir_taps != 0 && (fir_taps < 3 || fir_taps > 255 || (fir_taps & 1) == 0))
         return fail(SDRG_E_INVALID, "fir_taps must be 0 or odd in [3, 255], got %d", fir_taps);
     if (!std::isfinite(nco_hz)) return fail(SDRG_E_INVALID, "nco_hz must be finite");
-    HIP_TRY(hipSetDevice(e->device));
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
     HIP_TRY(hipStreamSynchronize(e->s_ssb));  // in-flight SSB kernels read the taps being replaced
     e->nco_hz = nco_hz;
     e->fir_taps = fir_taps;
@@ -736,7 +836,8 @@ int32_t sdrg_engine_pcm_len(const sdrg_engine *e) {
 
 int32_t sdrg_engine_reset_state(sdrg_engine *e) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
-    HIP_TRY(hipSetDevice(e->device));
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));
     HIP_TRY(hipMemset(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
@@ -751,7 +852,8 @@ int32_t sdrg_engine_reset_state(sdrg_engine *e) {
 
 int32_t sdrg_engine_set_pipelining(sdrg_engine *e, int32_t on) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
-    HIP_TRY(hipSetDevice(e->device));
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
     if (e->pipelined && !on) {  // re-join what is in flight so later work on s_main follows it
         HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
         HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));
@@ -762,7 +864,8 @@ int32_t sdrg_engine_set_pipelining(sdrg_engine *e, int32_t on) {
 
 int32_t sdrg_engine_set_stream(sdrg_engine *e, void *hip_stream) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
-    HIP_TRY(hipSetDevice(e->device));
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
     HIP_TRY(hipStreamSynchronize(e->s_main));  // work already enqueued stays ordered before the switch
     e->s_main = hip_stream ? static_cast<hipStream_t>(hip_stream) : e->s_own;
     return SDRG_OK;
@@ -796,7 +899,8 @@ int32_t sdrg_engine_pulse_outputs(const sdrg_engine *e, const sdrg_pulse_output 
 
 int32_t sdrg_engine_get_pulse_outputs(sdrg_engine *e, sdrg_pulse_output *spectral, sdrg_pulse_output *audio) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
-    HIP_TRY(hipSetDevice(e->device));
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));
     const size_t bytes = sizeof(sdrg_pulse_output) * (size_t)e->n_streams;
@@ -814,7 +918,8 @@ int32_t sdrg_engine_get_pulse_outputs(sdrg_engine *e, sdrg_pulse_output *spectra
 int32_t sdrg_engine_process_device(sdrg_engine *e, const void *iq, int32_t format, int32_t stages, float *spectra,
                                    sdrg_frame_record *records, int16_t *pcm, int64_t now_ms) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
-    HIP_TRY(hipSetDevice(e->device));
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
     return enqueue(e, iq, format, stages, spectra, records, pcm, now_ms, false);
 }
 
@@ -836,7 +941,8 @@ int32_t sdrg_engine_process_host(sdrg_engine *e, const void *iq, int32_t format,
     if (!iq) return fail(SDRG_E_INVALID, "null iq");
     const int bps = bytes_per_sample(format);
     if (!bps) return fail(SDRG_E_INVALID, "unknown iq format %d", format);
-    HIP_TRY(hipSetDevice(e->device));
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
     const int n = e->cfg.samples_per_reading;
     const int B = e->n_streams;
     const size_t iq_bytes = (size_t)B * n * bps;
@@ -922,7 +1028,8 @@ int32_t sdrg_engine_set_callbacks(sdrg_engine *e, const sdrg_callbacks *cbs) {
 
 int32_t sdrg_engine_set_profiling(sdrg_engine *e, int32_t enabled) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
-    HIP_TRY(hipSetDevice(e->device));
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
     if (enabled && !e->ring_created) {
         for (auto &r : e->ring) {
             hipEvent_t *rev[] = {&r.t0, &r.spec, &r.stats, &r.ssb0, &r.ssb1, &r.end};

@@ -143,8 +143,8 @@ int32_t regrow(sdrg_pulse_bank *b, int new_cap) {
     return SDRG_OK;
 }
 
+// callers hold a DeviceScope for b->device
 int32_t before_launch(sdrg_pulse_bank *b, hipStream_t stream) {
-    PB_TRY(hipSetDevice(b->device));
     if (b->reset_pending) {
         PB_TRY(launch_pulse_reset(b->d_state, b->n_streams, b->cfg.t_target_init, stream));
         b->reset_pending = false;
@@ -176,7 +176,8 @@ int32_t pulse_bank_init(sdrg_pulse_bank *b, int kind, const sdrg_pulse_config *c
     b->cfg = *cfg;
     b->n_streams = n_streams;
     b->device = device;
-    PB_TRY(hipSetDevice(device));
+    DeviceScope dscope_(device);
+    PB_TRY(dscope_.error());
     if ((rc = dev_alloc(&b->d_state, (size_t)n_streams)) || (rc = dev_alloc(&b->d_out, (size_t)n_streams))) return rc;
     if (kind == SDRG_PULSE_SPECTRAL && (rc = dev_alloc(&b->d_fh, (size_t)n_streams * 2 * PULSE_FH_SLOTS))) return rc;
     if (kind == SDRG_PULSE_AUDIO && (rc = dev_alloc(&b->d_new_count, (size_t)n_streams))) return rc;
@@ -187,7 +188,7 @@ int32_t pulse_bank_init(sdrg_pulse_bank *b, int kind, const sdrg_pulse_config *c
 }
 
 void pulse_bank_release(sdrg_pulse_bank *b) {
-    (void)hipSetDevice(b->device);
+    DeviceScope dscope_(b->device);
     if (b->last_stream) (void)hipStreamSynchronize(b->last_stream);
     void *bufs[] = {b->d_state, b->d_e, b->d_f, b->d_rt, b->d_re, b->d_fh, b->d_out, b->d_in, b->d_new, b->d_new_count};
     for (void *p : bufs)
@@ -198,7 +199,8 @@ void pulse_bank_release(sdrg_pulse_bank *b) {
 int32_t pulse_bank_configure(sdrg_pulse_bank *b, const sdrg_pulse_config *cfg) {
     int32_t rc = pulse_config_check(b->kind, cfg);
     if (rc) return rc;
-    PB_TRY(hipSetDevice(b->device));
+    DeviceScope dscope_(b->device);
+    PB_TRY(dscope_.error());
     b->cfg = *cfg;
     if (b->kind == SDRG_PULSE_AUDIO) b->reset_pending = true;  // AudioPulseDetector(pendingConfig_)
     const int need = cap_for(*cfg);
@@ -208,6 +210,8 @@ int32_t pulse_bank_configure(sdrg_pulse_bank *b, const sdrg_pulse_config *cfg) {
 
 int32_t pulse_bank_spectral(sdrg_pulse_bank *b, const float *snr_sigma, const float *freq_hz, int stride_bytes,
                             sdrg_pulse_output *out, hipStream_t stream) {
+    DeviceScope dscope_(b->device);
+    PB_TRY(dscope_.error());
     if (b->kind != SDRG_PULSE_SPECTRAL) return fail(SDRG_E_INVALID, "not a spectral pulse bank");
     if (!snr_sigma || !freq_hz || !out) return fail(SDRG_E_INVALID, "null pointer");
     if (stride_bytes < 0 || (stride_bytes & 3)) return fail(SDRG_E_INVALID, "stride must be a multiple of 4");
@@ -219,6 +223,8 @@ int32_t pulse_bank_spectral(sdrg_pulse_bank *b, const float *snr_sigma, const fl
 }
 
 int32_t pulse_bank_audio_front(sdrg_pulse_bank *b, int n, AudioFront *af, hipStream_t stream) {
+    DeviceScope dscope_(b->device);
+    PB_TRY(dscope_.error());
     if (b->kind != SDRG_PULSE_AUDIO) return fail(SDRG_E_INVALID, "not an audio pulse bank");
     const PulseParams p = params_of(b);
     const size_t max_new = (size_t)std::max(n, 0) / (size_t)p.frame_samples + 2;  // (frameCount_ + n) / frameSamples_ < this
@@ -248,6 +254,8 @@ int32_t pulse_bank_audio_detect(sdrg_pulse_bank *b, sdrg_pulse_output *out, hipS
 
 int32_t pulse_bank_audio(sdrg_pulse_bank *b, const void *audio, int fmt, int n, int stride, sdrg_pulse_output *out,
                          hipStream_t stream) {
+    DeviceScope dscope_(b->device);
+    PB_TRY(dscope_.error());
     if (b->kind != SDRG_PULSE_AUDIO) return fail(SDRG_E_INVALID, "not an audio pulse bank");
     if (fmt != 0 && fmt != 1) return fail(SDRG_E_INVALID, "sample_format must be 0 (int16) or 1 (float)");
     if (n < 0 || (n > 0 && (!audio || stride < n))) return fail(SDRG_E_INVALID, "bad audio block (n %d, stride %d)", n, stride);
@@ -362,7 +370,8 @@ int32_t sdrg_pulse_bank_process_audio_device(sdrg_pulse_bank *b, const void *aud
 
 int32_t sdrg_pulse_bank_synchronize(sdrg_pulse_bank *b) {
     if (!b) return fail(SDRG_E_INVALID, "null bank");
-    PB_TRY(hipSetDevice(b->device));
+    DeviceScope dscope_(b->device);
+    PB_TRY(dscope_.error());
     PB_TRY(hipStreamSynchronize(call_stream(b)));
     return SDRG_OK;
 }
@@ -380,7 +389,8 @@ static int32_t stage_in(sdrg_pulse_bank *b, size_t bytes) {
 int32_t sdrg_pulse_bank_process_spectral_host(sdrg_pulse_bank *b, const float *snr_sigma, const float *freq_hz,
                                               sdrg_pulse_output *out) {
     if (!b || !snr_sigma || !freq_hz || !out) return fail(SDRG_E_INVALID, "null argument");
-    PB_TRY(hipSetDevice(b->device));
+    DeviceScope dscope_(b->device);
+    PB_TRY(dscope_.error());
     const size_t S = (size_t)b->n_streams;
     int32_t rc = stage_in(b, 2 * S * sizeof(float));
     if (rc) return rc;
@@ -399,7 +409,8 @@ int32_t sdrg_pulse_bank_process_audio_host(sdrg_pulse_bank *b, const void *audio
     if (!b || !out || (n > 0 && !audio)) return fail(SDRG_E_INVALID, "null argument");
     if (sample_format != 0 && sample_format != 1) return fail(SDRG_E_INVALID, "bad sample_format");
     if (n < 0) return fail(SDRG_E_INVALID, "negative n");
-    PB_TRY(hipSetDevice(b->device));
+    DeviceScope dscope_(b->device);
+    PB_TRY(dscope_.error());
     const size_t S = (size_t)b->n_streams, es = sample_format == 0 ? 2 : 4;
     int32_t rc = stage_in(b, S * (size_t)n * es);
     if (rc) return rc;

@@ -9,6 +9,33 @@
 
 namespace sdrg {
 
+// Raise a kernel's dynamic-LDS limit to `bytes` on the CURRENT device, once per (kernel, device): the
+// attribute is per device, and engines on several devices or threads may launch the same kernel
+// concurrently (engine.cpp; mutex-protected).
+hipError_t ensure_dynamic_lds(const void *kernel, int bytes);
+
+// Makes `device` current for the scope of an entry point and restores the caller's current device on
+// exit, so the C ABI never leaves the calling thread on another device (engine.cpp, pulse_bank.cpp).
+class DeviceScope {
+public:
+    explicit DeviceScope(int device) {
+        if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+        err_ = (prev_ == device) ? hipSuccess : hipSetDevice(device);
+        changed_ = err_ == hipSuccess && prev_ != device;
+    }
+    ~DeviceScope() {
+        if (changed_ && prev_ >= 0) (void)hipSetDevice(prev_);
+    }
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+    hipError_t error() const { return err_; }
+
+private:
+    int prev_ = -1;
+    bool changed_ = false;
+    hipError_t err_ = hipSuccess;
+};
+
 // ------------------------------------------------------------------------------------------------
 // Launchers (defined in the .hip translation units).  All are asynchronous on `stream`.
 // ------------------------------------------------------------------------------------------------

@@ -399,13 +399,8 @@ template <int LOG2N, int FMT>
 hipError_t launch_t(const void *iq, int n_frames, const float *tw, float *spectra, hipStream_t s) {
     using PL = Plan<LOG2N>;
     auto k = spectrum_kernel<LOG2N, FMT>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, PL::LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(k), PL::LDS_BYTES);
+    if (e != hipSuccess) return e;
     // the per-pass tables follow the full W_N table (layout of spectrum_fill_twiddles)
     const float4 *pass_tw = reinterpret_cast<const float4 *>(tw + 2 * (size_t)PL::N);
     hipLaunchKernelGGL(k, dim3(n_frames), dim3(PL::T), PL::LDS_BYTES, s, iq, spectra, pass_tw);
@@ -592,12 +587,8 @@ int device_cus() {
 template <int FMT>
 hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectra, hipStream_t s, int wg_per_cu = 2) {
     auto k = spectrum16k_kernel<FMT>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(k), LDS_BYTES);
+    if (e != hipSuccess) return e;
     static const int max_grid = [] {  // lab override (SDRG_SPECTRUM_GRID): persistent workgroups
         const char *v = getenv("SDRG_SPECTRUM_GRID");
         const int g = v ? atoi(v) : 0;

@@ -510,13 +510,8 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
     const int staged = (geo.span_len > 0 && geo.span_len <= STAGE_MAX) ? geo.span_len : STAGE_MAX;
     const int pool = (geo.max_pool + 3) & ~3;
     const size_t lds = sizeof(float) * (size_t)((pool > staged ? pool : staged) + 4);
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(stats_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (MAX_POOL + STAGE_MAX + 8) * 4);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel), (MAX_POOL + STAGE_MAX + 8) * 4);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(stats_kernel, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms, state, records);
     return hipGetLastError();
 }

@@ -17,6 +17,23 @@ struct RealJni {
     using Env = JNIEnv;
     using Obj = jobject;
     using Mid = jmethodID;
+    using Vm = JavaVM *;
+    static Vm VmOf(Env *e) {
+        JavaVM *vm = nullptr;
+        return e->GetJavaVM(&vm) == JNI_OK ? vm : nullptr;
+    }
+    // the SSB worker thread's JNIEnv (sdr-bridge-java-soapy.cpp:701-708)
+    static Env *Attach(Vm vm, bool *attached) {
+        *attached = false;
+        if (!vm) return nullptr;
+        JNIEnv *env = nullptr;
+        const jint r = vm->GetEnv(reinterpret_cast<void **>(&env), JNI_VERSION_1_6);
+        if (r == JNI_OK) return env;
+        if (r != JNI_EDETACHED || vm->AttachCurrentThread(&env, nullptr) != JNI_OK) return nullptr;
+        *attached = true;
+        return env;
+    }
+    static void Detach(Vm vm) { vm->DetachCurrentThread(); }
     static Obj NewGlobalRef(Env *e, Obj o) { return e->NewGlobalRef(o); }
     static void DeleteGlobalRef(Env *e, Obj o) { e->DeleteGlobalRef(o); }
     static Mid MethodOf(Env *e, Obj o, const char *sig) {
@@ -119,4 +136,10 @@ extern "C" JNIEXPORT void JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_setPulseC
 extern "C" JNIEXPORT jfloat JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_getAmbientAudioEnergy(JNIEnv *env, jobject) {
     std::lock_guard<std::mutex> lk(g_mu);
     return g_bridge.getAmbientAudioEnergy(env);
+}
+
+// getCurrentAudioRatio (sdr-bridge-java-soapy.cpp:1168-1171): ssbProcessor.getCurrentRatio(), always 0
+extern "C" JNIEXPORT jfloat JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_getCurrentAudioRatio(JNIEnv *env, jobject) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_bridge.getCurrentAudioRatio(env);
 }

@@ -78,7 +78,8 @@ PULSE_OUTPUT_DTYPE = np.dtype(
 EXPORTS = [
     "sdrg_abi_version", "sdrg_last_error", "sdrg_ssb_pcm_len", "sdrg_focus_window", "sdrg_host_alloc", "sdrg_host_free", "sdrg_ssb_design", "sdrg_engine_create", "sdrg_engine_destroy",
     "sdrg_engine_apply_config", "sdrg_engine_set_frequency", "sdrg_engine_set_frequency_focus_range",
-    "sdrg_engine_set_sound_mode", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
+    "sdrg_engine_set_sound_mode", "sdrg_engine_set_sample_rate", "sdrg_engine_set_samples_per_reading",
+    "sdrg_engine_input_released", "sdrg_engine_wait_input_released", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
     "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_set_stream",
     "sdrg_engine_set_pipelining", "sdrg_engine_set_ssb_variant", "sdrg_engine_get_ssb_variant",
     "sdrg_engine_process_host",
@@ -92,6 +93,10 @@ EXPORTS = [
     "sdrg_pulse_bank_process_audio_host", "sdrg_pulse_bank_synchronize", "sdrg_pulse_bank_set_stream",
     "sdrg_ingest_create", "sdrg_ingest_destroy", "sdrg_ingest_output_format", "sdrg_ingest_push", "sdrg_ingest_status",
     "sdrg_ingest_pop_batch", "sdrg_ingest_pop", "sdrg_ingest_set_samples_per_reading",
+    "sdrg_ssb_processor_create", "sdrg_ssb_processor_destroy", "sdrg_ssb_processor_start", "sdrg_ssb_processor_stop",
+    "sdrg_ssb_processor_enqueue", "sdrg_ssb_processor_set_sound_mode", "sdrg_ssb_processor_set_pulse_config",
+    "sdrg_ssb_processor_get_ambient_energy", "sdrg_ssb_processor_get_current_ratio", "sdrg_ssb_processor_drain",
+    "sdrg_ssb_processor_counters",
 ]
 
 
@@ -165,6 +170,14 @@ class _Callbacks(ctypes.Structure):
     ]
 
 
+CB_SSB_PCM = ctypes.CFUNCTYPE(None, _V, ctypes.POINTER(ctypes.c_int16), _I32)
+CB_SSB_PULSE = ctypes.CFUNCTYPE(None, _V, _F, _I32)
+
+
+class _SsbCallbacks(ctypes.Structure):
+    _fields_ = [("user", _V), ("pcm", CB_SSB_PCM), ("pulse", CB_SSB_PULSE)]
+
+
 _lib = None
 
 
@@ -193,6 +206,10 @@ def load() -> ctypes.CDLL:
         "sdrg_engine_set_frequency": (_I32, [P, _I64]),
         "sdrg_engine_set_frequency_focus_range": (_I32, [P, _I32]),
         "sdrg_engine_set_sound_mode": (_I32, [P, _I32]),
+        "sdrg_engine_set_sample_rate": (_I32, [P, _I64]),
+        "sdrg_engine_set_samples_per_reading": (_I32, [P, _I32]),
+        "sdrg_engine_input_released": (_I32, [P, ctypes.POINTER(_I32)]),
+        "sdrg_engine_wait_input_released": (_I32, [P, P]),
         "sdrg_engine_set_upper_sideband": (_I32, [P, _I32]),
         "sdrg_engine_get_config": (_I32, [P, ctypes.POINTER(_Config)]),
         "sdrg_engine_n_streams": (_I32, [P]),
@@ -237,6 +254,18 @@ def load() -> ctypes.CDLL:
         "sdrg_ingest_pop_batch": (_I32, [P, P, ctypes.POINTER(_I32)]),
         "sdrg_ingest_pop": (_I32, [P, _I32, P, ctypes.POINTER(_I32)]),
         "sdrg_ingest_set_samples_per_reading": (_I32, [P, _I32]),
+        "sdrg_ssb_processor_create": (_I32, [_I32, _I32, ctypes.POINTER(P)]),
+        "sdrg_ssb_processor_destroy": (_I32, [P]),
+        "sdrg_ssb_processor_start": (_I32, [P, ctypes.POINTER(_SsbCallbacks)]),
+        "sdrg_ssb_processor_stop": (_I32, [P]),
+        "sdrg_ssb_processor_enqueue": (_I32, [P, P, _I32, _I32, _I64]),
+        "sdrg_ssb_processor_set_sound_mode": (_I32, [P, _I32]),
+        "sdrg_ssb_processor_set_pulse_config": (_I32, [P, ctypes.POINTER(PulseConfig)]),
+        "sdrg_ssb_processor_get_ambient_energy": (_F, [P]),
+        "sdrg_ssb_processor_get_current_ratio": (_F, [P]),
+        "sdrg_ssb_processor_drain": (_I32, [P]),
+        "sdrg_ssb_processor_counters": (_I32, [P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
+                                              ctypes.POINTER(_I32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -349,6 +378,26 @@ class Engine:
     def setSoundMode(self, mode: int) -> None:
         _check(load().sdrg_engine_set_sound_mode(self._h, mode), "setSoundMode")
         self.cfg.soundMode = mode
+
+    def setSampleRate(self, sample_rate: int) -> None:
+        """JNI setSampleRate: BridgeConfig only (the SSB sees it next frame; the statistics at the next configure)."""
+        _check(load().sdrg_engine_set_sample_rate(self._h, sample_rate), "setSampleRate")
+        self.cfg.sampleRate = sample_rate
+
+    def setSamplesPerReading(self, n: int) -> None:
+        """JNI setSamplesPerReading: BridgeConfig only; the frame size of the next calls."""
+        _check(load().sdrg_engine_set_samples_per_reading(self._h, n), "setSamplesPerReading")
+        self.cfg.samplesPerReading = n
+
+    def input_released(self) -> bool:
+        """True once every kernel of the last call that reads its iq buffer has finished (non-blocking)."""
+        r = ctypes.c_int32()
+        _check(load().sdrg_engine_input_released(self._h, ctypes.byref(r)), "input_released")
+        return bool(r.value)
+
+    def wait_input_released(self, hip_stream: int | None = None) -> None:
+        """Make hip_stream (None: the engine's main stream) wait until the last call has released its iq buffer."""
+        _check(load().sdrg_engine_wait_input_released(self._h, hip_stream), "wait_input_released")
 
     def setUpperSideband(self, upper: bool) -> None:
         _check(load().sdrg_engine_set_upper_sideband(self._h, int(upper)), "setUpperSideband")
@@ -568,6 +617,75 @@ class PulseBank:
     def close(self) -> None:
         if getattr(self, "_h", None):
             load().sdrg_pulse_bank_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SSBProcessor:
+    """SSBProcessor (src/ssb/ssb_processor.h:24-58): a worker thread fed through a queue of at most queue_max
+    frames (the reference's 3) that drops the oldest frame when full; each frame runs the SSB chain and the audio
+    pulse detector on the GPU, then pcm_cb(pcm int16 array) (only when non-empty) and pulse_cb(strength, live_etat)
+    are called on the worker thread."""
+
+    def __init__(self, device: int = 0, queue_max: int = 0):
+        h = ctypes.c_void_p()
+        _check(load().sdrg_ssb_processor_create(device, queue_max, ctypes.byref(h)), "sdrg_ssb_processor_create")
+        self._h = h
+        self._cbs = None
+
+    def startProcessing(self, pcm_cb=None, pulse_cb=None) -> None:
+        def pcm(_u, p, n):
+            if pcm_cb is not None:
+                pcm_cb(np.ctypeslib.as_array(p, shape=(n,)).copy())
+
+        def pulse(_u, strength, live):
+            if pulse_cb is not None:
+                pulse_cb(strength, live)
+
+        self._cbs = _SsbCallbacks(None, CB_SSB_PCM(pcm), CB_SSB_PULSE(pulse))
+        _check(load().sdrg_ssb_processor_start(self._h, ctypes.byref(self._cbs)), "startProcessing")
+
+    def stopProcessing(self) -> None:
+        _check(load().sdrg_ssb_processor_stop(self._h), "stopProcessing")
+
+    def enqueueData(self, iq: np.ndarray, sample_rate: int, fmt: int = CF32) -> None:
+        """iq: one frame of raw samples in `fmt` (CF32: complex64 or interleaved float32)."""
+        a = np.ascontiguousarray(iq)
+        if fmt == CF32 and np.iscomplexobj(a):
+            a = np.ascontiguousarray(a, np.complex64).view(np.float32)
+        a = np.ascontiguousarray(a, NUMPY_DTYPE[fmt])
+        _check(load().sdrg_ssb_processor_enqueue(self._h, a.ctypes.data_as(ctypes.c_void_p), fmt, a.size // 2,
+                                                 sample_rate), "enqueueData")
+
+    def setSoundMode(self, mode: int) -> None:
+        _check(load().sdrg_ssb_processor_set_sound_mode(self._h, mode), "setSoundMode")
+
+    def setPulseConfig(self, cfg: PulseConfig) -> None:
+        _check(load().sdrg_ssb_processor_set_pulse_config(self._h, ctypes.byref(cfg)), "setPulseConfig")
+
+    def getAmbientEnergy(self) -> float:
+        return float(load().sdrg_ssb_processor_get_ambient_energy(self._h))
+
+    def getCurrentRatio(self) -> float:
+        return float(load().sdrg_ssb_processor_get_current_ratio(self._h))
+
+    def drain(self) -> None:
+        _check(load().sdrg_ssb_processor_drain(self._h), "drain")
+
+    def counters(self) -> dict:
+        e, d, p, st = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+        _check(load().sdrg_ssb_processor_counters(self._h, ctypes.byref(e), ctypes.byref(d), ctypes.byref(p),
+                                                  ctypes.byref(st)), "counters")
+        return {"enqueued": e.value, "dropped": d.value, "processed": p.value, "last_status": st.value}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            load().sdrg_ssb_processor_destroy(self._h)
             self._h = None
 
     def __del__(self):

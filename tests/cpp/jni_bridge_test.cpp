@@ -29,11 +29,25 @@ struct FakeEnv {
     std::vector<Call> log;
     int global_refs = 0;
 };
+// the "JVM": the SSB worker thread attaches to it and gets an env of its own (its own call log)
+struct FakeVm {
+    FakeEnv worker_env;
+    int attaches = 0, detaches = 0;
+};
+FakeVm g_vm;
 
 struct FakeJni {
     using Env = FakeEnv;
     using Obj = FakeObj *;
     using Mid = const char *;
+    using Vm = FakeVm *;
+    static Vm VmOf(Env *) { return &g_vm; }
+    static Env *Attach(Vm vm, bool *attached) {
+        vm->attaches++;  // one worker thread: no lock needed
+        *attached = true;
+        return &vm->worker_env;
+    }
+    static void Detach(Vm vm) { vm->detaches++; }
     static Obj NewGlobalRef(Env *e, Obj o) { e->global_refs++; return o; }
     static void DeleteGlobalRef(Env *e, Obj) { e->global_refs--; }
     static Mid MethodOf(Env *, Obj, const char *sig) { return sig; }
@@ -70,11 +84,86 @@ bool same_f(double got, float want) { return (float)got == want || (std::isnan(g
 
 }  // namespace
 
+void synth(std::vector<std::complex<float>> &buf, int f, int n, int64_t fs, uint64_t &x) {
+    for (int i = 0; i < n; i++) {  // keyed +2 kHz carrier over pseudo-random noise
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        const double t = (double)((int64_t)f * n + i) / fs;
+        const double a = (std::fmod(t, 0.45) < 0.08) ? 0.3 : 0.02;
+        const double ph = 2 * M_PI * 2000.0 * t;
+        buf[i] = {(float)(a * std::cos(ph) + ((double)(x & 0xffff) / 65536.0 - 0.5) * 0.05),
+                  (float)(a * std::sin(ph) + ((double)((x >> 16) & 0xffff) / 65536.0 - 0.5) * 0.05)};
+    }
+}
+
+// QUEUED mode (the reference's SSBProcessor): soapyCallback's 10 callbacks on the frame's thread, pcm + audioPulse
+// from the SSB worker thread (attached per call).  Draining the worker after every frame drops nothing, so the
+// worker's callbacks must equal the C ABI engine's SSB outputs frame for frame.
+int queued_phase() {
+    const int n = 4096, frames = 60;
+    const int64_t fs = 2000000, cf = 100000000;
+    FakeEnv env;
+    g_vm = FakeVm{};
+    B bridge;
+    if (!bridge.applyConfig(&env, cf, fs, n, 5, 10, 50, 200, 30, 1)) return 12;
+    FakeObj objs[B::N_CALLBACKS];
+    B::Obj cbs[B::N_CALLBACKS];
+    for (int i = 0; i < B::N_CALLBACKS; i++) {
+        objs[i].id = i;
+        cbs[i] = &objs[i];
+    }
+    bridge.read(&env, cbs);
+    sdrg_config c{cf, fs, n, 5, 10, 1, 50, 200, 30};
+    sdrg_engine *ref = nullptr;
+    if (sdrg_engine_create(&c, 1, 0, &ref)) return 13;
+    std::vector<float> spec(n);
+    std::vector<int16_t> pcm((size_t)sdrg_engine_pcm_len(ref));
+    sdrg_frame_record rec;
+    sdrg_pulse_output sp, ap;
+    std::vector<std::complex<float>> buf(n);
+    uint64_t x = 777;
+    for (int f = 0; f < frames; f++) {
+        synth(buf, f, n, fs, x);
+        env.log.clear();
+        g_vm.worker_env.log.clear();
+        const int64_t now = 1000 + 2 * f;
+        bridge.onFrame(&env, buf.data(), n, now);
+        bridge.drainSsb();
+        CHECK(bridge.lastStatus() == 0, "queued frame %d status %d", f, bridge.lastStatus());
+        if (sdrg_engine_process_host(ref, buf.data(), SDRG_IQ_CF32, SDRG_STAGE_ALL, spec.data(), &rec, pcm.data(), now))
+            return 14;
+        if (sdrg_engine_get_pulse_outputs(ref, &sp, &ap)) return 15;
+        CHECK(env.log.size() == 10, "queued frame %d: %zu frame-thread calls", f, env.log.size());
+        CHECK(g_vm.worker_env.log.size() == 2, "queued frame %d: %zu worker calls", f, g_vm.worker_env.log.size());
+        if (env.log.size() != 10 || g_vm.worker_env.log.size() != 2) continue;
+        CHECK(std::memcmp(env.log[0].floats.data(), spec.data(), 4 * n) == 0, "queued fft payload frame %d", f);
+        CHECK(same_f(env.log[9].args[0], rec.best1khz_snr_sigma) && env.log[9].args[1] == sp.live_etat,
+              "queued spectralPulse frame %d", f);
+        const Call &pc = g_vm.worker_env.log[0], &pu = g_vm.worker_env.log[1];
+        CHECK(pc.cb == B::PCM && pc.sig == B::kSignature[B::PCM] && pc.shorts == pcm, "queued pcm frame %d", f);
+        CHECK(pu.cb == B::AUDIO_PULSE && same_f(pu.args[0], ap.strength) && pu.args[1] == ap.live_etat,
+              "queued audioPulse frame %d", f);
+    }
+    int64_t enq, drop, proc;
+    bridge.ssbCounters(&enq, &drop, &proc);
+    CHECK(enq == frames && drop == 0 && proc == frames, "ssb counters %lld %lld %lld", (long long)enq,
+          (long long)drop, (long long)proc);
+    CHECK(bridge.getAmbientAudioEnergy(&env) == ap.strength, "queued ambient energy");
+    CHECK(bridge.getCurrentAudioRatio(&env) == 0.f, "current audio ratio");
+    CHECK(g_vm.attaches == g_vm.detaches && g_vm.attaches == 2 * frames, "attach/detach %d %d", g_vm.attaches,
+          g_vm.detaches);
+    bridge.stopReading(&env);
+    bridge.close(&env);
+    CHECK(env.global_refs == 0, "queued global refs after close %d", env.global_refs);
+    sdrg_engine_destroy(ref);
+    return 0;
+}
+
 int main() {
     const int n = 4096, frames = 180;
     const int64_t fs = 2000000, cf = 100000000;
     FakeEnv env;
     B bridge;
+    bridge.setSsbMode(B::SsbMode::SYNCHRONOUS);
     if (!bridge.applyConfig(&env, cf, fs, n, 5, 10, 50, 200, 30, 1)) {
         std::fprintf(stderr, "applyConfig failed: %s\n", sdrg_last_error());
         return 2;
@@ -108,14 +197,7 @@ int main() {
             bridge.setSoundMode(&env, 2);
             sdrg_engine_set_sound_mode(ref, 2);
         }
-        for (int i = 0; i < n; i++) {  // keyed +2 kHz carrier over pseudo-random noise
-            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
-            const double t = (double)(f * n + i) / fs;
-            const double a = (std::fmod(t, 0.45) < 0.08) ? 0.3 : 0.02;
-            const double ph = 2 * M_PI * 2000.0 * t;
-            buf[i] = {(float)(a * std::cos(ph) + ((double)(x & 0xffff) / 65536.0 - 0.5) * 0.05),
-                      (float)(a * std::sin(ph) + ((double)((x >> 16) & 0xffff) / 65536.0 - 0.5) * 0.05)};
-        }
+        synth(buf, f, n, fs, x);
         env.log.clear();
         const int64_t now = 1000 + 2 * f;
         bridge.onFrame(&env, buf.data(), n, now);
@@ -158,7 +240,10 @@ int main() {
     CHECK(env.global_refs == 0, "global refs after close %d", env.global_refs);
     sdrg_engine_destroy(ref);
     if (fails) return 1;
-    std::printf("OK %d frames, %d callbacks each, spectral live %d, audio live %d\n", frames, 12, sp.live_etat,
-                ap.live_etat);
+    const int q = queued_phase();
+    if (q) return q;
+    if (fails) return 1;
+    std::printf("OK %d frames, %d callbacks each, spectral live %d, audio live %d; queued SSB worker OK\n", frames, 12,
+                sp.live_etat, ap.live_etat);
     return 0;
 }
