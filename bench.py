@@ -36,6 +36,11 @@ NCO_HZ = 250e3  # --ssb-variant nco127: the NCO offset of the BASELINE configs[2
 B = 4096
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 ALG_BYTES_PER_SAMPLE = {"spectrum": 6.0}  # CS8: 2 B in + 4 B fftshifted float32 power out
+N_INPUTS = 3  # distinct input batches rotated per step: 3 x 128 MiB > the 256 MiB Infinity Cache
+# SSB latency floor: the low-pass recurrence's dependent chain, measured in-kernel at 39 cycles per sample
+# (s_memtime stamps), at the chip's 2.4 GHz maximum clock: no schedule finishes a frame sooner
+SSB_CHAIN_CYCLES = 39
+MAX_CLOCK_GHZ = 2.4
 
 
 def log(msg: str) -> None:
@@ -89,6 +94,21 @@ def d2d_copy_gbs(torch, dev, nbytes: int = 1 << 30, reps: int = 10) -> float:
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
+def host_cores() -> tuple[int, str]:
+    """Cores this process may use: its CPU affinity, capped by the cgroup CPU quota when one is set (a GPU box
+    shows the whole machine's CPUs in the affinity mask but grants this job a share of them)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, f"sched_getaffinity {aff}" + (f", cgroup cpu.max quota {quota}" if quota else "")
+
+
 def cpu_baseline(threads: int, target_cpu_s: float = 15.0) -> dict:
     """The oracle (our C restatement of the reference path: FFT + stats + SSB + pulse detectors per frame), one fresh stream per
     frame, timed on the host cores with `threads` worker threads (ctypes releases the GIL)."""
@@ -121,7 +141,8 @@ def cpu_baseline(threads: int, target_cpu_s: float = 15.0) -> dict:
     return {"value": round(total * N / wall / 1e6, 3), "unit": "IQ Msamples/s", "cores": threads, "kind": "port",
             "sample": f"{total} frames x {N} CS8 samples (FFT+stats+SSB+pulse detectors per frame, fresh stream "
                       "each), "
-                      f"{threads} threads, {wall:.2f} s wall, {per_frame * 1e3:.3f} ms/frame single-thread"}
+                      f"{threads} threads = every host core granted ({host_cores()[1]}), {wall:.2f} s wall, "
+                      f"{per_frame * 1e3:.3f} ms/frame single-thread"}
 
 
 def main() -> int:
@@ -131,7 +152,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--streams", type=int, default=B)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 (default): every core granted (host_cores)")
+    ap.add_argument("--no-labelled", action="store_true", help="skip the labelled configs[1]/configs[2] legs")
     ap.add_argument("--pipelined", type=int, default=1,
                     help="1 (default): each step's SSB stages run beside the next step's spectrum (all work of every "
                          "step is done; sdrg_engine_set_pipelining); 0: each step joins its SSB stream")
@@ -187,7 +209,9 @@ def main() -> int:
     variant = args.ssb_variant != "reference"
     if variant:
         eng.set_ssb_variant(NCO_HZ, 127)
-    iq = synth_device_frames(torch, dev, streams, seed=0x5D12 + rank, n=n, cs16=c5)
+    # N_INPUTS distinct batches rotated per step, so no step reads inputs the Infinity Cache kept from the last
+    iqs = [synth_device_frames(torch, dev, streams, seed=0x5D12 + 7919 * rank + k, n=n, cs16=c5)
+           for k in range(N_INPUTS)]
     spec = torch.empty((streams, n), dtype=torch.float32, device=dev)
     rec = torch.zeros((streams, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
     plen = eng.pcm_len
@@ -217,8 +241,13 @@ def main() -> int:
         torch.cuda.set_stream(work_stream)
         eng.set_stream(work_stream.cuda_stream)
 
-    def step():
-        eng.process_device(iq.data_ptr(), fmt, stages, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(), now[0])
+    calls = [0]
+
+    def step(st=None):
+        iq = iqs[calls[0] % N_INPUTS]
+        calls[0] += 1
+        eng.process_device(iq.data_ptr(), fmt, stages if st is None else st, spec.data_ptr(), rec.data_ptr(),
+                           pcm.data_ptr(), now[0])
         now[0] += n // 2000  # frame duration in ms at 2 Msps (8 ms for 16384)
         if world > 1:
             shard.gather_records(host(rec), world, rank, dst=0, out=gathered)  # records (peaks, stats) to rank 0
@@ -258,11 +287,46 @@ def main() -> int:
     eng.set_pipelining(False)
     eng.synchronize()
     eng.reset_timing_stats()
-    for _ in range(10):
-        eng.process_device(iq.data_ptr(), fmt, sdrg.STAGE_SPECTRUM, spec.data_ptr(), None, None, now[0])
+    for k in range(10):
+        eng.process_device(iqs[k % N_INPUTS].data_ptr(), fmt, sdrg.STAGE_SPECTRUM, spec.data_ptr(), None, None, now[0])
     eng.synchronize()
     spec_iso_ms = eng.timing_stats()["spectrum_ms"]
+    ssb_iso_ms = None
+    if args.stages == "all":  # the SSB stage alone (nothing else on the chip), for its latency-floor fraction
+        eng.reset_timing_stats()
+        for k in range(10):
+            eng.process_device(iqs[k % N_INPUTS].data_ptr(), fmt, sdrg.STAGE_SSB, None, None, pcm.data_ptr(), now[0])
+        eng.synchronize()
+        ssb_iso_ms = eng.timing_stats()["ssb_ms"]
     d2d = d2d_copy_gbs(torch, dev)
+
+    def labelled_rate(st, k_steps, variant_on=False):
+        """A separately labelled line measured in this same run: k_steps pipelined steps of stages st."""
+        if variant_on:
+            eng.set_ssb_variant(NCO_HZ, 127)
+        eng.set_pipelining(pipelined)
+        for _ in range(3):
+            step(st)
+        eng.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(k_steps):
+            step(st)
+        eng.synchronize()
+        dt = time.perf_counter() - t1
+        if variant_on:
+            eng.set_ssb_variant(0.0, 0)
+        return {"value": round(k_steps * streams * n / dt / 1e6, 2), "ms_per_step": round(dt / k_steps * 1e3, 4)}
+
+    labelled = {}
+    if world == 1 and args.config == "c3" and args.stages == "all" and not variant and not args.no_labelled:
+        eng.set_profiling(False)
+        labelled["configs1_fft_stats"] = dict(labelled_rate(sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS, args.steps),
+                                              workload="BASELINE configs[1]: same batch, FFT + |X|^2 + fftshift + "
+                                                       "log-mag/peak/signal-strength stats, no SSB")
+        labelled["configs2_nco127"] = dict(labelled_rate(sdrg.STAGE_ALL, args.steps, variant_on=True),
+                                           workload="BASELINE configs[2] as written (a build extension, not the "
+                                                    f"reference chain): SSB with an NCO mixer at +{NCO_HZ / 1e3:g} kHz "
+                                                    "+ 127-tap FIR decim 41, every other stage as the headline")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -286,6 +350,10 @@ def main() -> int:
                f"|X|^2 + fftshift + signal-strength stats over a {focus_khz} kHz focus; no SSB"),
     }[args.config]
     achieved_iso = alg_bytes / (spec_iso_ms * 1e-3) / 1e9 if spec_iso_ms > 0 else 0.0
+    # whole-step algorithmic bytes: IQ in + spectra out + 72-B records + PCM out (~6.05 B/sample CS8)
+    in_bps = 4.0 if c5 else 2.0
+    step_bytes = streams * n * (in_bps + 4.0) + streams * (sdrg.RECORD_DTYPE.itemsize + 2 * plen * (args.stages == "all"))
+    step_gbs = step_bytes / (ms_per_step * 1e-3) / 1e9
     out = {
         "metric": "IQ Msamples/s (16384-pt FFT+SSB) at 1/2/4/8 GPUs; % HBM roofline",
         "value": round(value, 2),
@@ -326,8 +394,26 @@ def main() -> int:
                                                                 "per second (SURVEY 8d's measured peak)",
                          "frac_timed": round(achieved / d2d, 4) if d2d else None,
                          "frac_isolated": round(achieved_iso / d2d, 4) if d2d else None},
+        "roofline_step": {"bound": "hbm", "achieved": round(step_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(step_gbs / HBM_PEAK_GBS, 4),
+                          "bytes_per_sample": round(step_bytes / (streams * n), 4),
+                          "measured": "whole-step algorithmic bytes (IQ in, spectra, records, PCM out) / ms_per_step"},
         "pipelined": pipelined,
+        "inputs": f"{N_INPUTS} distinct {streams}x{n} {fmt_name} batches ({N_INPUTS * streams * n * in_bps / 2**20:.0f} "
+                  "MiB) rotated per step in every leg, so inputs are not served from the 256 MiB Infinity Cache",
     }
+    if ssb_iso_ms:
+        floor_ms = n * SSB_CHAIN_CYCLES / (MAX_CLOCK_GHZ * 1e9) * 1e3
+        out["ssb_latency_floor"] = {
+            "kernel": "ssb_pipe_kernel (the reference's sample-serial SSB chain, bit-exact)",
+            "bound": "latency", "floor_ms": round(floor_ms, 4),
+            "basis": f"{n} samples x {SSB_CHAIN_CYCLES} cycles (the low-pass recurrence's dependent chain, "
+                     f"measured in-kernel) / {MAX_CLOCK_GHZ} GHz max clock",
+            "ssb_ms_alone": round(ssb_iso_ms, 4), "frac_alone": round(floor_ms / ssb_iso_ms, 4),
+            "ssb_ms_coresident": round(ts["ssb_ms"], 4),
+            "frac_coresident": round(floor_ms / ts["ssb_ms"], 4) if ts["ssb_ms"] > 0 else None}
+    if labelled:
+        out["labelled"] = labelled
     if rehearse:
         out["rehearsal"] = "gloo, every rank on cuda:0: a functional check of the N > 1 path, not a measurement"
     if variant:
@@ -339,7 +425,7 @@ def main() -> int:
     if (rank == 0 and world == 1 and not args.no_cpu_baseline and args.stages == "all" and not variant
             and args.config == "c3"):
         try:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_threads or host_cores()[0])
         except Exception as exc:  # the baseline is informative; never fail the bench line on it
             out["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:

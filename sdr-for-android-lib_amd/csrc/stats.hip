@@ -246,6 +246,7 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
     StatsState st = state[frame];
     if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
     sdrg_frame_record rec;
+    __builtin_memset(&rec, 0, sizeof(rec));  // tail padding included: records compare and gather as bytes
     rec.peak_bin = -1;
     rec.abs_peak_db = -130.0f;
     rec.signal_power_db = 0.0f;

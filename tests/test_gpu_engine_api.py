@@ -208,4 +208,4 @@ def test_engines_in_concurrent_threads(S, O):
     for k in range(2):
         for f in range(2):
             for a, b in zip(results[k][f], want[f]):
-                assert a.tobytes() == b.tobytes()
+                assert a.tobytes() == b.tobytes()  # records included: their tail padding is written as zeros
