@@ -38,7 +38,7 @@ extern "C" {
 typedef enum sdrg_status {
     SDRG_OK = 0,
     SDRG_E_INVALID = -1,      /* bad argument (null pointer, non-positive size, ...) */
-    SDRG_E_UNSUPPORTED = -2,  /* e.g. a spectrum of a size the FFT kernels do not cover */
+    SDRG_E_UNSUPPORTED = -2,  /* e.g. a frame size outside [1, 2^20] */
     SDRG_E_NOMEM = -3,        /* device allocation failed */
     SDRG_E_HIP = -4,          /* a HIP runtime call failed (message via sdrg_last_error) */
     SDRG_E_NODEVICE = -5      /* no gfx950 device / HIP runtime not usable */
@@ -75,8 +75,8 @@ enum {
 typedef struct sdrg_config {
     int64_t center_frequency;          /* Hz; the reference stores it as uint32 (bridge-config.h:18) */
     int64_t sample_rate;               /* Hz; uint32 in the reference */
-    int32_t samples_per_reading;       /* frame size N: any N in [1, 2^20] for SSB; the spectrum needs a
-                                          power of two in [64, 65536] (SDRBridge.kt:25 recommends multiples of 512) */
+    int32_t samples_per_reading;       /* frame size N: any N in [1, 2^20] (fftwf_plan_dft_1d plans any N,
+                                          fft_process.cpp:77-79; SDRBridge.kt:25 recommends multiples of 512) */
     int32_t freq_focus_range_khz;      /* focus half-width X in kHz */
     int32_t gain;
     int32_t sound_mode;                /* 0,1,2 (SDRBridge.kt:35-36); other values keep the last mode */

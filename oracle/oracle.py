@@ -153,7 +153,7 @@ def unpack(fmt: int, raw: np.ndarray, n: int) -> np.ndarray:
 def power_shifted(iq: np.ndarray, use_f64: bool = False) -> np.ndarray:
     iq = np.ascontiguousarray(iq, dtype=np.float32).reshape(-1)
     n = iq.size // 2
-    out = np.empty(n, dtype=np.float32)
+    out = np.zeros(n, dtype=np.float32)  # a fresh vector: for odd n element n-1 is never written (stays 0)
     rc = lib().oracle_power_shifted(_ptr(iq), n, int(use_f64), _ptr(out))
     assert rc == 0, rc
     return out
@@ -193,11 +193,18 @@ class FftState:
     def process(self, iq: np.ndarray, now_ms: int, use_f64: bool = False):
         iq = np.ascontiguousarray(iq, dtype=np.float32).reshape(-1)
         n = iq.size // 2
-        spec = np.empty(n, dtype=np.float32)
+        # power_shifted_vec persists across frames (fft_process.h:59): resize keeps its prefix, new elements are 0
+        # (for odd n the shift never writes element n-1, which keeps the vector's old value)
+        old = getattr(self, "_vec", None)
+        if old is None or old.size != n:
+            self._vec = np.zeros(n, dtype=np.float32)
+            if old is not None:
+                k = min(n, old.size)
+                self._vec[:k] = old[:k]
         rec = np.zeros(1, dtype=RECORD_DTYPE)
-        rc = lib().oracle_fft_process(_ptr(self.buf), _ptr(iq), n, now_ms, int(use_f64), _ptr(spec), _ptr(rec))
+        rc = lib().oracle_fft_process(_ptr(self.buf), _ptr(iq), n, now_ms, int(use_f64), _ptr(self._vec), _ptr(rec))
         assert rc == 0, rc
-        return spec, rec[0]
+        return self._vec.copy(), rec[0]
 
 
 def lpf_coefs(fs: float, fc: float, q: float) -> np.ndarray:

@@ -161,17 +161,66 @@ ORACLE_API int oracle_fft_f64(double *re, double *im, int n) {
     return 0;
 }
 
+/* Forward DFT in double for ANY n >= 1 (FFTW plans every size, fft_process.cpp:77-79): the radix-2 transform above
+ * for powers of two; otherwise Bluestein's chirp-z over the power of two M >= 2n - 1, X_k = conj(b_k) sum_j
+ * (x_j conj(b_j)) b_(k-j) with b_m = exp(i pi m^2 / n) (m^2 reduced mod 2n exactly), the convolution done with
+ * three double FFTs.  Relative error ~1e-15 of the frame's energy: an accuracy reference, like the pow-2 path. */
+ORACLE_API int oracle_dft_f64_any(double *re, double *im, int n) {
+    if (n < 1) return -1;
+    if (is_pow2(n)) return oracle_fft_f64(re, im, n);
+    int m = 1;
+    while (m < 2 * n - 1) m <<= 1;
+    double *br = (double *)malloc(sizeof(double) * (size_t)n), *bi = (double *)malloc(sizeof(double) * (size_t)n);
+    double *ar = (double *)calloc((size_t)m, sizeof(double)), *ai = (double *)calloc((size_t)m, sizeof(double));
+    double *cr = (double *)calloc((size_t)m, sizeof(double)), *ci = (double *)calloc((size_t)m, sizeof(double));
+    if (!br || !bi || !ar || !ai || !cr || !ci) {
+        free(br); free(bi); free(ar); free(ai); free(cr); free(ci);
+        return -3;
+    }
+    for (int64_t k = 0; k < n; k++) {
+        const int64_t q = (k * k) % (2 * (int64_t)n);
+        const double t = M_PI * (double)q / (double)n;
+        br[k] = cos(t);
+        bi[k] = sin(t);
+    }
+    for (int k = 0; k < n; k++) {  /* a = x conj(b) */
+        ar[k] = re[k] * br[k] + im[k] * bi[k];
+        ai[k] = im[k] * br[k] - re[k] * bi[k];
+    }
+    cr[0] = br[0];
+    ci[0] = bi[0];
+    for (int k = 1; k < n; k++) {
+        cr[k] = cr[m - k] = br[k];
+        ci[k] = ci[m - k] = bi[k];
+    }
+    oracle_fft_f64(ar, ai, m);
+    oracle_fft_f64(cr, ci, m);
+    for (int k = 0; k < m; k++) {  /* conj(A C) for the inverse through a forward transform */
+        const double pr = ar[k] * cr[k] - ai[k] * ci[k], pi = ar[k] * ci[k] + ai[k] * cr[k];
+        ar[k] = pr;
+        ai[k] = -pi;
+    }
+    oracle_fft_f64(ar, ai, m);
+    for (int k = 0; k < n; k++) {  /* X_k = conj(b_k) conj(.)/m */
+        const double zr = ar[k] / m, zi = -ai[k] / m;
+        re[k] = zr * br[k] + zi * bi[k];
+        im[k] = zi * br[k] - zr * bi[k];
+    }
+    free(br); free(bi); free(ar); free(ai); free(cr); free(ci);
+    return 0;
+}
+
 /* fft_process.cpp:77-97: FFT of the CF32 frame, power[i] = re*re + im*im (float), then fftshift.
  * use_f64 != 0 computes the transform in double and rounds X to float before the power. */
 ORACLE_API int oracle_power_shifted(const float *iq, int n, int use_f64, float *out_shifted) {
-    if (!iq || !out_shifted || !is_pow2(n)) return -1;
+    if (!iq || !out_shifted || n < 1) return -1;
     float *power = (float *)malloc(sizeof(float) * (size_t)n);
     if (!power) return -3;
-    if (use_f64) {
+    if (use_f64 || !is_pow2(n)) {  /* sizes the float radix-2 restatement does not cover: the double DFT */
         double *re = (double *)malloc(sizeof(double) * (size_t)n), *im = (double *)malloc(sizeof(double) * (size_t)n);
         if (!re || !im) { free(re); free(im); free(power); return -3; }
         for (int i = 0; i < n; i++) { re[i] = iq[2 * i]; im[i] = iq[2 * i + 1]; }
-        oracle_fft_f64(re, im, n);
+        oracle_dft_f64_any(re, im, n);
         for (int i = 0; i < n; i++) {
             const float xr = (float)re[i], xi = (float)im[i];
             power[i] = xr * xr + xi * xi;
@@ -185,7 +234,9 @@ ORACLE_API int oracle_power_shifted(const float *iq, int n, int use_f64, float *
         for (int i = 0; i < n; i++) power[i] = re[i] * re[i] + im[i] * im[i];   /* :83-86 */
         free(re); free(im);
     }
-    const int half = n / 2;                                                        /* :92-97 */
+    /* :92-97; for odd n the loop leaves out_shifted[n-1] as it was (the reference's vector keeps its old value)
+     * and drops power[n-1] */
+    const int half = n / 2;
     for (int i = 0; i < half; i++) {
         out_shifted[i] = power[i + half];
         out_shifted[i + half] = power[i];

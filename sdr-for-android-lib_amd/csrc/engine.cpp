@@ -163,6 +163,8 @@ struct sdrg_engine {
     float *d_fft_scratch = nullptr;   // four-step intermediate (N > 16384)
     size_t fft_scratch_elems = 0;
     sdrg_frame_record *d_rec_scratch = nullptr;
+    float *d_pool = nullptr;          // statistics' pooled bins beyond the LDS bound (wide focus, N > 65536)
+    size_t pool_elems = 0;
     // host-path staging
     void *d_iq_stage = nullptr;
     size_t iq_stage_bytes = 0;
@@ -221,13 +223,14 @@ int32_t validate_config(const sdrg_config *cfg) {
 }
 
 template <typename T>
-int32_t ensure_device(T **p, size_t *have, size_t need) {
+int32_t ensure_device(T **p, size_t *have, size_t need, bool zero = false) {
     if (*have >= need && *p) return SDRG_OK;
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     *have = 0;
     if (need == 0) return SDRG_OK;
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(p), need * sizeof(T)));
+    if (zero) HIP_TRY(hipMemset(*p, 0, need * sizeof(T)));
     *have = need;
     return SDRG_OK;
 }
@@ -434,7 +437,9 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
 
     float *spec = spectra;
     if (do_spec && !spec) {
-        int32_t rc = ensure_device(&e->d_spec_scratch, &e->spec_scratch_elems, (size_t)B * n);
+        // zeroed: for odd N the reference never writes power_shifted[N-1] (fft_process.cpp:92-97), which keeps the
+        // value its vector held -- 0 for a fresh vector, the same stream's last value afterwards
+        int32_t rc = ensure_device(&e->d_spec_scratch, &e->spec_scratch_elems, (size_t)B * n, true);
         if (rc) return rc;
         spec = e->d_spec_scratch;
     }
@@ -466,7 +471,8 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         if (e->fft_fs == 0) return fail(SDRG_E_INVALID, "the statistics' sample rate is 0");
         geo = stats_geometry(e->fft_fs, e->fft_fc, n, e->fft_focus);
         geo.cf_changed = e->cf_changed_pending ? 1 : 0;
-        if (geo.max_pool > 16384) return fail(SDRG_E_UNSUPPORTED, "pooled noise bins %d > 16384", geo.max_pool);
+        int32_t rc = ensure_device(&e->d_pool, &e->pool_elems, stats_global_pool_floats(geo, B));
+        if (rc) return rc;
     }
 
     // last of the checks and allocations: the SSB control statics of this call (committed at the end)
@@ -532,7 +538,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
     }
     if (do_stats) {
-        HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->s_main));
+        HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->d_pool, e->s_main));
         if (do_sp) {  // spectralPulseDetector.process(best1kHzSnrSigma, best1kHzCenterFreqHz) (:477-479)
             int32_t rc = pulse_bank_spectral(&e->spec_bank, &recs->best1khz_snr_sigma, &recs->best1khz_center_freq_hz,
                                              (int)sizeof(sdrg_frame_record), e->spec_bank.d_out, e->s_main);
@@ -698,7 +704,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (e->s_main) (void)hipStreamSynchronize(e->s_main);
     if (e->s_ssb) (void)hipStreamSynchronize(e->s_ssb);
     e->spec_bank.last_stream = e->audio_bank.last_stream = nullptr;  // drained above
-    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_nco_tab, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch,
+    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_nco_tab, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch, e->d_pool,
                     e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -958,7 +964,7 @@ int32_t sdrg_engine_process_host(sdrg_engine *e, const void *iq, int32_t format,
     const bool do_spec = stages & SDRG_STAGE_SPECTRUM, do_stats = stages & SDRG_STAGE_STATS,
                do_ssb = stages & SDRG_STAGE_SSB;
     if (do_spec) {
-        int32_t rc = ensure_device(&e->d_spec_stage, &e->spec_stage_elems, (size_t)B * n);
+        int32_t rc = ensure_device(&e->d_spec_stage, &e->spec_stage_elems, (size_t)B * n, true);  // see enqueue
         if (rc) return rc;
     }
     if (do_stats && !e->d_rec_stage)

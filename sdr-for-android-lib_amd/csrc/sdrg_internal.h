@@ -39,8 +39,9 @@ private:
 // ------------------------------------------------------------------------------------------------
 // Launchers (defined in the .hip translation units).  All are asynchronous on `stream`.
 // ------------------------------------------------------------------------------------------------
-// Spectrum kernels: N <= 16384 one LDS-resident workgroup per frame; N = 32768/65536 two-kernel four-step
-// in waves of SPECTRUM_WAVE_FRAMES frames (intermediate in `scratch`, spectrum_scratch_floats() floats).
+// Spectrum kernels, every N in [1, 2^20]: powers of two 64 .. 16384 one LDS-resident workgroup per frame,
+// 32768/65536 two-kernel four-step in waves of SPECTRUM_WAVE_FRAMES frames (intermediate in `scratch`,
+// spectrum_scratch_floats() floats); every other N through fftany.hip (mixed radix, four-step, Bluestein).
 constexpr int SPECTRUM_WAVE_FRAMES = 128;
 bool spectrum_supported(int n);
 size_t spectrum_scratch_floats(int n, int n_frames);
@@ -54,8 +55,11 @@ void spectrum_fill_twiddles(int n, float *out);
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles,
                            float *spectra, float *scratch, hipStream_t stream, bool beside_ssb = false);
 
+// gpool: [n_frames][stats_global_pool_floats / n_frames] device scratch for the pooled-bin median when the
+// pool exceeds what the kernel keeps in LDS (stats_global_pool_floats > 0; wide focus windows at N > 65536)
+size_t stats_global_pool_floats(const StatsGeometry &geo, int n_frames);
 hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry &geo, int64_t now_ms,
-                        StatsState *state, sdrg_frame_record *records, hipStream_t stream);
+                        StatsState *state, sdrg_frame_record *records, float *gpool, hipStream_t stream);
 
 // SSB chain.  The pipelined kernel needs no scratch; the lane-per-stream reference kernels (used for
 // sample rates below ~0.9 MHz, or when SDRG_SSB_REFERENCE_KERNELS=1) need

@@ -27,141 +27,15 @@
 #include <type_traits>
 #include <vector>
 
+#include "fftany.h"
 #include "sdrg_internal.h"
 
 namespace sdrg {
 namespace {
 
-typedef float f2 __attribute__((ext_vector_type(2)));
+#include "fft_codelets.h"
 
 constexpr int E = 32;  // complex values per thread
-
-// exp(-2 pi i k / 32), k in [0, 16)
-__device__ constexpr float W32_RE[16] = {1.0f, 0.980785251f, 0.923879504f, 0.831469595f, 0.707106769f,
-                                         0.555570245f, 0.382683426f, 0.195090324f, 0.0f, -0.195090324f,
-                                         -0.382683426f, -0.555570245f, -0.707106769f, -0.831469595f,
-                                         -0.923879504f, -0.980785251f};
-__device__ constexpr float W32_IM[16] = {-0.0f, -0.195090324f, -0.382683426f, -0.555570245f, -0.707106769f,
-                                         -0.831469595f, -0.923879504f, -0.980785251f, -1.0f, -0.980785251f,
-                                         -0.923879504f, -0.831469595f, -0.707106769f, -0.555570245f,
-                                         -0.382683426f, -0.195090324f};
-
-template <int R>
-__device__ __forceinline__ constexpr int bitrev(int i) {
-    int r = 0;
-    for (int b = 1; b < R; b <<= 1) {
-        r = (r << 1) | (i & 1);
-        i >>= 1;
-    }
-    return r;
-}
-
-template <int FMT>
-constexpr int bytes_per_sample() {
-    return FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2;
-}
-
-// ------------------------------------------------------------------------------------------------
-// Packed complex helpers (f2 = {re, im} in one 64-bit register pair)
-// ------------------------------------------------------------------------------------------------
-// a + (-i) b = (a.x + b.y, a.y - b.x)
-__device__ __forceinline__ f2 add_mi(f2 a, f2 b) {
-    f2 r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-// a - (-i) b = (a.x - b.y, a.y + b.x)
-__device__ __forceinline__ f2 sub_mi(f2 a, f2 b) {
-    f2 r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-// (b.x + b.y, b.y - b.x) = b (1 - i) = b W32^4 / c, c = 1/sqrt2
-__device__ __forceinline__ f2 rot45(f2 b) {
-    f2 r;
-    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b));
-    return r;
-}
-// a + c (-i) s = (a.x + c s.y, a.y - c s.x)
-__device__ __forceinline__ f2 fma_mi(f2 s, f2 c, f2 a) {
-    f2 r;
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]" : "=v"(r) : "v"(s), "v"(c), "v"(a));
-    return r;
-}
-// a - c (-i) s = (a.x - c s.y, a.y + c s.x)
-__device__ __forceinline__ f2 fma_pi(f2 s, f2 c, f2 a) {
-    f2 r;
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(s), "v"(c), "v"(a));
-    return r;
-}
-// a * w for a twiddle w held in registers: (a.x w.x, a.x w.y), then + (-a.y w.y, a.y w.x) with the swap
-// and the sign as operand modifiers (the compiler otherwise materialises (-w.y, w.x) with v_xor + v_mov)
-__device__ __forceinline__ f2 cmul_v(f2 a, f2 w) {
-    f2 u, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(u) : "v"(a), "v"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(w), "v"(u));
-    return r;
-}
-
-// radix-2 butterfly with twiddle W32^t on b: (a + W b, a - W b)
-template <int t>
-__device__ __forceinline__ void bfly(f2 &a, f2 &b) {
-    constexpr float C = 0.707106769f;
-    if constexpr (t == 0) {
-        const f2 x = a + b, y = a - b;
-        a = x; b = y;
-    } else if constexpr (t == 8) {
-        const f2 x = add_mi(a, b), y = sub_mi(a, b);
-        a = x; b = y;
-    } else if constexpr (t == 4) {
-        const f2 s = rot45(b);
-        const f2 x = a + s * f2{C, C}, y = a - s * f2{C, C};
-        a = x; b = y;
-    } else if constexpr (t == 12) {
-        const f2 s = rot45(b);
-        const f2 x = fma_mi(s, f2{C, C}, a), y = fma_pi(s, f2{C, C}, a);
-        a = x; b = y;
-    } else {
-        // x = a + b W as two fmas (b.x W, then b.y iW), y = 2a - x: three packed ops instead of four
-        const f2 w = {W32_RE[t], W32_IM[t]}, wi = {-W32_IM[t], W32_RE[t]};
-        const f2 x = (a + b.xx * w) + b.yy * wi;
-        const f2 y = a * f2{2.0f, 2.0f} - x;
-        a = x; b = y;
-    }
-}
-
-template <int R, int LEN, int BASE, int K>
-__device__ __forceinline__ void stage_k(f2 (&v)[R]) {
-    if constexpr (K < LEN / 2) {
-        bfly<K * (32 / LEN)>(v[BASE + K], v[BASE + K + LEN / 2]);
-        stage_k<R, LEN, BASE, K + 1>(v);
-    }
-}
-template <int R, int LEN, int BASE>
-__device__ __forceinline__ void stage(f2 (&v)[R]) {
-    if constexpr (BASE < R) {
-        stage_k<R, LEN, BASE, 0>(v);
-        stage<R, LEN, BASE + LEN>(v);
-    }
-}
-template <int R, int LEN>
-__device__ __forceinline__ void stages(f2 (&v)[R]) {
-    if constexpr (LEN <= R) {
-        stage<R, LEN, 0>(v);
-        stages<R, LEN * 2>(v);
-    }
-}
-
-// In-register DFT of R points (R | 32), natural order in and out (radix-2 DIT, bit reversal = renaming).
-template <int R>
-__device__ __forceinline__ void dft(f2 (&v)[R]) {
-    f2 w[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) w[bitrev<R>(i)] = v[i];
-    stages<R, 2>(w);
-#pragma unroll
-    for (int i = 0; i < R; ++i) v[i] = w[i];
-}
 
 // ------------------------------------------------------------------------------------------------
 // Samples
@@ -813,7 +687,10 @@ static void fill_pass_tables(std::vector<float> &tw, size_t at) {
 // evaluated in double and rounded once to float.
 size_t spectrum_k16_tables_offset() { return 2 * (size_t)16384; }
 
+static bool pow2_kernels(int n) { return n >= 64 && n <= 65536 && (n & (n - 1)) == 0; }
+
 size_t spectrum_twiddle_floats(int n) {
+    if (!pow2_kernels(n)) return any_table_floats(any_plan(n));  // fftany.hip
     size_t pass = 0;
     if (n == 16384) return spectrum_k16_tables_offset() + k16::TAB_FLOATS;
     switch (n) {
@@ -828,6 +705,10 @@ size_t spectrum_twiddle_floats(int n) {
 }
 
 void spectrum_fill_twiddles(int n, float *out) {
+    if (!pow2_kernels(n)) {
+        any_fill_tables(any_plan(n), out);
+        return;
+    }
     std::vector<float> tw(spectrum_twiddle_floats(n));
     for (int m = 0; m < n; m++) {
         const double a = -2.0 * M_PI * m / (double)n;
@@ -846,11 +727,10 @@ void spectrum_fill_twiddles(int n, float *out) {
     memcpy(out, tw.data(), tw.size() * sizeof(float));
 }
 
-bool spectrum_supported(int n) {
-    return n >= 64 && n <= 65536 && (n & (n - 1)) == 0;
-}
+bool spectrum_supported(int n) { return n >= 1 && n <= (1 << 20); }
 
 size_t spectrum_scratch_floats(int n, int n_frames) {
+    if (!pow2_kernels(n)) return any_scratch_floats(any_plan(n), n_frames);
     if (n <= 16384) return 0;
     const int wave = n_frames < SPECTRUM_WAVE_FRAMES ? n_frames : SPECTRUM_WAVE_FRAMES;
     return (size_t)wave * n * 2;
@@ -859,6 +739,7 @@ size_t spectrum_scratch_floats(int n, int n_frames) {
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles, float *spectra,
                            float *scratch, hipStream_t stream, bool beside_ssb) {
     if (n_frames <= 0) return hipSuccess;
+    if (!pow2_kernels(n)) return launch_spectrum_any(any_plan(n), iq, fmt, n_frames, twiddles, spectra, scratch, stream);
     switch (n) {
     case 32768: return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
     case 65536: return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);

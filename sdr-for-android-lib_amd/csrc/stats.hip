@@ -217,11 +217,13 @@ __device__ float kth_smallest(const float *vals, int cnt, int k, int *hist, int 
 
 __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ spectra, StatsGeometry g,
                                                      int64_t now_ms, StatsState *__restrict__ state,
-                                                     sdrg_frame_record *__restrict__ records) {
+                                                     sdrg_frame_record *__restrict__ records, float *gpool,
+                                                     int gpool_stride) {
     // one dynamic LDS area, used twice: first the staged bins of the window scans, then (after a barrier)
-    // the pooled dB values / gaps of the MAD median
+    // the pooled dB values / gaps of the MAD median -- unless the pool exceeds MAX_POOL bins (wide focus at
+    // N > 65536), which then lives in this frame's slice of the global scratch gpool
     extern __shared__ __attribute__((aligned(16))) float dyn[];
-    float *pool = dyn;
+    float *pool = gpool ? gpool + (size_t)blockIdx.x * gpool_stride : dyn;
     float *stage = dyn;
     __shared__ __attribute__((aligned(16))) int hist[256];
     __shared__ int sh_int[2];
@@ -503,17 +505,23 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
 
 }  // namespace
 
+size_t stats_global_pool_floats(const StatsGeometry &geo, int n_frames) {
+    return geo.max_pool > MAX_POOL ? (size_t)n_frames * (size_t)((geo.max_pool + 3) & ~3) : 0;
+}
+
 hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry &geo, int64_t now_ms,
-                        StatsState *state, sdrg_frame_record *records, hipStream_t stream) {
+                        StatsState *state, sdrg_frame_record *records, float *gpool, hipStream_t stream) {
     if (n_frames <= 0) return hipSuccess;
-    if (geo.max_pool > MAX_POOL) return hipErrorInvalidValue;
+    const bool global_pool = geo.max_pool > MAX_POOL;
+    if (global_pool && !gpool) return hipErrorInvalidValue;
     // the stage area (the staged span, or STAGE_MAX floats for the chunked window scans), reused for the pool
     const int staged = (geo.span_len > 0 && geo.span_len <= STAGE_MAX) ? geo.span_len : STAGE_MAX;
-    const int pool = (geo.max_pool + 3) & ~3;
+    const int pool = global_pool ? 0 : (geo.max_pool + 3) & ~3;
     const size_t lds = sizeof(float) * (size_t)((pool > staged ? pool : staged) + 4);
     hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel), (MAX_POOL + STAGE_MAX + 8) * 4);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(stats_kernel, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms, state, records);
+    hipLaunchKernelGGL(stats_kernel, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms, state, records,
+                       global_pool ? gpool : nullptr, (geo.max_pool + 3) & ~3);
     return hipGetLastError();
 }
 

@@ -134,3 +134,24 @@ def test_oracle_ssb_stages_match_reference_live(oracle_mod):
     _, got = O.SsbState().process(iq, 2_000_000, 1, stages=True)
     for k in ("dc_re", "lpf", "agc", "fir", "eq"):
         np.testing.assert_array_equal(_bits(got[k]), _bits(want[k]), err_msg=k)
+
+
+def test_power_shifted_any_n_vs_numpy(oracle_mod):
+    """The oracle's any-N double DFT (Bluestein for non-powers of two) against numpy's float64 FFT, with the
+    reference's fftshift loop (fft_process.cpp:92-97): for odd N element N-1 is never written (stays 0 in a fresh
+    vector) and bin N-1 is dropped."""
+    O = oracle_mod
+    rng = np.random.default_rng(8)
+    for n in (1, 2, 3, 5, 7, 12, 97, 1000, 1536, 3072, 4099, 10240, 12289, 20000, 24576):
+        x = (rng.normal(0, 0.3, 2 * n)).astype(np.float32)
+        got = O.power_shifted(x, use_f64=True)
+        X = np.fft.fft(x[0::2].astype(np.float64) + 1j * x[1::2].astype(np.float64))
+        p = (X.real.astype(np.float32) ** 2 + X.imag.astype(np.float32) ** 2).astype(np.float32)
+        half = n // 2
+        want = np.zeros(n, np.float32)
+        want[:half] = p[half:2 * half]
+        want[half:2 * half] = p[:half]
+        tol = 1e-5 * want + 1e-9 * want.max()
+        assert np.all(np.abs(got - want) <= tol), (n, np.max(np.abs(got - want)))
+        if n % 2:
+            assert got[n - 1] == 0.0
