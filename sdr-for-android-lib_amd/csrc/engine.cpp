@@ -132,6 +132,12 @@ struct sdrg_engine {
     int n_streams = 0;
     int device = 0;
     hipStream_t s_main = nullptr, s_ssb = nullptr;
+    // CU split (SDRG_CU_SPLIT, lab): the SSB stream and a spectrum/statistics stream restricted to disjoint
+    // halves of the CUs (hipExtStreamCreateWithCUMask), so the latency-bound SSB waves share no SIMD with the
+    // spectrum's; s_spec is forked from / joined into s_main per call like the SSB stream
+    hipStream_t s_spec = nullptr;
+    int spec_cus = 0;
+    hipEvent_t ev_fork_spec = nullptr, ev_join_spec = nullptr;
     hipStream_t s_own = nullptr;  // the engine's own main stream (s_main is it, or the caller's via set_stream)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // input release: recorded after the last kernel of a call that reads its iq buffer on each stream (the
@@ -509,10 +515,18 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));  // orders the SSB after the caller's producer work
         HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
     }
+    // the spectrum / statistics stream: s_main, or the CU-split stream forked from it
+    const bool split = e->s_spec && (do_spec || do_stats);
+    hipStream_t sm = split ? e->s_spec : e->s_main;
+    if (split) {
+        HIP_TRY(hipEventRecord(e->ev_fork_spec, e->s_main));
+        HIP_TRY(hipStreamWaitEvent(e->s_spec, e->ev_fork_spec, 0));
+    }
     if (do_spec) {
-        HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, e->s_main, do_ssb && early_fork));
-        if (prof) HIP_TRY(hipEventRecord(ev->spec, e->s_main));
-        HIP_TRY(hipEventRecord(e->ev_in_main, e->s_main));  // the spectrum is the main stream's last iq reader
+        HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, sm, do_ssb && early_fork && !split,
+                                split ? e->spec_cus : 0));
+        if (prof) HIP_TRY(hipEventRecord(ev->spec, sm));
+        HIP_TRY(hipEventRecord(e->ev_in_main, sm));  // the spectrum is the main stream's last iq reader
     }
     if (do_ssb) {  // fork
         if (!early_fork) {
@@ -538,13 +552,17 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
     }
     if (do_stats) {
-        HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->d_pool, e->s_main));
+        HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->d_pool, sm));
         if (do_sp) {  // spectralPulseDetector.process(best1kHzSnrSigma, best1kHzCenterFreqHz) (:477-479)
             int32_t rc = pulse_bank_spectral(&e->spec_bank, &recs->best1khz_snr_sigma, &recs->best1khz_center_freq_hz,
-                                             (int)sizeof(sdrg_frame_record), e->spec_bank.d_out, e->s_main);
+                                             (int)sizeof(sdrg_frame_record), e->spec_bank.d_out, sm);
             if (rc) return rc;
         }
-        if (prof) HIP_TRY(hipEventRecord(ev->stats, e->s_main));
+        if (prof) HIP_TRY(hipEventRecord(ev->stats, sm));
+    }
+    if (split) {
+        HIP_TRY(hipEventRecord(e->ev_join_spec, e->s_spec));
+        HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join_spec, 0));
     }
     if (do_ssb && !early_fork) HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));  // join
     if (prof) {
@@ -686,6 +704,26 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         hipStreamCreateWithPriority(&e->s_ssb, hipStreamNonBlocking, prio_ssb) != hipSuccess)
         return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
     e->s_main = e->s_own;
+    // lab: SDRG_CU_SPLIT = 1 (SSB on even CU-mask bits, spectrum/statistics on odd) or 2 (low / high half)
+    if (const char *v = getenv("SDRG_CU_SPLIT")) {
+        const int mode = atoi(v);
+        const int ncu = prop.multiProcessorCount;
+        if ((mode == 1 || mode == 2) && ncu >= 2) {
+            std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
+            for (int i = 0; i < ncu; i++) {
+                const bool a = mode == 1 ? (i % 2 == 0) : (i < ncu / 2);
+                (a ? ma : mb)[i / 32] |= 1u << (i % 32);
+            }
+            if (e->s_ssb) (void)hipStreamDestroy(e->s_ssb);
+            e->s_ssb = nullptr;
+            if (hipExtStreamCreateWithCUMask(&e->s_ssb, (uint32_t)ma.size(), ma.data()) != hipSuccess ||
+                hipExtStreamCreateWithCUMask(&e->s_spec, (uint32_t)mb.size(), mb.data()) != hipSuccess ||
+                hipEventCreateWithFlags(&e->ev_fork_spec, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&e->ev_join_spec, hipEventDisableTiming) != hipSuccess)
+                return cleanup(fail(SDRG_E_HIP, "CU-masked stream creation failed"));
+            e->spec_cus = ncu - ncu / 2;
+        }
+    }
     configure_fft(e);
     hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join, &e->ev_in_main, &e->ev_in_ssb};
     for (auto p : evs)
@@ -708,7 +746,8 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
                     e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
-    hipEvent_t evs[] = {e->ev_fork, e->ev_join, e->ev_in_main, e->ev_in_ssb};
+    if (e->s_spec) (void)hipStreamSynchronize(e->s_spec);
+    hipEvent_t evs[] = {e->ev_fork, e->ev_join, e->ev_in_main, e->ev_in_ssb, e->ev_fork_spec, e->ev_join_spec};
     for (hipEvent_t ev : evs)
         if (ev) (void)hipEventDestroy(ev);
     for (auto &r : e->ring) {
@@ -720,6 +759,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     pulse_bank_release(&e->audio_bank);
     if (e->s_own) (void)hipStreamDestroy(e->s_own);
     if (e->s_ssb) (void)hipStreamDestroy(e->s_ssb);
+    if (e->s_spec) (void)hipStreamDestroy(e->s_spec);
     delete e;
     return SDRG_OK;
 }

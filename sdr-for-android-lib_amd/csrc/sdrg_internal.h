@@ -52,8 +52,9 @@ void spectrum_fill_twiddles(int n, float *out);
 // beside_ssb: the previous call's SSB pipeline is expected to hold the CUs (pipelined calls); the persistent
 // N = 16384 kernel then launches one workgroup per CU, the one that co-resides with it (measured +2-3 % per
 // step over two), instead of two per CU for the chip alone.
+// n_cus: CUs the stream may use (0 = the device's; a CU-masked stream passes its share) for persistent grids.
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles,
-                           float *spectra, float *scratch, hipStream_t stream, bool beside_ssb = false);
+                           float *spectra, float *scratch, hipStream_t stream, bool beside_ssb = false, int n_cus = 0);
 
 // gpool: [n_frames][stats_global_pool_floats / n_frames] device scratch for the pooled-bin median when the
 // pool exceeds what the kernel keeps in LDS (stats_global_pool_floats > 0; wide focus windows at N > 65536)

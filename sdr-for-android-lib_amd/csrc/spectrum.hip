@@ -459,7 +459,8 @@ int device_cus() {
 
 // wg_per_cu: persistent workgroups per CU (2 alone; 1 when the SSB pipeline shares the CUs, see launch_spectrum)
 template <int FMT>
-hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectra, hipStream_t s, int wg_per_cu = 2) {
+hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectra, hipStream_t s, int wg_per_cu = 2,
+                  int n_cus = 0) {
     auto k = spectrum16k_kernel<FMT>;
     hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(k), LDS_BYTES);
     if (e != hipSuccess) return e;
@@ -468,19 +469,19 @@ hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectr
         const int g = v ? atoi(v) : 0;
         return g > 0 ? g : 0;
     }();
-    const int cap = max_grid > 0 ? max_grid : (wg_per_cu == 1 ? 1 : 2) * device_cus();
+    const int cap = max_grid > 0 ? max_grid : (wg_per_cu == 1 ? 1 : 2) * (n_cus > 0 ? n_cus : device_cus());
     const int grid = n_frames < cap ? n_frames : cap;
     hipLaunchKernelGGL(k, dim3(grid), dim3(T), LDS_BYTES, s, iq, spectra, tabs, n_frames);
     return hipGetLastError();
 }
 
 hipError_t launch_fmt(const void *iq, int fmt, int n_frames, const float *tabs, float *spectra, hipStream_t s,
-                      int wg_per_cu) {
+                      int wg_per_cu, int n_cus) {
     switch (fmt) {
-    case SDRG_IQ_CS8: return launch<SDRG_IQ_CS8>(iq, n_frames, tabs, spectra, s, wg_per_cu);
-    case SDRG_IQ_CU8: return launch<SDRG_IQ_CU8>(iq, n_frames, tabs, spectra, s, wg_per_cu);
-    case SDRG_IQ_CS16: return launch<SDRG_IQ_CS16>(iq, n_frames, tabs, spectra, s, wg_per_cu);
-    case SDRG_IQ_CF32: return launch<SDRG_IQ_CF32>(iq, n_frames, tabs, spectra, s, wg_per_cu);
+    case SDRG_IQ_CS8: return launch<SDRG_IQ_CS8>(iq, n_frames, tabs, spectra, s, wg_per_cu, n_cus);
+    case SDRG_IQ_CU8: return launch<SDRG_IQ_CU8>(iq, n_frames, tabs, spectra, s, wg_per_cu, n_cus);
+    case SDRG_IQ_CS16: return launch<SDRG_IQ_CS16>(iq, n_frames, tabs, spectra, s, wg_per_cu, n_cus);
+    case SDRG_IQ_CF32: return launch<SDRG_IQ_CF32>(iq, n_frames, tabs, spectra, s, wg_per_cu, n_cus);
     default: return hipErrorInvalidValue;
     }
 }
@@ -737,14 +738,14 @@ size_t spectrum_scratch_floats(int n, int n_frames) {
 }
 
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles, float *spectra,
-                           float *scratch, hipStream_t stream, bool beside_ssb) {
+                           float *scratch, hipStream_t stream, bool beside_ssb, int n_cus) {
     if (n_frames <= 0) return hipSuccess;
     if (!pow2_kernels(n)) return launch_spectrum_any(any_plan(n), iq, fmt, n_frames, twiddles, spectra, scratch, stream);
     switch (n) {
     case 32768: return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
     case 65536: return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
     case 16384: return k16::launch_fmt(iq, fmt, n_frames, twiddles + spectrum_k16_tables_offset(), spectra, stream,
-                                      beside_ssb ? 1 : 2);
+                                      beside_ssb ? 1 : 2, n_cus);
     case 64: return launch_n<6>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 128: return launch_n<7>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 256: return launch_n<8>(iq, fmt, n_frames, twiddles, spectra, stream);

@@ -336,11 +336,16 @@ constexpr int MAX_DONE = 8;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
 
 constexpr int TAPS_ROW = CH + 256 + CH + 4;
-constexpr int RAW_U4 = PG * 32;  // one prefetch batch: 512 B per stream = 32 uint4, as [piece 8][lane 64]
+#ifndef SDRG_PIPE_RAWB  // bytes of raw IQ per stream per prefetch batch
+#define SDRG_PIPE_RAWB 512
+#endif
+constexpr int RAWB = SDRG_PIPE_RAWB;
+constexpr int RAW_PIECES = RAWB / 64;     // 16-B LDS-DMA pieces per loader lane (lane = 4 x stream + quarter)
+constexpr int RAW_U4 = PG * RAWB / 16;    // one prefetch batch as [piece][lane 64] uint4
 
 template <int FMT>
-constexpr int batch_chunks() {  // chunks per 512-B-per-stream prefetch batch (DMA needs CH * bps <= 512)
-    constexpr int b = 512 / (CH * (FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2));
+constexpr int batch_chunks() {  // chunks per RAWB-per-stream prefetch batch (DMA needs CH * bps <= RAWB)
+    constexpr int b = RAWB / (CH * (FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2));
     return b > 0 ? b : 1;
 }
 #ifndef SDRG_PIPE_NRAW  // 2: one batch unpacked, one in flight (3 needs 8 KiB more LDS than co-residency allows)
@@ -536,16 +541,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     const char *ld_frame = iq + (size_t)(ld_live ? s0 + ld_s : s0) * p.n_in * bps;
     const int n_batches = (n_live + BC * CH - 1) / (BC * CH);
     auto issue_batch = [&](int kb) {
-        const char *src = ld_frame + (size_t)(kb * BC * CH + ld_q * 8 * SPU) * bps;
+        const char *src = ld_frame + (size_t)(kb * BC * CH + ld_q * RAW_PIECES * SPU) * bps;
 #pragma unroll
-        for (int q = 0; q < 8; q++)
+        for (int q = 0; q < RAW_PIECES; q++)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + 16 * q),
                                              (__attribute__((address_space(3))) void *)&L.raw[kb % NRAW][q * 64], 16, 0, 0);
     };
     if constexpr (DMA) {
         if (wave == W_LOAD && n_batches > 0) issue_batch(0);
         if (NRAW > 2 && wave == W_LOAD && n_batches > 1) issue_batch(1);
-        if (NRAW > 2 && n_batches > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // batch 0 landed, 1 in flight
+        if (NRAW > 2 && n_batches > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RAW_PIECES) : "memory");  // batch 0 landed, 1 in flight
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
@@ -676,7 +681,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 // the end of batch kb
                 if (it % BC == 0 && kb + NRAW - 1 < n_batches) issue_batch(kb + NRAW - 1);
                 if (it % BC == BC - 1) {
-                    if (NRAW > 2 && kb + 2 < n_batches) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                    if (NRAW > 2 && kb + 2 < n_batches) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RAW_PIECES) : "memory");
                     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
             }
@@ -706,7 +711,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                         if constexpr (DMA) {
                             constexpr int U4 = 8 * (int)bytes_per_sample<FMT>() / 16;  // 16-B pieces per 8 samples
                             const int off = ((c % BC) * CH + within) * (int)bytes_per_sample<FMT>();
-                            const int quarter = off >> 7, piece = (off & 127) >> 4;
+                            const int quarter = off / (RAWB / 4), piece = (off % (RAWB / 4)) >> 4;
                             uint4 u[U4];
 #pragma unroll
                             for (int q = 0; q < U4; q++) u[q] = L.raw[(c / BC) % NRAW][(piece + q) * 64 + sl * 4 + quarter];
@@ -979,24 +984,29 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         if (p.nco_on && pad < (size_t)NCO_LDS_BYTES) pad = NCO_LDS_BYTES;  // the dynamic part holds the NCO tables
 #if SDRG_PIPE_DYN_LDS
         pad = sizeof(PipeLds) + (p.nco_on ? NCO_LDS_BYTES : 0);
-        static bool attr_done = false;
-        if (!attr_done) {
 #define SDRG_PIPE_ATTR_SET(F)                                                                                          \
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(ssb_pipe_kernel<F, true>),                                  \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(PipeLds) + NCO_LDS_BYTES));     \
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(ssb_pipe_kernel<F, false>),                                 \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(PipeLds) + NCO_LDS_BYTES));
-            SDRG_PIPE_ATTR_SET(SDRG_IQ_CS8) SDRG_PIPE_ATTR_SET(SDRG_IQ_CU8) SDRG_PIPE_ATTR_SET(SDRG_IQ_CS16)
-            SDRG_PIPE_ATTR_SET(SDRG_IQ_CF32)
-#undef SDRG_PIPE_ATTR_SET
-            attr_done = true;
+    {                                                                                                                  \
+        hipError_t e1 = ensure_dynamic_lds(reinterpret_cast<const void *>(ssb_pipe_kernel<F, true>),                    \
+                                           (int)(sizeof(PipeLds) + NCO_LDS_BYTES));                                    \
+        hipError_t e2 = ensure_dynamic_lds(reinterpret_cast<const void *>(ssb_pipe_kernel<F, false>),                   \
+                                           (int)(sizeof(PipeLds) + NCO_LDS_BYTES));                                    \
+        if (e1 != hipSuccess) return e1;                                                                               \
+        if (e2 != hipSuccess) return e2;                                                                               \
+    }
+        switch (fmt) {
+        case SDRG_IQ_CS8: SDRG_PIPE_ATTR_SET(SDRG_IQ_CS8) break;
+        case SDRG_IQ_CU8: SDRG_PIPE_ATTR_SET(SDRG_IQ_CU8) break;
+        case SDRG_IQ_CS16: SDRG_PIPE_ATTR_SET(SDRG_IQ_CS16) break;
+        case SDRG_IQ_CF32: SDRG_PIPE_ATTR_SET(SDRG_IQ_CF32) break;
+        default: return hipErrorInvalidValue;
         }
+#undef SDRG_PIPE_ATTR_SET
 #endif
         const int bps = fmt == SDRG_IQ_CF32 ? 8 : fmt == SDRG_IQ_CS16 ? 4 : 2;
-        const int bc = 512 / (CH * bps) > 0 ? 512 / (CH * bps) : 1;  // batch_chunks<FMT>()
+        const int bc = RAWB / (CH * bps) > 0 ? RAWB / (CH * bps) : 1;  // batch_chunks<FMT>()
         const int n_live = p.n_in < p.samp_count ? p.n_in : p.samp_count;
         // LDS-DMA batches need whole 16-B pieces inside every frame
-        const bool dma = CH * bps <= 512 && (n_live % (bc * CH)) == 0 && ((size_t)p.n_in * bps) % 16 == 0 &&
+        const bool dma = CH * bps <= RAWB && (n_live % (bc * CH)) == 0 && ((size_t)p.n_in * bps) % 16 == 0 &&
                          (reinterpret_cast<uintptr_t>(iq) & 15) == 0;
         unsigned long long *stamps = ssb_stamps_buffer(n_frames);
         AudioFront af{};
