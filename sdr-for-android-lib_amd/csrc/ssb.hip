@@ -547,15 +547,23 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + 16 * q),
                                              (__attribute__((address_space(3))) void *)&L.raw[kb % NRAW][q * 64], 16, 0, 0);
     };
-    if constexpr (DMA) {
-        if (wave == W_LOAD && n_batches > 0) issue_batch(0);
-        if (NRAW > 2 && wave == W_LOAD && n_batches > 1) issue_batch(1);
-        if (NRAW > 2 && n_batches > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RAW_PIECES) : "memory");  // batch 0 landed, 1 in flight
+    // wait until at most `k` batches (the youngest) of this wave's LDS-DMA are still in flight
+    auto wait_raw = [](int k) {
+        static_assert(NRAW <= 4 && 2 * RAW_PIECES <= 63, "vmcnt immediates below");
+        if (NRAW >= 4 && k >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RAW_PIECES) : "memory");
+        else if (NRAW >= 3 && k >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RAW_PIECES) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    if constexpr (DMA) {
+        const int first = min(NRAW - 1, n_batches);  // batches 0 .. NRAW-2 in flight before the loop
+        if (wave == W_LOAD)
+            for (int kb = 0; kb < first; kb++) issue_batch(kb);
+        wait_raw(first - 1);  // batch 0 landed
     }
     __syncthreads();
 
     unsigned long long st_work = 0, st_t0 = stamps ? __builtin_amdgcn_s_memtime() : 0, st_a = st_t0;
+    const unsigned long long st_r0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;  // 100 MHz constant clock
     // Each role runs its own copy of the chunk loop (same trip count, one LDS barrier per iteration), so
     // the register allocator sees one role per loop and the kernel's VGPR count is the largest role's,
     // not the sum of every role's loop-invariant values.
@@ -680,10 +688,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 // batch kb + NRAW - 1 goes into the slot batch kb - 1 left; batch kb + 1 must have landed by
                 // the end of batch kb
                 if (it % BC == 0 && kb + NRAW - 1 < n_batches) issue_batch(kb + NRAW - 1);
-                if (it % BC == BC - 1) {
-                    if (NRAW > 2 && kb + 2 < n_batches) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(RAW_PIECES) : "memory");
-                    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
+                if (it % BC == BC - 1)  // batches issued beyond kb + 1 may stay in flight
+                    wait_raw(min(kb + NRAW - 1, n_batches - 1) - (kb + 1));
             }
             // ---- unpack the I channel of chunk it (lane = 4 x stream + part of CH/4 samples) ----
             {
@@ -872,8 +878,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         });
     }
     if (stamps && lane == 0) {  // diagnostic build only: per-wave work cycles and loop cycles
-        stamps[(blockIdx.x * PIPE_WAVES + wave) * 2] = st_work;
-        stamps[(blockIdx.x * PIPE_WAVES + wave) * 2 + 1] = __builtin_amdgcn_s_memtime() - st_t0;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * 3] = st_work;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * 3 + 1] = __builtin_amdgcn_s_memtime() - st_t0;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * 3 + 2] = __builtin_amdgcn_s_memrealtime() - st_r0;
     }
 
     if (high) __builtin_amdgcn_s_setprio(0);
@@ -920,8 +927,11 @@ bool ssb_force_reference_kernels() {
 
 // Diagnostic: SDRG_PIPE_STAMPS=1 makes the pipeline record per-wave work/loop cycles (s_memtime) and
 // ssb_report_stamps() print them per role.  Off by default (stamps == nullptr: no instruction executes).
+// Each call writes its own slot of a 64-call ring, so the report can average steady-state calls only (a
+// pipelined run's first and last calls run partly alone).
+constexpr int STAMP_CALLS = 64;
 static unsigned long long *g_stamps = nullptr;
-static int g_stamps_groups = 0;
+static int g_stamps_groups = 0, g_stamp_call = 0;
 unsigned long long *ssb_stamps_buffer(int n_frames) {
     static const bool on = [] {
         const char *v = getenv("SDRG_PIPE_STAMPS");
@@ -929,30 +939,63 @@ unsigned long long *ssb_stamps_buffer(int n_frames) {
     }();
     if (!on) return nullptr;
     const int groups = (n_frames + PG - 1) / PG;
+    const size_t per_call = (size_t)groups * PIPE_WAVES * 3;
     if (groups > g_stamps_groups) {
         if (g_stamps) (void)hipFree(g_stamps);
-        if (hipMalloc(reinterpret_cast<void **>(&g_stamps), sizeof(unsigned long long) * groups * PIPE_WAVES * 2) != hipSuccess)
+        if (hipMalloc(reinterpret_cast<void **>(&g_stamps), sizeof(unsigned long long) * per_call * STAMP_CALLS) !=
+            hipSuccess)
             return nullptr;
+        (void)hipMemset(g_stamps, 0, sizeof(unsigned long long) * per_call * STAMP_CALLS);
         g_stamps_groups = groups;
+        g_stamp_call = 0;
     }
-    return g_stamps;
+    return g_stamps + (size_t)(g_stamp_call++ % STAMP_CALLS) * (size_t)g_stamps_groups * PIPE_WAVES * 3;
 }
 
+// Per role: work / loop cycles, loop time and effective clock of the last call; then the same averaged over the
+// recorded calls except the first and the last (the steady state of a pipelined run).
 void ssb_report_stamps() {
-    if (!g_stamps) return;
-    std::vector<unsigned long long> h((size_t)g_stamps_groups * PIPE_WAVES * 2);
+    if (!g_stamps || g_stamp_call == 0) return;
+    const size_t per_call = (size_t)g_stamps_groups * PIPE_WAVES * 3;
+    const int ncalls = g_stamp_call < STAMP_CALLS ? g_stamp_call : STAMP_CALLS;
+    std::vector<unsigned long long> h(per_call * STAMP_CALLS);
     if (hipMemcpy(h.data(), g_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     const char *names[PIPE_WAVES] = {"DC", "LPF", "AGC", "LOAD", "FIR-0", "OUT", "EQ", "FIR-1", "DES-0", "DES-1",
                                      "DES-2", "DES-3"};
+    const int last = (g_stamp_call - 1) % STAMP_CALLS;
     for (int w = 0; w < PIPE_WAVES; w++) {
-        double work = 0, loop = 0;
-        for (int g = 0; g < g_stamps_groups; g++) {
-            work += h[(g * PIPE_WAVES + w) * 2];
-            loop += h[(g * PIPE_WAVES + w) * 2 + 1];
+        double work = 0, loop = 0, real = 0, swork = 0, sloop = 0, sreal = 0;
+        int sc = 0;
+        for (int k = 0; k < ncalls; k++) {
+            const unsigned long long *c = h.data() + (size_t)k * per_call;
+            double a = 0, b = 0, r = 0;
+            for (int g = 0; g < g_stamps_groups; g++) {
+                a += c[(g * PIPE_WAVES + w) * 3];
+                b += c[(g * PIPE_WAVES + w) * 3 + 1];
+                r += c[(g * PIPE_WAVES + w) * 3 + 2];
+            }
+            if (k == last) {
+                work = a;
+                loop = b;
+                real = r;
+            } else if (ncalls > 2 && k != (g_stamp_call - ncalls) % STAMP_CALLS) {  // not the first recorded call
+                swork += a;
+                sloop += b;
+                sreal += r;
+                sc++;
+            }
         }
-        fprintf(stderr, "[sdrg stamps] wave %d %-10s work %12.0f cyc  loop %12.0f cyc  (mean over %d groups)\n", w,
-                names[w], work / g_stamps_groups, loop / g_stamps_groups, g_stamps_groups);
+        const double G = g_stamps_groups;
+        // effective shader clock over the loop: s_memtime cycles / s_memrealtime (100 MHz) time
+        fprintf(stderr,
+                "[sdrg stamps] wave %d %-6s last: work %8.0f loop %8.0f cyc %6.1f us %.3f GHz | steady (%d calls): work "
+                "%8.0f loop %8.0f cyc %6.1f us %.3f GHz\n",
+                w, names[w], work / G, loop / G, real / G / 100.0, real > 0 ? loop / real * 0.1 : 0.0, sc,
+                sc ? swork / G / sc : 0.0, sc ? sloop / G / sc : 0.0, sc ? sreal / G / sc / 100.0 : 0.0,
+                sreal > 0 ? sloop / sreal * 0.1 : 0.0);
     }
+    g_stamp_call = 0;  // the next report covers the calls after this one
+    (void)hipMemset(g_stamps, 0, sizeof(unsigned long long) * per_call * STAMP_CALLS);
 }
 
 // Outputs whose window can overlap one chunk: floor((CH + NT - 2) / D) + 1; the FIR keeps one accumulator
