@@ -11,6 +11,11 @@
 // seeded at -130 dB), found by a wave reduction that prefers the lower index on ties; the MAD medians
 // are exact k-th-element radix selects instead of std::sort.  Only the trip-wise order-free parts
 // (dB conversions, the pooled-gap selection) run across lanes.
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
 #include "sdrg_internal.h"
 
 #pragma clang fp contract(off)
@@ -21,6 +26,19 @@ namespace {
 constexpr int WAVE = 64;
 constexpr int STAGE_MAX = 8192;  // bins staged into LDS for the window scans (32 KiB)
 constexpr int MAX_POOL = 16384;  // pooled-bin bound: N/4 at N = 65536 (the widest nBottom case, see engine.cpp)
+
+// Diagnostic build only (-DSDRG_STATS_STAMPS=1, tools/build_variant.sh): s_memtime at phase boundaries per frame
+#ifndef SDRG_STATS_STAMPS
+#define SDRG_STATS_STAMPS 0
+#endif
+constexpr int STAMP_PHASES = 10;
+
+__device__ unsigned long long g_stats_stamps[STAMP_PHASES * 8192];
+#define STATS_STAMP(k)                                                                                        \
+    do {                                                                                                      \
+        if (SDRG_STATS_STAMPS && threadIdx.x == 0 && blockIdx.x < 8192)                                       \
+            g_stats_stamps[blockIdx.x * STAMP_PHASES + (k)] = __builtin_amdgcn_s_memtime();                   \
+    } while (0)
 
 __device__ __forceinline__ float db_of(float p) { return 10.0f * log10f(p / 1.0f + 1e-20f); }  // refPower = 1
 
@@ -63,68 +81,223 @@ __device__ __forceinline__ WinScan scan_window(const float *__restrict__ P, int 
     return r;
 }
 
-// The same sequential loops for up to 11 windows whose bins do not fit the LDS stage at once (e.g. N = 65536
-// with a 200 kHz focus: three windows of 13107 bins).  All 64 lanes copy the next chunk of every window
-// (plus the w bins before it, which the sliding scan subtracts) from HBM into LDS, coalesced; then lane j
-// runs window j's plain sum and lane 32 + j its best-1-kHz sliding scan over that chunk, the two sequential
-// chains of a window on two lanes, in the reference's element order.  Without the staging each dependent
-// step of those chains waited on an HBM load.  Lane j (j < nwin) returns window j's WinScan.
-__device__ WinScan scan_windows_chunked(const float *__restrict__ P, float *buf, int buf_floats, int nwin,
-                                        const int *wlo, const int *whi, int w) {
-    const int lane = threadIdx.x;
-    const int row = buf_floats / nwin;        // floats per window row: w history bins + SC new ones
-    const int SC = row - w;                   // > 0: checked by the caller
-    const int j = lane & 31;
-    const bool sum_lane = lane < nwin, scan_lane = lane >= 32 && j < nwin;
-    const int my_lo = (j < nwin) ? wlo[j] : 0, my_len = (j < nwin) ? whi[j] - wlo[j] + 1 : 0;
+// Wide windows: the same sequential loops for up to 11 windows whose bins do not fit the LDS stage (e.g.
+// N = 65536 with a 200 kHz focus: three windows of 13107 bins).  One 256-thread workgroup per frame.  Four such
+// workgroups share a CU and the chains are one lane per window, so the kernel is bound by the CU's VALU issue:
+// the design spends as few wave-instructions per bin as the reference's float order allows.
+//   waves 2-3 (producers) stream chunk c of every window from HBM into one slot of an LDS ring: the bins x,
+//            the running-sum terms (x for the first w bins, then the sliding difference x[e] - x[e-w], the
+//            reference's `P[st+w-1] - P[st-1]`, :173-175, an order-free subtraction) and, when want_db, the
+//            bins' dB values; on the way they evaluate the focus window's dB values for its first maximum
+//            (fft_process.cpp:146-154).  Bins past a window's end are zeros (adding +0 changes no sum);
+//   wave 0   (chains) consumes chunk c - 1: every lane runs the same plain sequential sum over its row, 4 bins
+//            per ds_read_b128, writing its running values back: lane j sums window j's bins (the window sum
+//            s, :190-193, :149 for the focus), lane 16 + j its running-sum terms (rs, the best-1-kHz running
+//            sum, :171-178, :313-319, into the rs ring), lane 32 + j its dB values (want_db: the pooled-bin
+//            mean's sum, :259-263, when window j turns out to be the only bottom window);
+//   wave 1   (records) consumes chunk c - 2's running sums rs, lane-parallel: the chunk's first maximum over
+//            the bins e >= w - 1, kept when it exceeds the maximum so far -- the reference's last strict
+//            `rs > bv` record (bv starts at the first window's sum, bin w - 1), whose start is bestStart.
+// One barrier per chunk.
+constexpr int WIDE_WG = 256;
+constexpr int RING_FLOATS = 9216;  // 36 KiB at most: (2 slots x 3 rows + 2 rs rows) x windows x (SC + 4)
+
+struct WideScan {
+    float sum[11], bv[11], dsum[11];
+    int best_e[11];
+    float peak_db;
+    int peak_idx;
+};
+
+template <bool want_db>
+__device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, const int *wlo, const int *whi, int w,
+                          WideScan &out) {
+    // roles by wave: 0 chains, 1 records, 2-3 producers.  (Rotating the roles with the block index, so that the
+    // frames sharing a CU put their chain waves on different SIMDs, measured slower: the chain wave then shares
+    // its SIMD with the producers' issue-dense log10s.)
+    const int lane = threadIdx.x & 63, role = threadIdx.x >> 6;
+    const int fq = nwin - 1;
+    // SC = 2^lg bins per window per chunk, the largest that fits; rows are RS = SC + 4 floats apart, so the chain
+    // lanes' float4 accesses (one row each, same bin) fall in different LDS banks
+    int lg = 6;
+    while (8 * nwin * ((2 << lg) + 4) <= RING_FLOATS && lg < 12) lg++;
+    const int SC = 1 << lg, RS = SC + 4, slot_floats = 3 * RS * nwin;
+    float *rsring = ring + 2 * slot_floats;  // [2][nwin] rows
     int max_len = 0;
     for (int q = 0; q < nwin; q++) max_len = max(max_len, whi[q] - wlo[q] + 1);
-    float s = 0.0f, rs = 0.0f, bv = 0.0f;
-    int best_start = my_lo;
-    const float *mine = buf + j * row + w;  // mine[e - c0] = P[lo + e], e in [c0 - w, c0 + SC)
-    for (int c0 = 0; c0 < max_len; c0 += SC) {
-        for (int q = 0; q < nwin; q++) {
-            const int lo = wlo[q], len = whi[q] - wlo[q] + 1;
-            const int t0 = max(c0 - w, 0), t1 = min(c0 + SC, len);  // elements of window q this chunk needs
-#pragma unroll 16  // 16 loads in flight per lane: a rolled loop would wait out HBM latency per 256 B
-            for (int t = t0 + lane; t < t1; t += WAVE) buf[q * row + w + (t - c0)] = P[lo + t];
+    const int nch = (max_len + SC - 1) >> lg;
+
+    // chain lanes (wave 0): group 0 window sums, group 1 running sums, group 2 dB sums
+    const int grp = lane >> 4, j = lane & 15;
+    const bool chain = role == 0 && j < nwin && (grp < 2 || (grp == 2 && want_db && j < nwin - 1));
+    float acc = 0.0f;
+    // records (wave 1): the reference's strict `rs > bv` records over the bins e >= w - 1, bv starting at the
+    // first window's sum, end at the FIRST bin holding the maximum of rs over those bins: an order-free first
+    // arg-max.  G lanes per window each keep the first maximum of their bins; one reduction at the end.  Bins
+    // past the window's end hold its last running sum again, so they can only tie with a lower real bin.
+    const int G = WAVE / nwin, rq = min(lane / G, fq), rk = lane - rq * G;
+    const bool rec_lane = role == 1 && lane < G * nwin;
+    float rm = -INFINITY;
+    int ri = 0x7fffffff;
+    float pk = -130.0f;
+    int pki = 0x7fffffff;
+
+    // producers: PG threads per window, thread k of window pq's group handles bins k, k + PG, ... of each chunk.
+    // The bins (and the bins w before them) of chunk c + 1 are fetched into registers before the barrier that
+    // ends chunk c, so their HBM latency overlaps the consumers' work instead of following it.
+    constexpr int PTHREADS = WIDE_WG - 128;
+    constexpr int PR = 9;  // >= SC / PG for every nwin <= 11 (SC from the ring size above)
+    const int PG = PTHREADS / nwin, pw = role >= 2 ? ((role - 2) << 6) | lane : 0;
+    const int pq = min(pw / PG, fq), pk0 = pw - pq * PG;
+    const bool prod = role >= 2 && pw < PG * nwin;
+    const int plo = wlo[pq], plen = whi[pq] - plo + 1;
+    const float *Pq = P + plo;
+    float va[PR], vb[PR];
+    auto fetch = [&](int c) {
+        const int c0 = c << lg;
+#pragma unroll
+        for (int k = 0; k < PR; k++) {
+            const int t = pk0 + PG * k, e = c0 + t;
+            const bool ok = t < SC && e < plen;
+            va[k] = ok ? Pq[e] : 0.0f;
+            vb[k] = (ok && e >= w) ? Pq[e - w] : 0.0f;
         }
-        __syncthreads();
-        const int end = min(c0 + SC, my_len);
-        if (sum_lane) {
-#pragma unroll 8
-            for (int e = c0; e < end; e++) s += mine[e - c0];
-        } else if (scan_lane && my_len >= w) {
-            int e = c0;
-            for (; e < end && e < w; e++) {  // the first window's sum (:171-172)
-                rs += mine[e - c0];
-                if (e == w - 1) bv = rs;
+    };
+    auto store = [&](int c) {
+        const int c0 = c << lg;
+        float *row = ring + (c & 1) * slot_floats + pq * 3 * RS;
+#pragma unroll
+        for (int k = 0; k < PR; k++) {
+            const int t = pk0 + PG * k, e = c0 + t;
+            if (t < SC) {
+                const bool in = e < plen;
+                const float v = va[k];
+                row[t] = v;
+                row[RS + t] = (e >= w) ? v - vb[k] : v;
+                const float d = db_of(v);
+                if (want_db) row[2 * RS + t] = in ? d : 0.0f;
+                // a thread sees its focus bins in increasing order: strict > keeps its first maximum
+                if (in && pq == fq && d > pk) {
+                    pk = d;
+                    pki = plo + e;
+                }
             }
-#pragma unroll 4
-            for (; e < end; e++) {  // slide: start st = lo + e - w + 1 (:173-178)
-                rs += mine[e - c0] - mine[e - c0 - w];
-                if (rs > bv) {
-                    bv = rs;
-                    best_start = my_lo + e - w + 1;
+            __builtin_amdgcn_sched_barrier(0);  // one bin's log10 at a time: interleaved they would hold ~70 VGPRs
+        }
+    };
+    if (prod && nch > 0) fetch(0);
+
+    unsigned long long busy = 0;
+    for (int c = 0; c <= nch + 1; c++) {
+        const unsigned long long t_in = SDRG_STATS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+        if (role >= 2) {
+            if (prod && c < nch) {
+                store(c);
+                if (c + 1 < nch) fetch(c + 1);
+            }
+        } else if (role == 0) {
+            if (c >= 1 && c <= nch && chain) {
+                const float *slot = ring + ((c - 1) & 1) * slot_floats;
+                const float *src = slot + (j * 3 + grp) * RS;  // x, rs terms, dB rows
+                float *dst = grp == 1 ? rsring + (((c - 1) & 1) * nwin + j) * RS : const_cast<float *>(src);
+                // 16 bins per half-step, the next half's four float4 read before this half's adds (two register
+                // sets, no copies), so the LDS latency hides under 16 dependent adds
+                float4 A[4], B[4];
+                auto rd = [&](float4 (&X)[4], int u) {
+#pragma unroll
+                    for (int i = 0; i < 4; i++) X[i] = *reinterpret_cast<const float4 *>(src + u + 4 * i);
+                };
+                auto sum16 = [&](const float4 (&X)[4], int u) {
+                    float4 r[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        acc += X[i].x; r[i].x = acc;
+                        acc += X[i].y; r[i].y = acc;
+                        acc += X[i].z; r[i].z = acc;
+                        acc += X[i].w; r[i].w = acc;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];
+                };
+                rd(A, 0);
+                for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
+                    rd(B, t + 16);
+                    sum16(A, t);
+                    if (t + 32 < SC) rd(A, t + 32);
+                    sum16(B, t + 16);
+                }
+            }
+        } else if (c >= 2 && rec_lane) {
+            // chunk c - 2's running sums: lane k of window rq's group visits bins k, k + G, ... in increasing order
+            const int c0 = (c - 2) << lg;
+            const float *rsrow = rsring + ((c & 1) * nwin + rq) * RS;  // (c - 2) & 1
+            if (c0 + SC > w - 1) {
+                if (c0 >= w - 1) {
+                    for (int t = rk; t < SC; t += G) {
+                        const float v = rsrow[t];
+                        const bool gt = v > rm;  // strict: the lane keeps its first maximum
+                        rm = gt ? v : rm;
+                        ri = gt ? c0 + t : ri;
+                    }
+                } else {
+                    for (int t = rk; t < SC; t += G) {
+                        const float v = rsrow[t];
+                        const bool gt = c0 + t >= w - 1 && v > rm;
+                        rm = gt ? v : rm;
+                        ri = gt ? c0 + t : ri;
+                    }
                 }
             }
         }
+        if (SDRG_STATS_STAMPS) busy += __builtin_amdgcn_s_memtime() - t_in;
         __syncthreads();
     }
-    const float bv_scan = __shfl(bv, (lane & 31) + 32);
-    const int bs_scan = __shfl(best_start, (lane & 31) + 32);
-    WinScan r;
-    r.sum = s;
-    r.best_start = my_lo;
-    if (my_len <= 0) {
-        r.best1k = 0.0f;
-    } else if (my_len < w) {
-        r.best1k = s / my_len;
-    } else {
-        r.best1k = bv_scan / w;  // as scan_window: RN(max rs / w)
-        r.best_start = bs_scan;
+    if (SDRG_STATS_STAMPS && lane == 0 && role <= 2 && blockIdx.x < 8192)
+        g_stats_stamps[blockIdx.x * STAMP_PHASES + 6 + role] = busy;
+    if (role >= 2) {  // first maximum over the producer threads (lower bin on ties)
+        for (int off = WAVE / 2; off > 0; off >>= 1) {
+            const float ob = __shfl_xor(pk, off);
+            const int oi = __shfl_xor(pki, off);
+            if (ob > pk || (ob == pk && oi < pki)) {
+                pk = ob;
+                pki = oi;
+            }
+        }
+        if (role == 3 && lane == 0) {
+            out.peak_db = pk;
+            out.peak_idx = pki;
+        }
     }
-    return r;
+    if (role == 1) {  // first maximum per window over its lane group (lower bin on ties)
+        for (int q = 0; q < nwin; q++) {
+            float m = (rec_lane && rq == q) ? rm : -INFINITY;
+            int mi = (rec_lane && rq == q) ? ri : 0x7fffffff;
+            for (int off = WAVE / 2; off > 0; off >>= 1) {
+                const float om = __shfl_xor(m, off);
+                const int oi = __shfl_xor(mi, off);
+                if (om > m || (om == m && oi < mi)) {
+                    m = om;
+                    mi = oi;
+                }
+            }
+            if (lane == 0) {
+                out.bv[q] = m;
+                out.best_e[q] = mi;
+            }
+        }
+    }
+    if (chain && grp == 0) out.sum[j] = acc;
+    if (chain && grp == 2) out.dsum[j] = acc;
+    __syncthreads();
+    if (role == 2 && lane == 0) {
+        const bool other = pk > out.peak_db || (pk == out.peak_db && pki < out.peak_idx);
+        if (other) {
+            out.peak_db = pk;
+            out.peak_idx = pki;
+        }
+        if (out.peak_idx == 0x7fffffff) out.peak_idx = wlo[fq];
+    }
+    __syncthreads();
 }
 
 __device__ __forceinline__ float fmax_ref(float a, float b) { return (a < b) ? b : a; }  // std::max
@@ -165,57 +338,107 @@ __device__ __forceinline__ float kth_of4(float (&g)[4], int k) {
     return r;
 }
 
-// k-th smallest (0-based) of non-negative floats in vals[0..cnt) by 4 x 8-bit radix select (one wave).
-// Per digit: an LDS histogram (atomics), then a wave-parallel prefix scan (4 bins per lane) locates the
+// k-th smallest (0-based) of non-negative floats in vals[0..cnt) by an 8-bit-digit radix select (WG threads).
+// Bits that every value shares (AND == OR, found by one pass) need no digit pass, so the first histogram splits on
+// the highest bit where the values differ: the values are spread over the bins instead of all landing in the few
+// bins of a common exponent (which serialised the LDS atomics: wide windows at N = 65536 pool 13107 values).
+// Per digit: an LDS histogram (atomics), then a wave-parallel prefix scan (4 bins per lane, wave 0) locates the
 // bucket holding the k-th element.  Same element as the reference's std::sort + gaps[k].
-__device__ float kth_smallest(const float *vals, int cnt, int k, int *hist, int *) {
-    const int lane = threadIdx.x;
-    uint32_t prefix = 0, mask = 0;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-        *reinterpret_cast<int4 *>(&hist[4 * lane]) = make_int4(0, 0, 0, 0);
-        __syncthreads();
-        for (int q = lane; q < cnt; q += WAVE) {
-            const uint32_t b = __float_as_uint(vals[q]);
-            if ((b & mask) == prefix) atomicAdd(&hist[(b >> shift) & 0xff], 1);
+// visit(f) calls f(bits) once for every value this thread holds (an LDS/HBM array or registers).
+template <int WG, class Visit>
+__device__ float kth_smallest(Visit visit, int k, int *hist, uint32_t *xch) {
+    const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
+    uint32_t band = 0xffffffffu, bor = 0u;
+    visit([&](uint32_t b) {
+        band &= b;
+        bor |= b;
+    });
+    for (int off = WAVE / 2; off > 0; off >>= 1) {
+        band &= (uint32_t)__shfl_xor((int)band, off);
+        bor |= (uint32_t)__shfl_xor((int)bor, off);
+    }
+    if constexpr (WG > WAVE) {
+        if (lane == 0) {
+            xch[2 * wave] = band;
+            xch[2 * wave + 1] = bor;
         }
         __syncthreads();
-        const int4 h = *reinterpret_cast<const int4 *>(&hist[4 * lane]);
-        const int own = h.x + h.y + h.z + h.w;
-        int incl = own;
 #pragma unroll
-        for (int off = 1; off < WAVE; off <<= 1) {
-            const int v = __shfl_up(incl, off);
-            if (lane >= off) incl += v;
+        for (int v = 0; v < WG / WAVE; v++) {
+            band &= xch[2 * v];
+            bor |= xch[2 * v + 1];
         }
-        const unsigned long long over = __ballot(incl > k);  // non-empty: k < number of candidates
-        const int L = __ffsll((long long)over) - 1;
-        int d = 0, acc = incl - own;
-        if (lane == L) {
-            const int hv[4] = {h.x, h.y, h.z, h.w};
-            int j = 3;  // the lane's last bin unless an earlier one already passes k
+    }
+    const uint32_t diff = band ^ bor;
+    if (diff == 0) return __uint_as_float(band);  // every value equal
+    int top = 31 - __clz(diff);                   // highest bit where the values differ
+    uint32_t mask = top >= 31 ? 0u : ~((2u << top) - 1u);
+    uint32_t prefix = band & mask;
+    while (top >= 0) {
+        const int lo = top >= 7 ? top - 7 : 0;
+        const uint32_t dm = (1u << (top - lo + 1)) - 1u;
+        for (int i = 4 * tid; i < 256; i += 4 * WG) *reinterpret_cast<int4 *>(&hist[i]) = make_int4(0, 0, 0, 0);
+        __syncthreads();
+        visit([&](uint32_t b) {
+            if ((b & mask) == prefix) atomicAdd(&hist[(b >> lo) & dm], 1);
+        });
+        __syncthreads();
+        if (wave == 0) {
+            const int4 h = *reinterpret_cast<const int4 *>(&hist[4 * lane]);
+            const int own = h.x + h.y + h.z + h.w;
+            int incl = own;
 #pragma unroll
-            for (int t = 2; t >= 0; t--) {
-                int before = acc;
-#pragma unroll
-                for (int u = 0; u < t; u++) before += hv[u];
-                if (before + hv[t] > k) j = t;
+            for (int off = 1; off < WAVE; off <<= 1) {
+                const int v = __shfl_up(incl, off);
+                if (lane >= off) incl += v;
             }
+            const unsigned long long over = __ballot(incl > k);  // non-empty: k < number of candidates
+            const int L = __ffsll((long long)over) - 1;
+            if (lane == L) {
+                int acc = incl - own;
+                const int hv[4] = {h.x, h.y, h.z, h.w};
+                int j = 3;  // the lane's last bin unless an earlier one already passes k
 #pragma unroll
-            for (int u = 0; u < 3; u++)
-                if (u < j) acc += hv[u];
-            d = 4 * L + j;
+                for (int t = 2; t >= 0; t--) {
+                    int before = acc;
+#pragma unroll
+                    for (int u = 0; u < t; u++) before += hv[u];
+                    if (before + hv[t] > k) j = t;
+                }
+#pragma unroll
+                for (int u = 0; u < 3; u++)
+                    if (u < j) acc += hv[u];
+                xch[8] = (uint32_t)(4 * L + j);
+                xch[9] = (uint32_t)acc;
+            }
         }
-        d = __shfl(d, L);
-        acc = __shfl(acc, L);
-        k -= acc;
-        prefix |= (uint32_t)d << shift;
-        mask |= 0xffu << shift;
+        __syncthreads();
+        const uint32_t d = xch[8];
+        k -= (int)xch[9];
+        prefix |= d << lo;
+        mask |= dm << lo;
+        top = lo - 1;
         __syncthreads();
     }
     return __uint_as_float(prefix);
 }
 
-__global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ spectra, StatsGeometry g,
+template <int WG>
+__device__ float kth_smallest_of(const float *vals, int cnt, int k, int *hist, uint32_t *xch) {
+    return kth_smallest<WG>(
+        [&](auto f) {
+            for (int q = threadIdx.x; q < cnt; q += WG) f(__float_as_uint(vals[q]));
+        },
+        k, hist, xch);
+}
+
+// the wide kernel's pool when it fits the threads' registers: value q = threadIdx.x + WIDE_WG * r of v[r]
+constexpr int REG_POOL = 64;
+
+// WG = WAVE: one wave per frame, window bins staged in LDS (or read from HBM); WG = WIDE_WG: wide windows
+// (scan_wide), the pool in the frame's slice of the global scratch gpool.
+template <int WG>
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void stats_kernel(const float *__restrict__ spectra, StatsGeometry g,
                                                      int64_t now_ms, StatsState *__restrict__ state,
                                                      sdrg_frame_record *__restrict__ records, float *gpool,
                                                      int gpool_stride) {
@@ -226,9 +449,11 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
     float *pool = gpool ? gpool + (size_t)blockIdx.x * gpool_stride : dyn;
     float *stage = dyn;
     __shared__ __attribute__((aligned(16))) int hist[256];
-    __shared__ int sh_int[2];
+    __shared__ uint32_t sh_xch[10];
+    __shared__ WideScan sh_wide;
+    constexpr bool WIDE = WG > WAVE;
     __shared__ int sh_nbottom, sh_best_start;
-    __shared__ float w_mean_db[10], w_best1k_db[10];
+    __shared__ float w_mean_db[10], w_best1k_db[10], w_dsum[10];
     __shared__ int w_lo[10], w_hi[10], order[10];
     __shared__ float sh_f[4];
     __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
@@ -256,35 +481,40 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
     rec.n_ref_windows = 0;
 
     if (g.focus_len > 0) {
-        // ---- 6.2 focus peak: first maximum of dB, seeded at -130 (fft_process.cpp:142-154) ----
-        float best = -130.0f;
-        int bidx = 0x7fffffff;
-#pragma unroll 8  // loads in flight (13107-bin focus windows at N = 65536 / 200 kHz)
-        for (int i = g.focus_lo + lane; i <= g.focus_hi; i += WAVE) {
-            const float d = db_of(P[i]);
-            if (d > best) {
-                best = d;
-                bidx = i;
-            }
-        }
-        for (int off = WAVE / 2; off > 0; off >>= 1) {
-            const float ob = __shfl_xor(best, off);
-            const int oi = __shfl_xor(bidx, off);
-            if (ob > best || (ob == best && oi < bidx)) {
-                best = ob;
-                bidx = oi;
-            }
-        }
-        const float abs_peak_db = best;
-        const int peak_bin = (bidx == 0x7fffffff) ? g.focus_lo : bidx;
-
-        // ---- 6.2 focus sum + 6.3 reference windows: one lane per window (reference order), lane n_ref
-        //      takes the focus window; all of them run the same sequential scan in lockstep ----
         const int w1k = g.win_bins_1k;
         const int n_ref = g.n_ref;
         // stage the bins every window touches into LDS (coalesced) when they fit, so the sequential
-        // per-lane scans below read LDS instead of waiting on HBM for every element
-        const bool staged = g.span_len > 0 && g.span_len <= STAGE_MAX;
+        // per-lane scans below read LDS instead of waiting on HBM for every element; windows too wide to
+        // stage together are streamed through the same LDS area in chunks (scan_windows_chunked)
+        const bool staged = !WIDE && g.span_len > 0 && g.span_len <= STAGE_MAX;
+        const int nb_geo = max(1, (int)(n_ref * 0.4f));             // nBottom (:233), known from the geometry
+        const bool spec_pool = WIDE && n_ref >= 2 && nb_geo == 1;  // pooled-bin sum = one window's dB sum
+
+        // ---- 6.2 focus peak: first maximum of dB, seeded at -130 (fft_process.cpp:142-154); the chunked
+        //      scan evaluates it while it streams the focus window ----
+        float best = -130.0f;
+        int bidx = 0x7fffffff;
+        if constexpr (!WIDE) {
+#pragma unroll 8
+            for (int i = g.focus_lo + lane; i <= g.focus_hi; i += WAVE) {
+                const float d = db_of(P[i]);
+                if (d > best) {
+                    best = d;
+                    bidx = i;
+                }
+            }
+            for (int off = WAVE / 2; off > 0; off >>= 1) {
+                const float ob = __shfl_xor(best, off);
+                const int oi = __shfl_xor(bidx, off);
+                if (ob > best || (ob == best && oi < bidx)) {
+                    best = ob;
+                    bidx = oi;
+                }
+            }
+        }
+
+        // ---- 6.2 focus sum + 6.3 reference windows: one lane per window (reference order), lane n_ref
+        //      takes the focus window; all of them run the same sequential scan in lockstep ----
         if (staged) {
 #pragma unroll 16
             for (int i = lane; i < g.span_len; i += WAVE) stage[i] = P[g.span_lo + i];
@@ -295,16 +525,39 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
             sh_geo_hi[n_ref] = g.focus_hi;
         }
         __syncthreads();
-        // windows too wide to stage together: chunked through the same LDS area (all lanes take part)
-        const bool chunked = !staged && STAGE_MAX / (n_ref + 1) - w1k >= 64;
-        WinScan wsc{};
-        if (chunked) wsc = scan_windows_chunked(P, stage, STAGE_MAX, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k);
+        if constexpr (WIDE) {
+            STATS_STAMP(0);
+            if (spec_pool)
+                scan_wide<true>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, sh_wide);
+            else
+                scan_wide<false>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, sh_wide);
+            STATS_STAMP(1);
+            best = sh_wide.peak_db;
+            bidx = sh_wide.peak_idx;
+            if (lane < n_ref) w_dsum[lane] = sh_wide.dsum[lane];
+        }
+        const float abs_peak_db = best;
+        const int peak_bin = (bidx == 0x7fffffff) ? g.focus_lo : bidx;
         if (lane <= n_ref) {
             const bool is_focus = (lane == n_ref);
             const int lo = sh_geo_lo[lane];
             const int hi = sh_geo_hi[lane];
-            const WinScan ws = chunked ? wsc : staged ? scan_window(stage - g.span_lo, lo, hi, w1k) : scan_window(P, lo, hi, w1k);
             const int n = hi - lo + 1;
+            WinScan ws;
+            if constexpr (WIDE) {
+                ws.sum = sh_wide.sum[lane];
+                ws.best_start = lo;
+                if (n <= 0) {
+                    ws.best1k = 0.0f;
+                } else if (n < w1k) {
+                    ws.best1k = ws.sum / n;
+                } else {
+                    ws.best1k = sh_wide.bv[lane] / w1k;  // as scan_window: RN(max rs / w)
+                    ws.best_start = lo + sh_wide.best_e[lane] - w1k + 1;
+                }
+            } else {
+                ws = staged ? scan_window(stage - g.span_lo, lo, hi, w1k) : scan_window(P, lo, hi, w1k);
+            }
             if (is_focus) {
                 sh_f[0] = db_of(ws.sum / n);  // signalPowerDb (:155)
                 sh_f[1] = ws.best1k;          // focusBest1kLinear (:302)
@@ -365,20 +618,61 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
             __syncthreads();
             n_bottom = sh_nbottom;
 
+            STATS_STAMP(2);
             // ---- 6.4b pooled per-bin dB of the bottom windows, sorted-window order (:252-269) ----
             int cnt = 0;
-            for (int j = 0; j < n_bottom; j++) {
-                const int lo = w_lo[order[j]], hi = w_hi[order[j]];
-#pragma unroll 8
-                for (int i = lo + lane; i <= hi; i += WAVE) {
-                    const int q = cnt + (i - lo);
-                    if (q < g.max_pool) pool[q] = db_of(P[i]);
+            float med = 0.0f;
+            bool med_done = false;
+            if (spec_pool) {
+                // one bottom window: its dB sum came out of the chunked scan (same values, same order, from 0);
+                // the pool holds the |dB - mean| gaps directly
+                const int wb = order[0];
+                const int lo = w_lo[wb], hi = w_hi[wb];
+                cnt = hi - lo + 1;
+                if (lane == 0) sh_f[2] = w_dsum[wb] / (float)cnt;
+                __syncthreads();
+                const float m = sh_f[2];
+                if (WIDE && cnt <= REG_POOL * WG) {
+                    // gaps in registers: the select's passes read no memory
+                    float v[REG_POOL];
+#pragma unroll
+                    for (int r = 0; r < REG_POOL; r++) {
+                        const int q = lane + WG * r;
+                        v[r] = q < cnt ? P[lo + q] : 0.0f;
+                    }
+#pragma unroll
+                    for (int r = 0; r < REG_POOL; r++) {
+                        v[r] = fabsf(db_of(v[r]) - m);
+                        __builtin_amdgcn_sched_barrier(0);  // one log10 at a time (register pressure)
+                    }
+                    STATS_STAMP(3);
+                    med = kth_smallest<WG>(
+                        [&](auto f) {
+#pragma unroll
+                            for (int r = 0; r < REG_POOL; r++)
+                                if (lane + WG * r < cnt) f(__float_as_uint(v[r]));
+                        },
+                        cnt / 2, hist, sh_xch);
+                    med_done = true;
+                } else {
+#pragma unroll 4
+                    for (int i = lo + lane; i <= hi; i += WG) pool[i - lo] = fabsf(db_of(P[i]) - m);
+                    __syncthreads();
                 }
-                cnt += hi - lo + 1;
+            } else {
+                for (int j = 0; j < n_bottom; j++) {
+                    const int lo = w_lo[order[j]], hi = w_hi[order[j]];
+#pragma unroll 8
+                    for (int i = lo + lane; i <= hi; i += WG) {
+                        const int q = cnt + (i - lo);
+                        if (q < g.max_pool) pool[q] = db_of(P[i]);
+                    }
+                    cnt += hi - lo + 1;
+                }
+                if (cnt > g.max_pool) cnt = g.max_pool;  // host sizes max_pool from the geometry
+                __syncthreads();
             }
-            if (cnt > g.max_pool) cnt = g.max_pool;  // host sizes max_pool from the geometry
-            __syncthreads();
-            if (lane == 0) {
+            if (lane == 0 && !spec_pool) {
                 // sequential sum in pool order (:259-263); 16 values per step read with 4 ds_read_b128
                 float m = 0.0f;
                 int q = 0;
@@ -400,9 +694,15 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
             }
             __syncthreads();
             const float per_bin_mean = sh_f[2];
-            for (int q = lane; q < cnt; q += WAVE) pool[q] = fabsf(pool[q] - per_bin_mean);
-            __syncthreads();
-            const float med = kth_smallest(pool, cnt, cnt / 2, hist, sh_int);
+            if (!spec_pool) {
+                for (int q = lane; q < cnt; q += WG) pool[q] = fabsf(pool[q] - per_bin_mean);
+                __syncthreads();
+            }
+            if (!med_done) {
+                STATS_STAMP(3);
+                med = kth_smallest_of<WG>(pool, cnt, cnt / 2, hist, sh_xch);
+            }
+            STATS_STAMP(4);
             const float sigma_bin = (cnt > 0) ? fmax_ref(1.4816f * med, 1.0f) : 1.0f;
             if (cnt > 0) st.per_bin_mean = per_bin_mean;
             const float pbm = (cnt > 0) ? per_bin_mean : 0.0f;
@@ -440,6 +740,7 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
             }
         }
 
+        STATS_STAMP(5);
         if (lane == 0) {
             // ---- 6.5 frequency tracking (:333-361), clock injected ----
             if (st.tracking_frequency == 0.0f) st.tracking_frequency = g.cf_float;
@@ -505,23 +806,59 @@ __global__ __launch_bounds__(WAVE) void stats_kernel(const float *__restrict__ s
 
 }  // namespace
 
+// spans beyond the LDS stage take the wide kernel (scan_wide), whose pool is in HBM scratch (the radix select's
+// passes then read it from L2/MALL; LDS keeps the ring small enough for four frames per CU)
+static bool wide_for(const StatsGeometry &geo) { return geo.span_len > STAGE_MAX; }
+static bool global_pool_for(const StatsGeometry &geo) { return wide_for(geo) || geo.max_pool > MAX_POOL; }
+
 size_t stats_global_pool_floats(const StatsGeometry &geo, int n_frames) {
-    return geo.max_pool > MAX_POOL ? (size_t)n_frames * (size_t)((geo.max_pool + 3) & ~3) : 0;
+    return global_pool_for(geo) ? (size_t)n_frames * (size_t)((geo.max_pool + 3) & ~3) : 0;
 }
 
 hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry &geo, int64_t now_ms,
                         StatsState *state, sdrg_frame_record *records, float *gpool, hipStream_t stream) {
     if (n_frames <= 0) return hipSuccess;
-    const bool global_pool = geo.max_pool > MAX_POOL;
+    const bool global_pool = global_pool_for(geo);
     if (global_pool && !gpool) return hipErrorInvalidValue;
-    // the stage area (the staged span, or STAGE_MAX floats for the chunked window scans), reused for the pool
-    const int staged = (geo.span_len > 0 && geo.span_len <= STAGE_MAX) ? geo.span_len : STAGE_MAX;
-    const int pool = global_pool ? 0 : (geo.max_pool + 3) & ~3;
-    const size_t lds = sizeof(float) * (size_t)((pool > staged ? pool : staged) + 4);
-    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel), (MAX_POOL + STAGE_MAX + 8) * 4);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(stats_kernel, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms, state, records,
-                       global_pool ? gpool : nullptr, (geo.max_pool + 3) & ~3);
+    if (geo.n_ref > 10) return hipErrorInvalidValue;
+    const int pool_stride = (geo.max_pool + 3) & ~3;
+    if (wide_for(geo)) {
+        size_t lds = sizeof(float) * (size_t)RING_FLOATS;
+        if (SDRG_STATS_STAMPS && getenv("SDRG_STATS_LDS_KB")) {  // diagnostic: fewer frames per CU
+            lds = (size_t)atoi(getenv("SDRG_STATS_LDS_KB")) * 1024;
+            hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel<WIDE_WG>), (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(stats_kernel<WIDE_WG>, dim3(n_frames), dim3(WIDE_WG), lds, stream, spectra, geo, now_ms,
+                           state, records, gpool, pool_stride);
+    } else {
+        // the stage area (the staged span), reused for the pool
+        const int staged = geo.span_len > 0 ? geo.span_len : 0;
+        const int pool = global_pool ? 0 : pool_stride;
+        const size_t lds = sizeof(float) * (size_t)((pool > staged ? pool : staged) + 4);
+        hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel<WAVE>), (MAX_POOL + STAGE_MAX + 8) * 4);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(stats_kernel<WAVE>, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms, state,
+                           records, global_pool ? gpool : nullptr, pool_stride);
+    }
+    if (SDRG_STATS_STAMPS) {  // diagnostic build: mean cycles per phase over the frames of this call
+        std::vector<unsigned long long> h((size_t)STAMP_PHASES * 8192);
+        if (hipStreamSynchronize(stream) == hipSuccess &&
+            hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_stats_stamps), h.size() * 8) == hipSuccess) {
+            const int nf = n_frames < 8192 ? n_frames : 8192;
+            double d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int f = 0; f < nf; f++) {
+                const unsigned long long *t = &h[(size_t)f * STAMP_PHASES];
+                for (int k = 0; k < 5; k++) d[k] += (double)(t[k + 1] - t[k]);
+                d[5] += (double)t[6];
+                d[6] += (double)t[7];
+                d[7] += (double)t[8];
+            }
+            fprintf(stderr, "[stats stamps] cycles/frame: wide scan %.0f (busy: chain wave %.0f, record wave %.0f, producers %.0f) | "
+                            "sort+6.4a %.0f | pool %.0f | select %.0f | tail %.0f\n", d[0] / nf, d[5] / nf, d[6] / nf,
+                    d[7] / nf, d[1] / nf, d[2] / nf, d[3] / nf, d[4] / nf);
+        }
+    }
     return hipGetLastError();
 }
 

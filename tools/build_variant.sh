@@ -7,7 +7,7 @@ D=sdr-for-android-lib_amd; B=$D/build/variant_$NAME; mkdir -p $B
 HIP="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics $FLAGS"
 $HIP -c $D/csrc/spectrum.hip -o $B/spectrum.o
 $HIP -c $D/csrc/fftany.hip -o $B/fftany.o
-$HIP -ffp-contract=off -c $D/csrc/stats.hip -o $B/stats.o
+$HIP -ffp-contract=off -fno-slp-vectorize -c $D/csrc/stats.hip -o $B/stats.o
 $HIP -ffp-contract=off -fno-slp-vectorize -c $D/csrc/ssb.hip -o $B/ssb.o
 $HIP -ffp-contract=off -c $D/csrc/pulse.hip -o $B/pulse.o
 make -s -C $D  # host objects

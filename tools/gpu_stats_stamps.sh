@@ -1,0 +1,5 @@
+#!/bin/bash
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+SDRG_LIB_PATH=$PWD/sdr-for-android-lib_amd/lib/libsdrg_sstamp.so timeout -k 10 120 python tools/kernel_lab.py --stages spectrum+stats --n 65536 --fmt CS16 --streams 1024 --focus 200 --calls 3 > gpurun_out/sstamp.log 2>&1 || { echo failed; tail gpurun_out/sstamp.log; exit 1; }
+cat gpurun_out/sstamp.log
