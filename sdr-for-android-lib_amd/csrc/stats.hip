@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "sdrg_internal.h"
@@ -25,7 +26,6 @@ namespace {
 
 constexpr int WAVE = 64;
 constexpr int STAGE_MAX = 8192;  // bins staged into LDS for the window scans (32 KiB)
-constexpr int MAX_POOL = 16384;  // pooled-bin bound: N/4 at N = 65536 (the widest nBottom case, see engine.cpp)
 
 // Diagnostic build only (-DSDRG_STATS_STAMPS=1, tools/build_variant.sh): s_memtime at phase boundaries per frame
 #ifndef SDRG_STATS_STAMPS
@@ -48,14 +48,15 @@ struct WinScan {
     int best_start;  // first start maximising the raw running sum (focus scan, :311-320)
 };
 
-// One lane replays the reference's sequential loops over P[lo..hi] (P: staged LDS copy or HBM).
-__device__ __forceinline__ WinScan scan_window(const float *__restrict__ P, int lo, int hi, int w) {
+// One lane replays the reference's sequential loops over the window P[lo..hi], staged in LDS at W (W[i - lo]).
+// (The window's own base pointer, not a virtual P: LDS pointers must stay inside the allocation.)
+__device__ __forceinline__ WinScan scan_window(const float *__restrict__ W, int lo, int hi, int w) {
     WinScan r;
     float s = 0.0f;
-#pragma unroll 8
-    for (int i = lo; i <= hi; i++) s += P[i];
-    r.sum = s;
     const int len = hi - lo + 1;
+#pragma unroll 8
+    for (int i = 0; i < len; i++) s += W[i];
+    r.sum = s;
     r.best_start = lo;
     if (len <= 0) {
         r.best1k = 0.0f;
@@ -64,14 +65,14 @@ __device__ __forceinline__ WinScan scan_window(const float *__restrict__ P, int 
     } else {
         float rs = 0.0f;
 #pragma unroll 8
-        for (int i = lo; i < lo + w; i++) rs += P[i];
+        for (int i = 0; i < w; i++) rs += W[i];
         float bv = rs;
 #pragma unroll 4
-        for (int st = lo + 1; st + w - 1 <= hi; st++) {
-            rs += P[st + w - 1] - P[st - 1];
+        for (int st = 1; st + w - 1 < len; st++) {
+            rs += W[st + w - 1] - W[st - 1];
             if (rs > bv) {
                 bv = rs;
-                r.best_start = st;
+                r.best_start = lo + st;
             }
         }
         // the reference keeps best = max over st of rs/w (:171-178); x -> RN(x / w) is monotone for w > 0,
@@ -302,20 +303,6 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
 
 __device__ __forceinline__ float fmax_ref(float a, float b) { return (a < b) ? b : a; }  // std::max
 
-// Ascending sort of 10 (key, index) pairs by (key, index): odd-even transposition network, registers only.
-__device__ __forceinline__ void sort_pairs10(float (&k)[10], int (&ix)[10]) {
-#pragma unroll
-    for (int round = 0; round < 10; round++) {
-#pragma unroll
-        for (int i = round & 1; i + 1 < 10; i += 2) {
-            const bool sw = (k[i + 1] < k[i]) || (k[i + 1] == k[i] && ix[i + 1] < ix[i]);
-            const float ka = sw ? k[i + 1] : k[i], kb = sw ? k[i] : k[i + 1];
-            const int ia = sw ? ix[i + 1] : ix[i], ib = sw ? ix[i] : ix[i + 1];
-            k[i] = ka; k[i + 1] = kb; ix[i] = ia; ix[i + 1] = ib;
-        }
-    }
-}
-
 // k-th smallest (k < 4) of 4 floats (the reference sorts then indexes: same value).
 __device__ __forceinline__ float kth_of4(float (&g)[4], int k) {
 #pragma unroll
@@ -442,12 +429,11 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                                                      int64_t now_ms, StatsState *__restrict__ state,
                                                      sdrg_frame_record *__restrict__ records, float *gpool,
                                                      int gpool_stride) {
-    // one dynamic LDS area, used twice: first the staged bins of the window scans, then (after a barrier)
-    // the pooled dB values / gaps of the MAD median -- unless the pool exceeds MAX_POOL bins (wide focus at
-    // N > 65536), which then lives in this frame's slice of the global scratch gpool
+    // dynamic LDS: narrow, the staged bins of every window (window q at stage + sh_woff[q]), then the pooled
+    // dB values / gaps of the MAD median; wide, scan_wide's ring (the pool is in the frame's slice of gpool)
     extern __shared__ __attribute__((aligned(16))) float dyn[];
-    float *pool = gpool ? gpool + (size_t)blockIdx.x * gpool_stride : dyn;
     float *stage = dyn;
+    __shared__ int sh_woff[12];
     __shared__ __attribute__((aligned(16))) int hist[256];
     __shared__ uint32_t sh_xch[10];
     __shared__ WideScan sh_wide;
@@ -470,6 +456,21 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
         }
     }
     const float *P = spectra + frame * (size_t)g.n;
+    if (lane == 0) {
+        sh_geo_lo[g.n_ref] = g.focus_lo;
+        sh_geo_hi[g.n_ref] = g.focus_hi;
+        int o = 0;
+        for (int q = 0; q <= g.n_ref; q++) {
+            sh_woff[q] = o;
+            o += max(0, (q < g.n_ref ? g.win_hi[q] - g.win_lo[q] : g.focus_hi - g.focus_lo) + 1);
+        }
+        sh_woff[g.n_ref + 1] = o;
+    }
+    __syncthreads();
+    const int stage_total = sh_woff[g.n_ref + 1];
+    // narrow: the pool after the staged bins (LDS); wide: the frame's slice of gpool
+    float *pool = WIDE ? gpool + (size_t)blockIdx.x * gpool_stride : dyn + ((stage_total + 3) & ~3);
+    const int pool_cap = WIDE ? g.max_pool : gpool_stride;  // narrow: gpool_stride carries the LDS pool's size
     StatsState st = state[frame];
     if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
     sdrg_frame_record rec;
@@ -480,27 +481,41 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
     rec.valid = 0;
     rec.n_ref_windows = 0;
 
-    if (g.focus_len > 0) {
+    if (g.focus_len > 0 && (WIDE || stage_total <= STAGE_MAX)) {
         const int w1k = g.win_bins_1k;
         const int n_ref = g.n_ref;
-        // stage the bins every window touches into LDS (coalesced) when they fit, so the sequential
-        // per-lane scans below read LDS instead of waiting on HBM for every element; windows too wide to
-        // stage together are streamed through the same LDS area in chunks (scan_windows_chunked)
-        const bool staged = !WIDE && g.span_len > 0 && g.span_len <= STAGE_MAX;
+        // narrow: every window's bins are staged into LDS (coalesced, all loads in flight at once), so the focus
+        // peak, the sequential per-lane scans and the pool read LDS instead of HBM; windows too wide to stage
+        // together take the wide kernel (scan_wide; launch_stats routes them by the same count)
         const int nb_geo = max(1, (int)(n_ref * 0.4f));             // nBottom (:233), known from the geometry
         const bool spec_pool = WIDE && n_ref >= 2 && nb_geo == 1;  // pooled-bin sum = one window's dB sum
 
-        // ---- 6.2 focus peak: first maximum of dB, seeded at -130 (fft_process.cpp:142-154); the chunked
-        //      scan evaluates it while it streams the focus window ----
+        // ---- 6.2 focus peak: first maximum of dB, seeded at -130 (fft_process.cpp:142-154), evaluated while
+        //      the focus bins are staged (wide: while scan_wide streams the focus window) ----
         float best = -130.0f;
         int bidx = 0x7fffffff;
+        unsigned long long nst0 = 0, nst1 = 0, nst2 = 0;  // diagnostic stamps of the narrow path
+        if (!WIDE) STATS_STAMP(0);
+        if (SDRG_STATS_STAMPS) nst0 = __builtin_amdgcn_s_memtime();
         if constexpr (!WIDE) {
-#pragma unroll 8
-            for (int i = g.focus_lo + lane; i <= g.focus_hi; i += WAVE) {
-                const float d = db_of(P[i]);
-                if (d > best) {
-                    best = d;
-                    bidx = i;
+            // the window of bin i: the number of window offsets at or below it (offsets in registers)
+            int wo[11];
+#pragma unroll
+            for (int k = 0; k < 11; k++) wo[k] = (k <= n_ref) ? sh_woff[k + 1] : 0x7fffffff;
+            const int foff = sh_woff[n_ref];
+#pragma unroll 16
+            for (int i = lane; i < stage_total; i += WAVE) {
+                int q = 0;
+#pragma unroll
+                for (int k = 0; k < 10; k++) q += (i >= wo[k]) ? 1 : 0;
+                const float v = P[sh_geo_lo[q] + (i - sh_woff[q])];
+                stage[i] = v;
+                if (q == n_ref) {  // lanes see increasing bins: strict > keeps each lane's first maximum
+                    const float d = db_of(v);
+                    if (d > best) {
+                        best = d;
+                        bidx = g.focus_lo + (i - foff);
+                    }
                 }
             }
             for (int off = WAVE / 2; off > 0; off >>= 1) {
@@ -515,16 +530,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
 
         // ---- 6.2 focus sum + 6.3 reference windows: one lane per window (reference order), lane n_ref
         //      takes the focus window; all of them run the same sequential scan in lockstep ----
-        if (staged) {
-#pragma unroll 16
-            for (int i = lane; i < g.span_len; i += WAVE) stage[i] = P[g.span_lo + i];
-            __syncthreads();
-        }
-        if (lane == 0) {
-            sh_geo_lo[n_ref] = g.focus_lo;
-            sh_geo_hi[n_ref] = g.focus_hi;
-        }
+        if (SDRG_STATS_STAMPS) nst1 = __builtin_amdgcn_s_memtime();
         __syncthreads();
+        if (SDRG_STATS_STAMPS) nst2 = __builtin_amdgcn_s_memtime();
         if constexpr (WIDE) {
             STATS_STAMP(0);
             if (spec_pool)
@@ -538,6 +546,10 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
         }
         const float abs_peak_db = best;
         const int peak_bin = (bidx == 0x7fffffff) ? g.focus_lo : bidx;
+        if (!WIDE && SDRG_STATS_STAMPS && threadIdx.x == 0 && blockIdx.x < 8192) {
+            g_stats_stamps[blockIdx.x * STAMP_PHASES + 6] = nst1 - nst0;
+            g_stats_stamps[blockIdx.x * STAMP_PHASES + 7] = nst2 - nst1;
+        }
         if (lane <= n_ref) {
             const bool is_focus = (lane == n_ref);
             const int lo = sh_geo_lo[lane];
@@ -556,7 +568,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                     ws.best_start = lo + sh_wide.best_e[lane] - w1k + 1;
                 }
             } else {
-                ws = staged ? scan_window(stage - g.span_lo, lo, hi, w1k) : scan_window(P, lo, hi, w1k);
+                ws = scan_window(stage + sh_woff[lane], lo, hi, w1k);
             }
             if (is_focus) {
                 sh_f[0] = db_of(ws.sum / n);  // signalPowerDb (:155)
@@ -570,6 +582,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
             }
         }
         __syncthreads();
+        if (!WIDE) STATS_STAMP(1);
         const float signal_power_db = sh_f[0];
         const int valid = (n_ref >= 2);
         rec.peak_bin = peak_bin;
@@ -584,20 +597,22 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
             st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
         } else {
             int n_bottom = 1;
-            if (lane == 0) {
-                // std::sort of <= 16 elements in libstdc++ is a (stable) insertion sort: the same order is a
-                // sort by (meanDb, window index), done here by a network on registers
-                float key[10];
-                int ix[10];
-#pragma unroll
-                for (int i = 0; i < 10; i++) {
-                    key[i] = (i < n_ref) ? w_mean_db[i] : INFINITY;
-                    ix[i] = i;
+            // std::sort of <= 16 elements in libstdc++ is a (stable) insertion sort: the same order is a sort by
+            // (meanDb, window index); lane i places window i at its rank
+            if (lane < n_ref) {
+                const float ki = w_mean_db[lane];
+                int rank = 0;
+                for (int k = 0; k < n_ref; k++) {
+                    const float kk = w_mean_db[k];
+                    rank += (kk < ki || (kk == ki && k < lane)) ? 1 : 0;
                 }
-                sort_pairs10(key, ix);
+                order[rank] = lane;
+            }
+            __syncthreads();
+            if (lane == 0) {
+                float key[4];
 #pragma unroll
-                for (int i = 0; i < 10; i++)
-                    if (i < n_ref) order[i] = ix[i];
+                for (int i = 0; i < 4; i++) key[i] = (i < n_ref) ? w_mean_db[order[i]] : INFINITY;
                 const int nb0 = (int)(n_ref * 0.4f);
                 n_bottom = nb0 > 1 ? nb0 : 1;  // <= 4 (n_ref <= 10)
                 // 6.4a (:235-247)
@@ -661,15 +676,16 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                 }
             } else {
                 for (int j = 0; j < n_bottom; j++) {
-                    const int lo = w_lo[order[j]], hi = w_hi[order[j]];
+                    const int wj = order[j], len = w_hi[wj] - w_lo[wj] + 1;
+                    const float *src = WIDE ? P + w_lo[wj] : stage + sh_woff[wj];
 #pragma unroll 8
-                    for (int i = lo + lane; i <= hi; i += WG) {
-                        const int q = cnt + (i - lo);
-                        if (q < g.max_pool) pool[q] = db_of(P[i]);
+                    for (int i = lane; i < len; i += WG) {
+                        const int q = cnt + i;
+                        if (q < pool_cap) pool[q] = db_of(src[i]);
                     }
-                    cnt += hi - lo + 1;
+                    cnt += len;
                 }
-                if (cnt > g.max_pool) cnt = g.max_pool;  // host sizes max_pool from the geometry
+                if (cnt > pool_cap) cnt = pool_cap;  // host sizes max_pool from the geometry
                 __syncthreads();
             }
             if (lane == 0 && !spec_pool) {
@@ -808,8 +824,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
 
 // spans beyond the LDS stage take the wide kernel (scan_wide), whose pool is in HBM scratch (the radix select's
 // passes then read it from L2/MALL; LDS keeps the ring small enough for four frames per CU)
-static bool wide_for(const StatsGeometry &geo) { return geo.span_len > STAGE_MAX; }
-static bool global_pool_for(const StatsGeometry &geo) { return wide_for(geo) || geo.max_pool > MAX_POOL; }
+// bins the narrow kernel stages: every reference window and the focus window
+static int stage_bins(const StatsGeometry &geo) {
+    int o = std::max(0, geo.focus_hi - geo.focus_lo + 1);  // as the kernel's sh_woff
+    for (int q = 0; q < geo.n_ref && q < 10; q++) o += std::max(0, geo.win_hi[q] - geo.win_lo[q] + 1);
+    return o;
+}
+static bool wide_for(const StatsGeometry &geo) { return stage_bins(geo) > STAGE_MAX; }
+static bool global_pool_for(const StatsGeometry &geo) { return wide_for(geo); }
 
 size_t stats_global_pool_floats(const StatsGeometry &geo, int n_frames) {
     return global_pool_for(geo) ? (size_t)n_frames * (size_t)((geo.max_pool + 3) & ~3) : 0;
@@ -832,14 +854,14 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
         hipLaunchKernelGGL(stats_kernel<WIDE_WG>, dim3(n_frames), dim3(WIDE_WG), lds, stream, spectra, geo, now_ms,
                            state, records, gpool, pool_stride);
     } else {
-        // the stage area (the staged span), reused for the pool
-        const int staged = geo.span_len > 0 ? geo.span_len : 0;
-        const int pool = global_pool ? 0 : pool_stride;
-        const size_t lds = sizeof(float) * (size_t)((pool > staged ? pool : staged) + 4);
-        hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel<WAVE>), (MAX_POOL + STAGE_MAX + 8) * 4);
+        // the staged windows, then the pool (<= the staged bins: it pools whole windows)
+        const int staged = (stage_bins(geo) + 3) & ~3;
+        const int pool = std::min(pool_stride, staged);
+        const size_t lds = sizeof(float) * (size_t)(staged + pool + 4);
+        hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel<WAVE>), (2 * STAGE_MAX + 4) * 4);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(stats_kernel<WAVE>, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms, state,
-                           records, global_pool ? gpool : nullptr, pool_stride);
+                           records, nullptr, pool);
     }
     if (SDRG_STATS_STAMPS) {  // diagnostic build: mean cycles per phase over the frames of this call
         std::vector<unsigned long long> h((size_t)STAMP_PHASES * 8192);
@@ -854,7 +876,8 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
                 d[6] += (double)t[7];
                 d[7] += (double)t[8];
             }
-            fprintf(stderr, "[stats stamps] cycles/frame: wide scan %.0f (busy: chain wave %.0f, record wave %.0f, producers %.0f) | "
+            fprintf(stderr, "[stats stamps] cycles/frame: scans %.0f (wide busy: chain wave / record wave / producers, narrow: "
+                            "focus peak / stage copy: %.0f %.0f %.0f) | "
                             "sort+6.4a %.0f | pool %.0f | select %.0f | tail %.0f\n", d[0] / nf, d[5] / nf, d[6] / nf,
                     d[7] / nf, d[1] / nf, d[2] / nf, d[3] / nf, d[4] / nf);
         }
