@@ -145,6 +145,35 @@ def cpu_baseline(threads: int, target_cpu_s: float = 15.0) -> dict:
                       f"{per_frame * 1e3:.3f} ms/frame single-thread"}
 
 
+def rehearsal_verify(torch, dist, world, rank, streams, rec, f_stage, pcm, gather_pcm, gathered, f_out, p_out):
+    """--rehearse-gloo: after the timed steps, every rank hashes what it contributed to the last step's gathers
+    (records, focus slices, PCM bytes) and rank 0 checks that each rank's block of its gathered buffers hashes
+    the same -- the gather delivered every rank's data, in rank order, bit for bit."""
+    import hashlib
+    torch.cuda.synchronize()
+
+    def digest(t):
+        return hashlib.sha256(t.detach().cpu().contiguous().numpy().tobytes()).hexdigest()
+
+    mine = {"records": digest(rec)}
+    if f_stage is not None:
+        mine["focus"] = digest(f_stage)
+    if gather_pcm:
+        mine["pcm"] = digest(pcm.view(torch.uint8))
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    if rank != 0:
+        return None
+    result = {}
+    for key, buf in (("records", gathered), ("focus", f_out), ("pcm", p_out)):
+        if buf is None:
+            continue
+        ok = all(digest(buf[r * streams:(r + 1) * streams]) == every[r][key] for r in range(world))
+        result[key] = "ok" if ok else "MISMATCH"
+    result["ranks"] = world
+    return result
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -281,6 +310,8 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rehearsal_check = rehearsal_verify(torch, dist, world, rank, streams, rec, f_stage, pcm, gather_pcm, gathered, f_out,
+                                       p_out) if rehearse else None
     ts = eng.timing_stats()
     # the spectrum kernel alone (no SSB sharing the chip), a few launches after the timed region: its
     # isolated HBM rate, reported beside the timed-region one
@@ -416,6 +447,7 @@ def main() -> int:
         out["labelled"] = labelled
     if rehearse:
         out["rehearsal"] = "gloo, every rank on cuda:0: a functional check of the N > 1 path, not a measurement"
+        out["rehearsal_check"] = rehearsal_check
     if variant:
         out["ssb_variant"] = {"nco_hz": NCO_HZ, "fir_taps": 127, "note": "not the reference's chain; no CPU baseline"}
     if args.config != "c3":

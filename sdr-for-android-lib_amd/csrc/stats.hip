@@ -421,6 +421,7 @@ __device__ float kth_smallest_of(const float *vals, int cnt, int k, int *hist, u
 
 // the wide kernel's pool when it fits the threads' registers: value q = threadIdx.x + WIDE_WG * r of v[r]
 constexpr int REG_POOL = 64;
+constexpr int NARROW_REG_POOL = 24;  // the narrow kernel's pool in registers up to 24 x 64 values
 
 // WG = WAVE: one wave per frame, window bins staged in LDS (or read from HBM); WG = WIDE_WG: wide windows
 // (scan_wide), the pool in the frame's slice of the global scratch gpool.
@@ -429,8 +430,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                                                      int64_t now_ms, StatsState *__restrict__ state,
                                                      sdrg_frame_record *__restrict__ records, float *gpool,
                                                      int gpool_stride) {
-    // dynamic LDS: narrow, the staged bins of every window (window q at stage + sh_woff[q]), then the pooled
-    // dB values / gaps of the MAD median; wide, scan_wide's ring (the pool is in the frame's slice of gpool)
+    // dynamic LDS: narrow, the staged bins of every window (window q at stage + sh_woff[q]), then their dB
+    // values at the same offsets (the focus peak, the pooled bins); wide, scan_wide's ring (the pool is in the
+    // frame's slice of gpool)
     extern __shared__ __attribute__((aligned(16))) float dyn[];
     float *stage = dyn;
     __shared__ int sh_woff[12];
@@ -467,10 +469,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
         sh_woff[g.n_ref + 1] = o;
     }
     __syncthreads();
-    const int stage_total = sh_woff[g.n_ref + 1];
+    const int stage_total = sh_woff[g.n_ref + 1], stage_pad = (stage_total + 3) & ~3;
     // narrow: the pool after the staged bins (LDS); wide: the frame's slice of gpool
-    float *pool = WIDE ? gpool + (size_t)blockIdx.x * gpool_stride : dyn + ((stage_total + 3) & ~3);
-    const int pool_cap = WIDE ? g.max_pool : gpool_stride;  // narrow: gpool_stride carries the LDS pool's size
+    float *pool = gpool + (size_t)blockIdx.x * gpool_stride;  // wide only
     StatsState st = state[frame];
     if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
     sdrg_frame_record rec;
@@ -498,23 +499,38 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
         if (!WIDE) STATS_STAMP(0);
         if (SDRG_STATS_STAMPS) nst0 = __builtin_amdgcn_s_memtime();
         if constexpr (!WIDE) {
-            // the window of bin i: the number of window offsets at or below it (offsets in registers)
-            int wo[11];
+            // staged bin i of window q reads P[i + dl[q]]; q = the number of window starts wo[] at or below i
+            int wo[10], dl[11];
 #pragma unroll
-            for (int k = 0; k < 11; k++) wo[k] = (k <= n_ref) ? sh_woff[k + 1] : 0x7fffffff;
+            for (int k = 0; k < 11; k++) dl[k] = (k <= n_ref) ? sh_geo_lo[k] - sh_woff[k] : 0;
+#pragma unroll
+            for (int k = 0; k < 10; k++) wo[k] = (k < n_ref) ? sh_woff[k + 1] : 0x7fffffff;
             const int foff = sh_woff[n_ref];
-#pragma unroll 16
-            for (int i = lane; i < stage_total; i += WAVE) {
-                int q = 0;
+            float *dbs = stage + stage_pad;
+            for (int base = lane; base < stage_total; base += 16 * WAVE) {
+                // 16 bins per lane in flight: every load issued before the first is used
+                float v[16];
 #pragma unroll
-                for (int k = 0; k < 10; k++) q += (i >= wo[k]) ? 1 : 0;
-                const float v = P[sh_geo_lo[q] + (i - sh_woff[q])];
-                stage[i] = v;
-                if (q == n_ref) {  // lanes see increasing bins: strict > keeps each lane's first maximum
-                    const float d = db_of(v);
-                    if (d > best) {
-                        best = d;
-                        bidx = g.focus_lo + (i - foff);
+                for (int u = 0; u < 16; u++) {
+                    const int i = base + WAVE * u;
+                    int d = dl[0];
+#pragma unroll
+                    for (int k = 0; k < 10; k++) d = (i >= wo[k]) ? dl[k + 1] : d;
+                    v[u] = (i < stage_total) ? P[i + d] : 0.0f;
+                }
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const int i = base + WAVE * u;
+                    if (i < stage_total) {
+                        const float d = db_of(v[u]);
+                        stage[i] = v[u];
+                        dbs[i] = d;
+                        // the focus window is the last: lanes see its bins in increasing order, strict > keeps
+                        // each lane's first maximum
+                        if (i >= foff && d > best) {
+                            best = d;
+                            bidx = g.focus_lo + (i - foff);
+                        }
                     }
                 }
             }
@@ -636,18 +652,121 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
             STATS_STAMP(2);
             // ---- 6.4b pooled per-bin dB of the bottom windows, sorted-window order (:252-269) ----
             int cnt = 0;
-            float med = 0.0f;
-            bool med_done = false;
-            if (spec_pool) {
-                // one bottom window: its dB sum came out of the chunked scan (same values, same order, from 0);
-                // the pool holds the |dB - mean| gaps directly
+            float med = 0.0f, per_bin_mean = 0.0f;
+            if constexpr (!WIDE) {
+                // the pool is the bottom windows' staged dB values, window after window in sorted order
+                const float *dbs = stage + stage_pad;
+                for (int j = 0; j < n_bottom; j++) cnt += w_hi[order[j]] - w_lo[order[j]] + 1;
+                if (cnt <= NARROW_REG_POOL * WAVE) {
+                    // the pool in registers, value q = lane + 64 r: the whole wave gathers it, the sequential sum
+                    // (:259-263) walks it in pool order through v_readlane (no LDS latency in the chain), and the
+                    // select's passes read no memory
+                    int cum[5], base[4];
+                    cum[0] = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const bool in = j < n_bottom;
+                        const int wj = in ? order[j] : 0;
+                        cum[j + 1] = cum[j] + (in ? w_hi[wj] - w_lo[wj] + 1 : 0);
+                        base[j] = (in ? sh_woff[wj] : 0) - cum[j];  // dbs index of pool value q in window j
+                    }
+                    float v[NARROW_REG_POOL];
+                    // the pool in order, aligned for lane 0's float4 reads, over the staged bins (dead after the
+                    // scans, whose reads completed before the barrier after the window sort)
+                    float *pl = stage;
+#pragma unroll
+                    for (int r = 0; r < NARROW_REG_POOL; r++) {
+                        const int q = lane + WAVE * r;
+                        int bq = base[0];
+#pragma unroll
+                        for (int j = 1; j < 4; j++) bq = (q >= cum[j]) ? base[j] : bq;
+                        v[r] = (q < cnt) ? dbs[q + bq] : 0.0f;
+                    }
+                    __syncthreads();  // the pool may overlap the first dB values: every gather first
+#pragma unroll
+                    for (int r = 0; r < NARROW_REG_POOL; r++) {
+                        const int q = lane + WAVE * r;
+                        if (q < ((cnt + 15) & ~15)) pl[q] = v[r];  // zero tail up to a 16-value block
+                    }
+                    __syncthreads();
+                    if (lane == 0) {
+                        // 16 values per block read as four float4, the next block's reads issued before this
+                        // block's adds; the zero tail is not added
+                        float m = 0.0f;
+                        float4 A[4], B[4];
+                        auto rd = [&](float4 (&X)[4], int u) {
+#pragma unroll
+                            for (int i = 0; i < 4; i++) X[i] = *reinterpret_cast<const float4 *>(pl + u + 4 * i);
+                        };
+                        auto add16 = [&](const float4 (&X)[4], int n) {
+                            const float x[16] = {X[0].x, X[0].y, X[0].z, X[0].w, X[1].x, X[1].y, X[1].z, X[1].w,
+                                                 X[2].x, X[2].y, X[2].z, X[2].w, X[3].x, X[3].y, X[3].z, X[3].w};
+                            if (n >= 16) {
+#pragma unroll
+                                for (int i = 0; i < 16; i++) m += x[i];
+                            } else {
+#pragma unroll
+                                for (int i = 0; i < 16; i++)
+                                    if (i < n) m += x[i];
+                            }
+                        };
+                        rd(A, 0);
+                        for (int q = 0; q < cnt; q += 32) {
+                            if (q + 16 < cnt) rd(B, q + 16);
+                            add16(A, cnt - q);
+                            if (q + 16 >= cnt) break;
+                            if (q + 32 < cnt) rd(A, q + 32);
+                            add16(B, cnt - q - 16);
+                        }
+                        sh_f[2] = m / (float)cnt;
+                    }
+                    __syncthreads();
+                    per_bin_mean = sh_f[2];
+                    STATS_STAMP(3);
+#pragma unroll
+                    for (int r = 0; r < NARROW_REG_POOL; r++) v[r] = fabsf(v[r] - per_bin_mean);
+                    med = kth_smallest<WG>(
+                        [&](auto f) {
+#pragma unroll
+                            for (int r = 0; r < NARROW_REG_POOL; r++)
+                                if (lane + WAVE * r < cnt) f(__float_as_uint(v[r]));
+                        },
+                        cnt / 2, hist, sh_xch);
+                } else {
+                    if (lane == 0) {
+                        float m = 0.0f;
+                        for (int j = 0; j < n_bottom; j++) {
+                            const int wj = order[j], len = w_hi[wj] - w_lo[wj] + 1;
+                            const float *d = dbs + sh_woff[wj];
+#pragma unroll 8
+                            for (int i = 0; i < len; i++) m += d[i];
+                        }
+                        sh_f[2] = m / (float)cnt;
+                    }
+                    __syncthreads();
+                    per_bin_mean = sh_f[2];
+                    STATS_STAMP(3);
+                    med = kth_smallest<WG>(
+                        [&](auto f) {
+                            for (int j = 0; j < n_bottom; j++) {
+                                const int wj = order[j], len = w_hi[wj] - w_lo[wj] + 1;
+                                const float *d = dbs + sh_woff[wj];
+                                for (int i = lane; i < len; i += WG) f(__float_as_uint(fabsf(d[i] - per_bin_mean)));
+                            }
+                        },
+                        cnt / 2, hist, sh_xch);
+                }
+            } else if (spec_pool) {
+                // one bottom window: its dB sum came out of the wide scan (same values, same order, from 0); the
+                // pool holds the |dB - mean| gaps directly
                 const int wb = order[0];
                 const int lo = w_lo[wb], hi = w_hi[wb];
                 cnt = hi - lo + 1;
                 if (lane == 0) sh_f[2] = w_dsum[wb] / (float)cnt;
                 __syncthreads();
-                const float m = sh_f[2];
-                if (WIDE && cnt <= REG_POOL * WG) {
+                per_bin_mean = sh_f[2];
+                const float m = per_bin_mean;
+                if (cnt <= REG_POOL * WG) {
                     // gaps in registers: the select's passes read no memory
                     float v[REG_POOL];
 #pragma unroll
@@ -668,53 +787,37 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                                 if (lane + WG * r < cnt) f(__float_as_uint(v[r]));
                         },
                         cnt / 2, hist, sh_xch);
-                    med_done = true;
                 } else {
 #pragma unroll 4
                     for (int i = lo + lane; i <= hi; i += WG) pool[i - lo] = fabsf(db_of(P[i]) - m);
                     __syncthreads();
+                    STATS_STAMP(3);
+                    med = kth_smallest_of<WG>(pool, cnt, cnt / 2, hist, sh_xch);
                 }
             } else {
+                // several bottom windows (wide): pooled in HBM scratch, summed in order by one thread
                 for (int j = 0; j < n_bottom; j++) {
                     const int wj = order[j], len = w_hi[wj] - w_lo[wj] + 1;
-                    const float *src = WIDE ? P + w_lo[wj] : stage + sh_woff[wj];
+                    const float *src = P + w_lo[wj];
 #pragma unroll 8
                     for (int i = lane; i < len; i += WG) {
                         const int q = cnt + i;
-                        if (q < pool_cap) pool[q] = db_of(src[i]);
+                        if (q < g.max_pool) pool[q] = db_of(src[i]);
                     }
                     cnt += len;
                 }
-                if (cnt > pool_cap) cnt = pool_cap;  // host sizes max_pool from the geometry
+                if (cnt > g.max_pool) cnt = g.max_pool;  // host sizes max_pool from the geometry
                 __syncthreads();
-            }
-            if (lane == 0 && !spec_pool) {
-                // sequential sum in pool order (:259-263); 16 values per step read with 4 ds_read_b128
-                float m = 0.0f;
-                int q = 0;
-                for (; q + 16 <= cnt; q += 16) {
-                    float4 b[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) b[u] = *reinterpret_cast<const float4 *>(&pool[q + 4 * u]);
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        m += b[u].x;
-                        m += b[u].y;
-                        m += b[u].z;
-                        m += b[u].w;
-                    }
+                if (lane == 0) {
+                    float m = 0.0f;
+#pragma unroll 8
+                    for (int q = 0; q < cnt; q++) m += pool[q];
+                    sh_f[2] = m / (float)cnt;
                 }
-                for (; q < cnt; q++) m += pool[q];
-                m /= (float)cnt;
-                sh_f[2] = m;
-            }
-            __syncthreads();
-            const float per_bin_mean = sh_f[2];
-            if (!spec_pool) {
+                __syncthreads();
+                per_bin_mean = sh_f[2];
                 for (int q = lane; q < cnt; q += WG) pool[q] = fabsf(pool[q] - per_bin_mean);
                 __syncthreads();
-            }
-            if (!med_done) {
                 STATS_STAMP(3);
                 med = kth_smallest_of<WG>(pool, cnt, cnt / 2, hist, sh_xch);
             }
@@ -854,14 +957,13 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
         hipLaunchKernelGGL(stats_kernel<WIDE_WG>, dim3(n_frames), dim3(WIDE_WG), lds, stream, spectra, geo, now_ms,
                            state, records, gpool, pool_stride);
     } else {
-        // the staged windows, then the pool (<= the staged bins: it pools whole windows)
+        // the staged windows' bins (later the pool in order, + a 16-value zero tail), then their dB values
         const int staged = (stage_bins(geo) + 3) & ~3;
-        const int pool = std::min(pool_stride, staged);
-        const size_t lds = sizeof(float) * (size_t)(staged + pool + 4);
-        hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel<WAVE>), (2 * STAGE_MAX + 4) * 4);
+        const size_t lds = sizeof(float) * (size_t)(2 * staged + 16);
+        hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel<WAVE>), (2 * STAGE_MAX + 16) * 4);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(stats_kernel<WAVE>, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms, state,
-                           records, nullptr, pool);
+                           records, nullptr, 0);
     }
     if (SDRG_STATS_STAMPS) {  // diagnostic build: mean cycles per phase over the frames of this call
         std::vector<unsigned long long> h((size_t)STAMP_PHASES * 8192);
