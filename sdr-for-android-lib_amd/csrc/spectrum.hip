@@ -316,7 +316,7 @@ namespace k16 {
 constexpr int ABL = SDRG_K16_ABLATE;
 
 constexpr int LOG2N = 14, N = 1 << LOG2N, T = N / E, HALF = N / 2;
-constexpr int XCH_F2 = HALF + HALF / 32;  // padded half-frame exchange buffer, f2 slots
+constexpr int XCH_F2 = HALF;              // half-frame exchange buffer, f2 slots (XOR-swizzled, no padding)
 constexpr int P1_F2 = 32 * 32;            // P1[r][k] = w_1024^(r k), r, k < 32
 constexpr int A2_F4 = 16;                 // A2[m] = (w_16384^(2m), w_16384^(2m+1)), m < 16
 constexpr int TAB_FLOATS = 2 * P1_F2 + 4 * A2_F4;
@@ -324,6 +324,67 @@ constexpr int LDS_BYTES = XCH_F2 * 8 + P1_F2 * 8 + A2_F4 * 16;
 static_assert(2 * LDS_BYTES <= 160 * 1024, "two workgroups per CU");
 
 typedef float f2s __attribute__((ext_vector_type(2)));
+
+// The exchanges move half a frame at a time through XCH_F2 slots.  Slot s of a half is stored at
+// s ^ (2 ((s >> 5) & 15)): the XOR permutes 16-byte units inside each 256-byte row, so every access pattern
+// below -- a thread's 32 consecutive slots written as float4 pairs, 16 lanes reading consecutive slots, and
+// 16 lanes reading float4 pairs 2t, 2t + 1 -- spreads a wave's 16-lane groups over all 16 bank groups, and
+// a pair stays 16-byte aligned and adjacent, so half the exchange traffic moves as ds_read/write_b128.
+__device__ __forceinline__ float4 pair4(f2 a, f2 b) { return make_float4(a.x, a.y, b.x, b.y); }
+
+// pass-0 outputs (radix 32, NS = 1: thread t writes slots 32 t + r) -> pass-1 inputs (thread t reads t + 512 r)
+__device__ __forceinline__ void exch1(f2 *lds, f2 (&v)[E]) {
+    const int t = threadIdx.x;
+    char *lb = reinterpret_cast<char *>(lds);
+    f2 nxt[E];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if ((t >= T / 2) == (h == 1)) {
+            const int tp = t - h * (T / 2);
+            int row = 256 * tp + ((tp & 15) << 4);  // byte offset of the row, ORed with its XOR
+            asm volatile("" : "+v"(row));  // per frame: hoisted out of the frame loop, the 16 addresses hold 16 VGPRs
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                *reinterpret_cast<float4 *>(lb + (row ^ (q << 4))) = pair4(v[2 * q], v[2 * q + 1]);
+                __builtin_amdgcn_sched_barrier(0);  // one pair's 4-register tuple at a time
+            }
+        }
+        __syncthreads();
+        const f2 *rb = lds + (t ^ (2 * ((t >> 5) & 15)));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) nxt[16 * h + r] = rb[512 * r];
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = nxt[i];
+}
+
+// pass-1 outputs (radix 32, NS = 32: slots (t / 32) 1024 + t mod 32 + 32 r) -> pass-2 inputs (radix 16, butterflies
+// 2t and 2t + 1: slots 2t + b + 1024 r, read as float4 pairs)
+__device__ __forceinline__ void exch2(f2 *lds, f2 (&v)[E]) {
+    const int t = threadIdx.x;
+    f2 nxt[E];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (((t >> 5) >= 8) == (h == 1)) {
+            int row = ((t >> 5) - 8 * h) * 1024 + (t & 31);
+            asm volatile("" : "+v"(row));  // as in exch1
+#pragma unroll
+            for (int r = 0; r < 32; ++r) lds[(row ^ (2 * (r & 15))) + 32 * r] = v[r];
+        }
+        __syncthreads();
+        const float4 *rb = reinterpret_cast<const float4 *>(lds + ((2 * t) ^ (2 * ((t >> 4) & 15))));
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float4 p = rb[512 * r];  // slots 2t, 2t + 1 of row 1024 r
+            nxt[8 * h + r] = f2{p.x, p.y};
+            nxt[16 + 8 * h + r] = f2{p.z, p.w};
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[i] = nxt[i];
+}
 
 // raw samples x[t + 512 r] of frame f into registers (zero-extended 16/32-bit words)
 template <int FMT>
@@ -368,14 +429,14 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
         }
         const int next = frame + gridDim.x;
         if constexpr (!(ABL & 8)) dft<32>(v);
-        if constexpr (!(ABL & 4)) exchange<LOG2N, 32, 1, 32, false>(xch, v);
+        if constexpr (!(ABL & 4)) exch1(xch, v);
         // ---- pass 1: radix 32, NS = 32 ----
         if constexpr (!(ABL & 1)) {
 #pragma unroll
             for (int r = 1; r < 32; ++r) v[r] = cmul_v(v[r], p1_row[r * 32]);
         }
         if constexpr (!(ABL & 8)) dft<32>(v);
-        if constexpr (!(ABL & 4)) exchange<LOG2N, 32, 32, 16, true>(xch, v);
+        if constexpr (!(ABL & 4)) exch2(xch, v);
         // ---- pass 2: radix 16, NS = 1024, butterflies j = 2t + b held as v[16 b + r] ----
         if constexpr (!(ABL & 2)) {
             f2 wa, wb;  // w_16384^j for j = 2t, 2t + 1

@@ -5,7 +5,8 @@ set -e
 NAME=$1; FLAGS=$2
 D=sdr-for-android-lib_amd; B=$D/build/variant_$NAME; mkdir -p $B
 HIP="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-atomics $FLAGS"
-$HIP -c $D/csrc/spectrum.hip -o $B/spectrum.o
+# SPECTRUM_SRC: an alternative spectrum.hip (A/B of a kernel change in one GPU session)
+$HIP -I$D/csrc -Iinclude -c ${SPECTRUM_SRC:-$D/csrc/spectrum.hip} -o $B/spectrum.o
 $HIP -c $D/csrc/fftany.hip -o $B/fftany.o
 $HIP -ffp-contract=off -fno-slp-vectorize -c $D/csrc/stats.hip -o $B/stats.o
 $HIP -ffp-contract=off -fno-slp-vectorize -c $D/csrc/ssb.hip -o $B/ssb.o
