@@ -15,6 +15,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "sdrg_internal.h"
@@ -657,7 +658,9 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                 // the pool is the bottom windows' staged dB values, window after window in sorted order
                 const float *dbs = stage + stage_pad;
                 for (int j = 0; j < n_bottom; j++) cnt += w_hi[order[j]] - w_lo[order[j]] + 1;
-                if (cnt <= NARROW_REG_POOL * WAVE) {
+                // the pool in registers, R values per lane: 8 (c2's 4 x 82 bins) or 24 (c5's 4 x 327)
+                auto reg_pool = [&](auto r_const) {
+                    constexpr int R = decltype(r_const)::value;
                     // the pool in registers, value q = lane + 64 r: the whole wave gathers it, the sequential sum
                     // (:259-263) walks it in pool order through v_readlane (no LDS latency in the chain), and the
                     // select's passes read no memory
@@ -670,12 +673,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                         cum[j + 1] = cum[j] + (in ? w_hi[wj] - w_lo[wj] + 1 : 0);
                         base[j] = (in ? sh_woff[wj] : 0) - cum[j];  // dbs index of pool value q in window j
                     }
-                    float v[NARROW_REG_POOL];
+                    float v[R];
                     // the pool in order, aligned for lane 0's float4 reads, over the staged bins (dead after the
                     // scans, whose reads completed before the barrier after the window sort)
                     float *pl = stage;
 #pragma unroll
-                    for (int r = 0; r < NARROW_REG_POOL; r++) {
+                    for (int r = 0; r < R; r++) {
                         const int q = lane + WAVE * r;
                         int bq = base[0];
 #pragma unroll
@@ -684,7 +687,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                     }
                     __syncthreads();  // the pool may overlap the first dB values: every gather first
 #pragma unroll
-                    for (int r = 0; r < NARROW_REG_POOL; r++) {
+                    for (int r = 0; r < R; r++) {
                         const int q = lane + WAVE * r;
                         if (q < ((cnt + 15) & ~15)) pl[q] = v[r];  // zero tail up to a 16-value block
                     }
@@ -724,14 +727,19 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                     per_bin_mean = sh_f[2];
                     STATS_STAMP(3);
 #pragma unroll
-                    for (int r = 0; r < NARROW_REG_POOL; r++) v[r] = fabsf(v[r] - per_bin_mean);
+                    for (int r = 0; r < R; r++) v[r] = fabsf(v[r] - per_bin_mean);
                     med = kth_smallest<WG>(
                         [&](auto f) {
 #pragma unroll
-                            for (int r = 0; r < NARROW_REG_POOL; r++)
+                            for (int r = 0; r < R; r++)
                                 if (lane + WAVE * r < cnt) f(__float_as_uint(v[r]));
                         },
                         cnt / 2, hist, sh_xch);
+                };
+                if (cnt <= 8 * WAVE) {
+                    reg_pool(std::integral_constant<int, 8>{});
+                } else if (cnt <= NARROW_REG_POOL * WAVE) {
+                    reg_pool(std::integral_constant<int, NARROW_REG_POOL>{});
                 } else {
                     if (lane == 0) {
                         float m = 0.0f;
