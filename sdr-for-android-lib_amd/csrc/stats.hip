@@ -34,6 +34,7 @@ constexpr int STAGE_MAX = 8192;  // bins staged into LDS for the window scans (3
 #endif
 constexpr int STAMP_PHASES = 10;
 
+
 __device__ unsigned long long g_stats_stamps[STAMP_PHASES * 8192];
 #define STATS_STAMP(k)                                                                                        \
     do {                                                                                                      \
@@ -50,36 +51,44 @@ struct WinScan {
 };
 
 // One lane replays the reference's sequential loops over the window P[lo..hi], staged in LDS at W (W[i - lo]).
-// (The window's own base pointer, not a virtual P: LDS pointers must stay inside the allocation.)
+// (The window's own base pointer, not a virtual P: LDS pointers must stay inside the allocation.)  The window
+// sum (:190-193) and the best-1-kHz scan (:171-178) run in one loop: the scan's first window sum is the window
+// sum's first w terms in the same order (the same float), and after it the two chains are independent, so
+// they overlap instead of running one after the other.
 __device__ __forceinline__ WinScan scan_window(const float *__restrict__ W, int lo, int hi, int w) {
     WinScan r;
-    float s = 0.0f;
     const int len = hi - lo + 1;
-#pragma unroll 8
-    for (int i = 0; i < len; i++) s += W[i];
-    r.sum = s;
     r.best_start = lo;
-    if (len <= 0) {
-        r.best1k = 0.0f;
-    } else if (len < w) {
-        r.best1k = s / len;
-    } else {
-        float rs = 0.0f;
+    float s = 0.0f;
+    int i = 0;
+    const int head = len < w ? len : w;
 #pragma unroll 8
-        for (int i = 0; i < w; i++) rs += W[i];
-        float bv = rs;
-#pragma unroll 4
-        for (int st = 1; st + w - 1 < len; st++) {
-            rs += W[st + w - 1] - W[st - 1];
-            if (rs > bv) {
-                bv = rs;
-                r.best_start = lo + st;
-            }
-        }
-        // the reference keeps best = max over st of rs/w (:171-178); x -> RN(x / w) is monotone for w > 0,
-        // so that maximum is exactly RN(max rs / w): one division instead of one per step
-        r.best1k = bv / w;
+    for (; i < head; i++) s += W[i];
+    if (len <= 0) {
+        r.sum = s;
+        r.best1k = 0.0f;
+        return r;
     }
+    if (len < w) {
+        r.sum = s;
+        r.best1k = s / len;
+        return r;
+    }
+    float rs = s, bv = s;
+#pragma unroll 8
+    for (; i < len; i++) {
+        const float x = W[i];
+        s += x;
+        rs += x - W[i - w];
+        if (rs > bv) {
+            bv = rs;
+            r.best_start = lo + i - w + 1;
+        }
+    }
+    r.sum = s;
+    // the reference keeps best = max over st of rs/w (:171-178); x -> RN(x / w) is monotone for w > 0,
+    // so that maximum is exactly RN(max rs / w): one division instead of one per step
+    r.best1k = bv / w;
     return r;
 }
 
@@ -326,6 +335,124 @@ __device__ __forceinline__ float kth_of4(float (&g)[4], int k) {
     return r;
 }
 
+// ---- per-frame scalar parts, shared by the narrow and the wide kernel (one lane per frame) ----
+__device__ __forceinline__ int n_bottom_of(int n_ref) {
+    const int nb0 = (int)(n_ref * 0.4f);  // nBottom (:233), <= 4 (n_ref <= 10)
+    return nb0 > 1 ? nb0 : 1;
+}
+
+// 6.4a (:235-247): mean SNR over the nBottom lowest windows (order: the windows sorted by mean dB)
+__device__ __forceinline__ void mean_snr_6_4a(const float *w_mean_db, const int *order, int n_ref, float signal_power_db,
+                                              StatsState &st) {
+    const int n_bottom = n_bottom_of(n_ref);
+    float key[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) key[i] = (i < n_ref) ? w_mean_db[order[i]] : INFINITY;
+    float mean = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        if (i < n_bottom) mean += key[i];
+    mean /= n_bottom;
+    float gp[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) gp[i] = (i < n_bottom) ? fabsf(key[i] - mean) : INFINITY;
+    const float sigma = fmax_ref(1.4816f * kth_of4(gp, n_bottom / 2), 0.5f);
+    const float snr_db = signal_power_db - mean;
+    st.mean_snr_db = snr_db;
+    st.mean_snr_sigma = snr_db / sigma;
+}
+
+// 6.4b tail + 6.4c (:274, :281-288) + 6.4d (:292-327)
+__device__ __forceinline__ void snr_6_4cd(const StatsGeometry &g, StatsState &st, float abs_peak_db, float pbm,
+                                          float sigma_bin, int n_bottom, const float *w_best1k_db, const int *order,
+                                          float focus_best1k_linear, int best_start) {
+    const int w1k = g.win_bins_1k;
+    st.peak_above_noise_mean_db = abs_peak_db - pbm;  // :274
+    const float logN = logf((float)g.focus_len);
+    const float sqrt2logN = sqrtf(2.0f * logN);
+    const float gumbel_loc = pbm + sigma_bin * sqrt2logN;
+    const float gumbel_sig = fmax_ref(sigma_bin * 3.14159f / (sqrtf(6.0f) * sqrt2logN), 0.5f);
+    st.max_bin_snr_db = abs_peak_db - gumbel_loc;
+    st.max_bin_snr_sigma = st.max_bin_snr_db / gumbel_sig;
+    float mean1k = 0.0f;
+    for (int i = 0; i < n_bottom; i++) mean1k += w_best1k_db[order[i]];
+    mean1k /= n_bottom;
+    float g1k[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) g1k[i] = (i < n_bottom) ? fabsf(w_best1k_db[order[i]] - mean1k) : INFINITY;
+    const float sigma_floor_1k = sigma_bin / sqrtf((float)w1k);
+    float sigma1k = 1.4816f * kth_of4(g1k, n_bottom / 2);
+    if (sigma1k < sigma_floor_1k) sigma1k = sigma_floor_1k;
+    if (sigma1k < 0.5f) sigma1k = 0.5f;
+    if (focus_best1k_linear > 0.0f) {
+        const float focus_best1k_db = db_of(focus_best1k_linear);
+        st.best1khz_snr_db = focus_best1k_db - mean1k;
+        st.best1khz_snr_sigma = st.best1khz_snr_db / sigma1k;
+        st.best1khz_center_freq_hz = (best_start + w1k / 2) * g.freq_per_bin + g.cf_minus_nyq;
+    } else {
+        st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
+    }
+}
+
+// 6.5 frequency tracking (:333-361), clock injected; 6.6 detection (:365-378)
+__device__ __forceinline__ void track_detect_6_5_6_6(const StatsGeometry &g, StatsState &st, int valid,
+                                                     float abs_peak_db, int peak_bin, int64_t now_ms) {
+    if (st.tracking_frequency == 0.0f) st.tracking_frequency = g.cf_float;
+    if (st.center_frequency_changed) {
+        st.tracking_frequency = g.cf_float;
+        st.center_frequency_changed = 0;
+    }
+    if (!st.max_peak_set) {
+        st.max_peak_db = -130.0f;
+        st.max_peak_freq = g.cf_float;
+        st.max_peak_set = 1;
+    }
+    if (valid && abs_peak_db > st.max_peak_db) {
+        st.max_peak_db = abs_peak_db;
+        st.max_peak_freq = peak_bin * g.freq_per_bin + g.cf_u32_minus_nyq;
+        st.time_last_max_peak_ms = now_ms;
+    }
+    const int64_t ms_since = now_ms - st.time_last_max_peak_ms;
+    if (st.time_last_update_ms < st.time_last_max_peak_ms && ms_since > 300) {
+        st.tracking_frequency = st.max_peak_freq;
+        st.time_last_update_ms = now_ms;
+        st.max_peak_db = -130.0f;
+    }
+    const bool above = valid && (st.mean_snr_sigma >= 4.0f);
+    if (above) {
+        if (st.peak_confirmed < 1) st.peak_confirmed++;
+    } else {
+        st.peak_confirmed = 0;
+    }
+    const int flag = (above && st.peak_confirmed >= 1) ? 3 : 0;
+    // det_buf[det_idx] = flag with constant indices (no private-memory indexing)
+    const int d0 = (st.det_idx == 0) ? flag : st.det_buf[0];
+    const int d1 = (st.det_idx == 1) ? flag : st.det_buf[1];
+    const int d2 = (st.det_idx == 2) ? flag : st.det_buf[2];
+    st.det_buf[0] = d0;
+    st.det_buf[1] = d1;
+    st.det_buf[2] = d2;
+    st.det_idx = (st.det_idx + 1) % 3;
+    int m = d0;
+    if (d1 > m) m = d1;
+    if (d2 > m) m = d2;
+    st.detection_flag_sent = m;
+}
+
+__device__ __forceinline__ void finish_record(sdrg_frame_record &rec, const StatsState &st) {
+    rec.tracking_frequency = (int64_t)roundf(st.tracking_frequency);
+    rec.mean_snr_db = st.mean_snr_db;
+    rec.mean_snr_sigma = st.mean_snr_sigma;
+    rec.peak_above_noise_mean_db = st.peak_above_noise_mean_db;
+    rec.max_bin_snr_db = st.max_bin_snr_db;
+    rec.max_bin_snr_sigma = st.max_bin_snr_sigma;
+    rec.best1khz_snr_db = st.best1khz_snr_db;
+    rec.best1khz_snr_sigma = st.best1khz_snr_sigma;
+    rec.best1khz_center_freq_hz = st.best1khz_center_freq_hz;
+    rec.per_bin_mean = st.per_bin_mean;
+    rec.detection_flag = st.detection_flag_sent;
+}
+
 // k-th smallest (0-based) of non-negative floats in vals[0..cnt) by an 8-bit-digit radix select (WG threads).
 // Bits that every value shares (AND == OR, found by one pass) need no digit pass, so the first histogram splits on
 // the highest bit where the values differ: the values are spread over the bins instead of all landing in the few
@@ -424,82 +551,164 @@ __device__ float kth_smallest_of(const float *vals, int cnt, int k, int *hist, u
 constexpr int REG_POOL = 64;
 constexpr int NARROW_REG_POOL = 24;  // the narrow kernel's pool in registers up to 24 x 64 values
 
-// WG = WAVE: one wave per frame, window bins staged in LDS (or read from HBM); WG = WIDE_WG: wide windows
-// (scan_wide), the pool in the frame's slice of the global scratch gpool.
-template <int WG>
-__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void stats_kernel(const float *__restrict__ spectra, StatsGeometry g,
-                                                     int64_t now_ms, StatsState *__restrict__ state,
-                                                     sdrg_frame_record *__restrict__ records, float *gpool,
-                                                     int gpool_stride) {
-    // dynamic LDS: narrow, the staged bins of every window (window q at stage + sh_woff[q]), then their dB
-    // values at the same offsets (the focus peak, the pooled bins); wide, scan_wide's ring (the pool is in the
-    // frame's slice of gpool)
-    extern __shared__ __attribute__((aligned(16))) float dyn[];
-    float *stage = dyn;
-    __shared__ int sh_woff[12];
-    __shared__ __attribute__((aligned(16))) int hist[256];
-    __shared__ uint32_t sh_xch[10];
-    __shared__ WideScan sh_wide;
-    constexpr bool WIDE = WG > WAVE;
-    __shared__ int sh_nbottom, sh_best_start;
-    __shared__ float w_mean_db[10], w_best1k_db[10], w_dsum[10];
-    __shared__ int w_lo[10], w_hi[10], order[10];
-    __shared__ float sh_f[4];
-    __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
+extern "C" __device__ uint32_t __ockl_wfred_and_u32(uint32_t);
+extern "C" __device__ uint32_t __ockl_wfred_or_u32(uint32_t);
+extern "C" __device__ int __ockl_wfscan_add_i32(int, bool);
 
-    const int lane = threadIdx.x;
-    const size_t frame = blockIdx.x;
-    // the window bounds are indexed by lane below: copy them out of the kernel arguments with constant
-    // indices (a lane-indexed kernarg array would be copied to scratch)
+// k-th smallest for FPW frames per wave: lane group fg (G = 64 / FPW lanes) selects in its own values (visit
+// calls f(bits) for the values this lane holds; groups with active == false take no part).  The same radix
+// select as kth_smallest, with a 256-bin histogram per group and a group-wide scan (256 / G bins per lane).
+template <int G, class Visit>
+__device__ float kth_smallest_group(Visit visit, int k, bool active, int (*hist)[256], uint32_t (*xch)[2]) {
+    constexpr int FPW = WAVE / G, B = 256 / G;
+    const int lane = threadIdx.x, fg = lane / G, gl = lane % G;
+    int *h = hist[fg];
+    uint32_t band = 0xffffffffu, bor = 0u;
+    if (active)
+        visit([&](uint32_t b) {
+            band &= b;
+            bor |= b;
+        });
+    if constexpr (G == WAVE) {  // DPP wave reductions (no LDS round trips)
+        band = __ockl_wfred_and_u32(band);
+        bor = __ockl_wfred_or_u32(bor);
+    } else {
+        for (int off = G / 2; off > 0; off >>= 1) {  // xor partners stay inside the aligned group
+            band &= (uint32_t)__shfl_xor((int)band, off);
+            bor |= (uint32_t)__shfl_xor((int)bor, off);
+        }
+    }
+    const uint32_t diff = band ^ bor;
+    int top = (active && diff != 0) ? 31 - __clz(diff) : -1;  // highest bit where the values differ
+    uint32_t mask = (top < 0 || top >= 31) ? 0u : ~((2u << top) - 1u);
+    uint32_t prefix = top < 0 ? band : band & mask;  // top < 0: every value equal (or no frame)
+    while (__ballot(top >= 0)) {
+        const bool on = top >= 0;
+        const int lo = top >= 7 ? top - 7 : 0;
+        const uint32_t dm = on ? (1u << (top - lo + 1)) - 1u : 0u;
 #pragma unroll
-    for (int i = 0; i < 10; i++) {
+        for (int i = 0; i < B; i += 4) *reinterpret_cast<int4 *>(&h[gl * B + i]) = make_int4(0, 0, 0, 0);
+        __syncthreads();
+        if (on)
+            visit([&](uint32_t b) {
+                if ((b & mask) == prefix) atomicAdd(&h[(b >> lo) & dm], 1);
+            });
+        __syncthreads();
+        int hv[B];
+#pragma unroll
+        for (int i = 0; i < B; i += 4) {
+            const int4 q = *reinterpret_cast<const int4 *>(&h[gl * B + i]);
+            hv[i] = q.x;
+            hv[i + 1] = q.y;
+            hv[i + 2] = q.z;
+            hv[i + 3] = q.w;
+        }
+        int own = 0;
+#pragma unroll
+        for (int i = 0; i < B; i++) own += hv[i];
+        int incl = own;
+        if constexpr (G == WAVE) {
+            incl = __ockl_wfscan_add_i32(own, true);  // DPP inclusive scan
+        } else {
+#pragma unroll
+            for (int off = 1; off < G; off <<= 1) {
+                const int v = __shfl_up(incl, off);
+                if (gl >= off) incl += v;
+            }
+        }
+        const unsigned long long over = __ballot(on && incl > k);  // per group non-empty: k < candidates
+        const int L = __ffsll((long long)((over >> (fg * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1)))) - 1;
+        if (on && gl == L) {
+            int acc = incl - own, j = B - 1;
+            bool found = false;
+#pragma unroll
+            for (int t = 0; t < B; t++) {  // the first of the lane's bins that passes k
+                const bool here = !found && acc + hv[t] > k;
+                j = here ? t : j;
+                found = found || here;
+                acc += found ? 0 : hv[t];
+            }
+            xch[fg][0] = (uint32_t)(L * B + j);
+            xch[fg][1] = (uint32_t)acc;
+        }
+        __syncthreads();
+        if (on) {
+            const uint32_t d = xch[fg][0];
+            k -= (int)xch[fg][1];
+            prefix |= d << lo;
+            mask |= dm << lo;
+            top = lo - 1;
+        }
+        __syncthreads();
+    }
+    (void)FPW;
+    return __uint_as_float(prefix);
+}
+
+// Narrow statistics, FPW frames per wave (lane group fg = lane / G of G = 64 / FPW lanes holds frame
+// blockIdx.x * FPW + fg).  Every window's bins are staged compactly into the group's LDS region (window q at
+// sh_woff[q]) with their dB values, all of a lane's loads in flight at once; the focus peak is evaluated during
+// that copy.  The order-free work (copy, dB, pooled gaps, select) runs across the group's lanes; the
+// reference's sequential sums run one lane per window (the window scans) or per frame (the pooled mean, the
+// scalar tail) -- and those, the chains that leave most of a wave's lanes idle, serve FPW frames per
+// instruction.  gf: floats of LDS per group.
+template <int FPW>
+__global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restrict__ spectra, StatsGeometry g,
+                                                            int64_t now_ms, StatsState *__restrict__ state,
+                                                            sdrg_frame_record *__restrict__ records, int n_frames,
+                                                            int gf) {
+    constexpr int G = WAVE / FPW;
+    extern __shared__ __attribute__((aligned(16))) float dyn[];
+    __shared__ int sh_woff[12];
+    __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
+    __shared__ __attribute__((aligned(16))) int hist[FPW][256];
+    __shared__ uint32_t sh_xch[FPW][2];
+    __shared__ float w_mean_db[FPW][10], w_best1k_db[FPW][10];
+    __shared__ int order[FPW][10];
+    __shared__ float sh_f[FPW][4];
+    __shared__ int sh_best_start[FPW];
+
+    const int lane = threadIdx.x, fg = lane / G, gl = lane % G;
+    const int frame = blockIdx.x * FPW + fg;
+    const bool active = frame < n_frames;
+    const int n_ref = g.n_ref;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {  // constant kernarg indices (a lane-indexed kernarg array would go to scratch)
         if (lane == i) {
             sh_geo_lo[i] = g.win_lo[i];
             sh_geo_hi[i] = g.win_hi[i];
         }
     }
-    const float *P = spectra + frame * (size_t)g.n;
     if (lane == 0) {
-        sh_geo_lo[g.n_ref] = g.focus_lo;
-        sh_geo_hi[g.n_ref] = g.focus_hi;
+        sh_geo_lo[n_ref] = g.focus_lo;
+        sh_geo_hi[n_ref] = g.focus_hi;
         int o = 0;
-        for (int q = 0; q <= g.n_ref; q++) {
+        for (int q = 0; q <= n_ref; q++) {
             sh_woff[q] = o;
-            o += max(0, (q < g.n_ref ? g.win_hi[q] - g.win_lo[q] : g.focus_hi - g.focus_lo) + 1);
+            o += max(0, (q < n_ref ? g.win_hi[q] - g.win_lo[q] : g.focus_hi - g.focus_lo) + 1);
         }
-        sh_woff[g.n_ref + 1] = o;
+        sh_woff[n_ref + 1] = o;
     }
     __syncthreads();
-    const int stage_total = sh_woff[g.n_ref + 1], stage_pad = (stage_total + 3) & ~3;
-    // narrow: the pool after the staged bins (LDS); wide: the frame's slice of gpool
-    float *pool = gpool + (size_t)blockIdx.x * gpool_stride;  // wide only
-    StatsState st = state[frame];
+    const int stage_total = sh_woff[n_ref + 1], stage_pad = (stage_total + 3) & ~3;
+    float *stage = dyn + fg * gf;
+    float *dbs = stage + stage_pad;
+    const float *P = spectra + (size_t)(active ? frame : 0) * g.n;
+    StatsState st{};
+    if (active) st = state[frame];
     if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
     sdrg_frame_record rec;
     __builtin_memset(&rec, 0, sizeof(rec));  // tail padding included: records compare and gather as bytes
     rec.peak_bin = -1;
     rec.abs_peak_db = -130.0f;
-    rec.signal_power_db = 0.0f;
-    rec.valid = 0;
-    rec.n_ref_windows = 0;
 
-    if (g.focus_len > 0 && (WIDE || stage_total <= STAGE_MAX)) {
+    if (g.focus_len > 0 && stage_total <= STAGE_MAX) {
         const int w1k = g.win_bins_1k;
-        const int n_ref = g.n_ref;
-        // narrow: every window's bins are staged into LDS (coalesced, all loads in flight at once), so the focus
-        // peak, the sequential per-lane scans and the pool read LDS instead of HBM; windows too wide to stage
-        // together take the wide kernel (scan_wide; launch_stats routes them by the same count)
-        const int nb_geo = max(1, (int)(n_ref * 0.4f));             // nBottom (:233), known from the geometry
-        const bool spec_pool = WIDE && n_ref >= 2 && nb_geo == 1;  // pooled-bin sum = one window's dB sum
-
-        // ---- 6.2 focus peak: first maximum of dB, seeded at -130 (fft_process.cpp:142-154), evaluated while
-        //      the focus bins are staged (wide: while scan_wide streams the focus window) ----
+        STATS_STAMP(0);
+        // ---- staging + 6.2 focus peak: first maximum of dB, seeded at -130 (fft_process.cpp:142-154) ----
         float best = -130.0f;
         int bidx = 0x7fffffff;
-        unsigned long long nst0 = 0, nst1 = 0, nst2 = 0;  // diagnostic stamps of the narrow path
-        if (!WIDE) STATS_STAMP(0);
-        if (SDRG_STATS_STAMPS) nst0 = __builtin_amdgcn_s_memtime();
-        if constexpr (!WIDE) {
+        {
             // staged bin i of window q reads P[i + dl[q]]; q = the number of window starts wo[] at or below i
             int wo[10], dl[11];
 #pragma unroll
@@ -507,27 +716,26 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
 #pragma unroll
             for (int k = 0; k < 10; k++) wo[k] = (k < n_ref) ? sh_woff[k + 1] : 0x7fffffff;
             const int foff = sh_woff[n_ref];
-            float *dbs = stage + stage_pad;
-            for (int base = lane; base < stage_total; base += 16 * WAVE) {
-                // 16 bins per lane in flight: every load issued before the first is used
+            const int lim = active ? stage_total : 0;
+            for (int base = gl; base < lim; base += 16 * G) {
                 float v[16];
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
-                    const int i = base + WAVE * u;
+                    const int i = base + G * u;
                     int d = dl[0];
 #pragma unroll
                     for (int k = 0; k < 10; k++) d = (i >= wo[k]) ? dl[k + 1] : d;
-                    v[u] = (i < stage_total) ? P[i + d] : 0.0f;
+                    v[u] = (i < lim) ? P[i + d] : 0.0f;
                 }
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
-                    const int i = base + WAVE * u;
-                    if (i < stage_total) {
+                    const int i = base + G * u;
+                    if (i < lim) {
                         const float d = db_of(v[u]);
                         stage[i] = v[u];
                         dbs[i] = d;
-                        // the focus window is the last: lanes see its bins in increasing order, strict > keeps
-                        // each lane's first maximum
+                        // the focus window is the last: a lane sees its bins in increasing order, strict >
+                        // keeps each lane's first maximum
                         if (i >= foff && d > best) {
                             best = d;
                             bidx = g.focus_lo + (i - foff);
@@ -535,7 +743,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                     }
                 }
             }
-            for (int off = WAVE / 2; off > 0; off >>= 1) {
+            for (int off = G / 2; off > 0; off >>= 1) {  // first maximum over the group (lower bin on ties)
                 const float ob = __shfl_xor(best, off);
                 const int oi = __shfl_xor(bidx, off);
                 if (ob > best || (ob == best && oi < bidx)) {
@@ -544,50 +752,249 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                 }
             }
         }
-
-        // ---- 6.2 focus sum + 6.3 reference windows: one lane per window (reference order), lane n_ref
-        //      takes the focus window; all of them run the same sequential scan in lockstep ----
-        if (SDRG_STATS_STAMPS) nst1 = __builtin_amdgcn_s_memtime();
         __syncthreads();
-        if (SDRG_STATS_STAMPS) nst2 = __builtin_amdgcn_s_memtime();
-        if constexpr (WIDE) {
-            STATS_STAMP(0);
-            if (spec_pool)
-                scan_wide<true>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, sh_wide);
-            else
-                scan_wide<false>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, sh_wide);
-            STATS_STAMP(1);
-            best = sh_wide.peak_db;
-            bidx = sh_wide.peak_idx;
-            if (lane < n_ref) w_dsum[lane] = sh_wide.dsum[lane];
-        }
+        if (SDRG_STATS_STAMPS && threadIdx.x == 0 && blockIdx.x < 8192)  // slot 6: the staging copy's cycles
+            g_stats_stamps[blockIdx.x * STAMP_PHASES + 6] = __builtin_amdgcn_s_memtime() - g_stats_stamps[blockIdx.x * STAMP_PHASES];
         const float abs_peak_db = best;
         const int peak_bin = (bidx == 0x7fffffff) ? g.focus_lo : bidx;
-        if (!WIDE && SDRG_STATS_STAMPS && threadIdx.x == 0 && blockIdx.x < 8192) {
-            g_stats_stamps[blockIdx.x * STAMP_PHASES + 6] = nst1 - nst0;
-            g_stats_stamps[blockIdx.x * STAMP_PHASES + 7] = nst2 - nst1;
-        }
-        if (lane <= n_ref) {
-            const bool is_focus = (lane == n_ref);
-            const int lo = sh_geo_lo[lane];
-            const int hi = sh_geo_hi[lane];
-            const int n = hi - lo + 1;
-            WinScan ws;
-            if constexpr (WIDE) {
-                ws.sum = sh_wide.sum[lane];
-                ws.best_start = lo;
-                if (n <= 0) {
-                    ws.best1k = 0.0f;
-                } else if (n < w1k) {
-                    ws.best1k = ws.sum / n;
-                } else {
-                    ws.best1k = sh_wide.bv[lane] / w1k;  // as scan_window: RN(max rs / w)
-                    ws.best_start = lo + sh_wide.best_e[lane] - w1k + 1;
-                }
+
+        // ---- 6.2 focus sum + 6.3 reference windows: lane gl scans window gl (the focus is window n_ref) ----
+        if (active && gl <= n_ref) {
+            const int lo = sh_geo_lo[gl], hi = sh_geo_hi[gl], n = hi - lo + 1;
+            const WinScan ws = scan_window(stage + sh_woff[gl], lo, hi, w1k);
+            if (gl == n_ref) {
+                sh_f[fg][0] = db_of(ws.sum / n);  // signalPowerDb (:155)
+                sh_f[fg][1] = ws.best1k;          // focusBest1kLinear (:302)
+                sh_best_start[fg] = ws.best_start;
             } else {
-                ws = scan_window(stage + sh_woff[lane], lo, hi, w1k);
+                w_mean_db[fg][gl] = db_of(ws.sum / n);
+                w_best1k_db[fg][gl] = db_of(ws.best1k);
             }
-            if (is_focus) {
+        }
+        __syncthreads();
+        STATS_STAMP(1);
+        const float signal_power_db = sh_f[fg][0];
+        const int valid = (n_ref >= 2);
+        rec.peak_bin = peak_bin;
+        rec.abs_peak_db = abs_peak_db;
+        rec.signal_power_db = signal_power_db;
+        rec.valid = valid;
+        rec.n_ref_windows = n_ref;
+
+        if (!valid) {
+            st.mean_snr_db = st.mean_snr_sigma = 0.0f;
+            st.peak_above_noise_mean_db = st.max_bin_snr_db = st.max_bin_snr_sigma = 0.0f;
+            st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
+        } else {
+            // std::sort of <= 16 elements in libstdc++ is a (stable) insertion sort: the same order is a sort by
+            // (meanDb, window index); lane gl places window gl at its rank
+            if (active && gl < n_ref) {
+                const float ki = w_mean_db[fg][gl];
+                int rank = 0;
+                for (int k = 0; k < n_ref; k++) {
+                    const float kk = w_mean_db[fg][k];
+                    rank += (kk < ki || (kk == ki && k < gl)) ? 1 : 0;
+                }
+                order[fg][rank] = gl;
+            }
+            __syncthreads();
+            const int n_bottom = n_bottom_of(n_ref);
+            if (active && gl == 0) mean_snr_6_4a(w_mean_db[fg], order[fg], n_ref, signal_power_db, st);
+            STATS_STAMP(2);
+
+            // ---- 6.4b pooled per-bin dB of the bottom windows, sorted-window order (:252-269) ----
+            int cnt = 0, cum[5], basej[4];
+            cum[0] = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const bool in = j < n_bottom;
+                const int wj = in ? order[fg][j] : 0;
+                cum[j + 1] = cum[j] + (in ? sh_geo_hi[wj] - sh_geo_lo[wj] + 1 : 0);
+                basej[j] = (in ? sh_woff[wj] : 0) - cum[j];  // dbs index of pool value q in window j
+            }
+            cnt = cum[4];
+            float med = 0.0f, per_bin_mean = 0.0f;
+            // the pool in registers (value q = gl + G r) when it fits, else visited in place
+            auto pooled = [&](auto r_const) {
+                constexpr int R = decltype(r_const)::value;
+                float v[R];
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const int q = gl + G * r;
+                    int bq = basej[0];
+#pragma unroll
+                    for (int j = 1; j < 4; j++) bq = (q >= cum[j]) ? basej[j] : bq;
+                    v[r] = (active && q < cnt) ? dbs[q + bq] : 0.0f;
+                }
+                // the pool in order, for lane 0's float4 reads, over the staged bins (dead since the scans); only a
+                // pool reaching the dB values waits for every lane's gather first
+                float *pl = stage;
+                if (((cnt + 15) & ~15) > stage_pad) __syncthreads();
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const int q = gl + G * r;
+                    if (active && q < ((cnt + 15) & ~15)) pl[q] = v[r];  // zero tail up to a 16-value block
+                }
+                __syncthreads();
+                if (active && gl == 0) {
+                    // the sequential sum (:259-263), 16 values per block read as four float4 one block ahead
+                    float m = 0.0f;
+                    float4 A[4], Bv[4];
+                    auto rd = [&](float4 (&X)[4], int u) {
+#pragma unroll
+                        for (int i = 0; i < 4; i++) X[i] = *reinterpret_cast<const float4 *>(pl + u + 4 * i);
+                    };
+                    auto add16 = [&](const float4 (&X)[4], int n) {
+                        const float x[16] = {X[0].x, X[0].y, X[0].z, X[0].w, X[1].x, X[1].y, X[1].z, X[1].w,
+                                             X[2].x, X[2].y, X[2].z, X[2].w, X[3].x, X[3].y, X[3].z, X[3].w};
+                        if (n >= 16) {
+#pragma unroll
+                            for (int i = 0; i < 16; i++) m += x[i];
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 16; i++)
+                                if (i < n) m += x[i];
+                        }
+                    };
+                    rd(A, 0);
+                    for (int q = 0; q < cnt; q += 32) {
+                        if (q + 16 < cnt) rd(Bv, q + 16);
+                        add16(A, cnt - q);
+                        if (q + 16 >= cnt) break;
+                        if (q + 32 < cnt) rd(A, q + 32);
+                        add16(Bv, cnt - q - 16);
+                    }
+                    sh_f[fg][2] = m / (float)cnt;
+                }
+                __syncthreads();
+                per_bin_mean = sh_f[fg][2];
+                STATS_STAMP(3);
+#pragma unroll
+                for (int r = 0; r < R; r++) v[r] = fabsf(v[r] - per_bin_mean);
+                med = kth_smallest_group<G>(
+                    [&](auto f) {
+#pragma unroll
+                        for (int r = 0; r < R; r++)
+                            if (gl + G * r < cnt) f(__float_as_uint(v[r]));
+                    },
+                    cnt / 2, active, hist, sh_xch);
+            };
+            if (cnt <= 8 * G) {
+                pooled(std::integral_constant<int, 8>{});
+            } else if (cnt <= NARROW_REG_POOL * G) {
+                pooled(std::integral_constant<int, NARROW_REG_POOL>{});
+            } else {
+                if (active && gl == 0) {
+                    float m = 0.0f;
+                    for (int j = 0; j < n_bottom; j++) {
+                        const int wj = order[fg][j], len = sh_geo_hi[wj] - sh_geo_lo[wj] + 1;
+                        const float *d = dbs + sh_woff[wj];
+#pragma unroll 8
+                        for (int i = 0; i < len; i++) m += d[i];
+                    }
+                    sh_f[fg][2] = m / (float)cnt;
+                }
+                __syncthreads();
+                per_bin_mean = sh_f[fg][2];
+                med = kth_smallest_group<G>(
+                    [&](auto f) {
+                        for (int j = 0; j < n_bottom; j++) {
+                            const int wj = order[fg][j], len = sh_geo_hi[wj] - sh_geo_lo[wj] + 1;
+                            const float *d = dbs + sh_woff[wj];
+                            for (int i = gl; i < len; i += G) f(__float_as_uint(fabsf(d[i] - per_bin_mean)));
+                        }
+                    },
+                    cnt / 2, active, hist, sh_xch);
+            }
+            STATS_STAMP(4);
+            const float sigma_bin = (cnt > 0) ? fmax_ref(1.4816f * med, 1.0f) : 1.0f;
+            if (cnt > 0) st.per_bin_mean = per_bin_mean;
+            const float pbm = (cnt > 0) ? per_bin_mean : 0.0f;
+            if (active && gl == 0)
+                snr_6_4cd(g, st, abs_peak_db, pbm, sigma_bin, n_bottom, w_best1k_db[fg], order[fg], sh_f[fg][1],
+                          sh_best_start[fg]);
+        }
+        STATS_STAMP(5);
+        if (active && gl == 0) track_detect_6_5_6_6(g, st, valid, abs_peak_db, peak_bin, now_ms);
+    }
+    if (active && gl == 0) {
+        finish_record(rec, st);
+        if (records) records[frame] = rec;
+        state[frame] = st;
+    }
+}
+
+// Wide statistics: windows too wide to stage together (BASELINE configs[4]: 65536 bins at a 200 kHz focus),
+// one WIDE_WG-thread workgroup per frame; the window scans in scan_wide, the pool in the frame's slice of the
+// global scratch gpool (or in registers when it fits).
+__global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) void stats_wide_kernel(
+    const float *__restrict__ spectra, StatsGeometry g, int64_t now_ms, StatsState *__restrict__ state,
+    sdrg_frame_record *__restrict__ records, float *gpool, int gpool_stride) {
+    constexpr int WG = WIDE_WG;
+    extern __shared__ __attribute__((aligned(16))) float dyn[];  // scan_wide's ring
+    __shared__ __attribute__((aligned(16))) int hist[256];
+    __shared__ uint32_t sh_xch[10];
+    __shared__ WideScan sh_wide;
+    __shared__ int sh_best_start;
+    __shared__ float w_mean_db[10], w_best1k_db[10], w_dsum[10];
+    __shared__ int w_lo[10], w_hi[10], order[10];
+    __shared__ float sh_f[4];
+    __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
+
+    const int lane = threadIdx.x;
+    const size_t frame = blockIdx.x;
+    const int n_ref = g.n_ref;
+    // the window bounds are indexed by thread below: copy them out of the kernel arguments with constant
+    // indices (a thread-indexed kernarg array would be copied to scratch)
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        if (lane == i) {
+            sh_geo_lo[i] = g.win_lo[i];
+            sh_geo_hi[i] = g.win_hi[i];
+        }
+    }
+    if (lane == 0) {
+        sh_geo_lo[n_ref] = g.focus_lo;
+        sh_geo_hi[n_ref] = g.focus_hi;
+    }
+    __syncthreads();
+    const float *P = spectra + frame * (size_t)g.n;
+    float *pool = gpool + frame * (size_t)gpool_stride;
+    StatsState st = state[frame];
+    if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
+    sdrg_frame_record rec;
+    __builtin_memset(&rec, 0, sizeof(rec));  // tail padding included: records compare and gather as bytes
+    rec.peak_bin = -1;
+    rec.abs_peak_db = -130.0f;
+
+    if (g.focus_len > 0) {
+        const int w1k = g.win_bins_1k;
+        const int n_bottom = n_bottom_of(n_ref);
+        const bool spec_pool = n_ref >= 2 && n_bottom == 1;  // pooled-bin sum = one window's dB sum
+        STATS_STAMP(0);
+        if (spec_pool)
+            scan_wide<true>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, sh_wide);
+        else
+            scan_wide<false>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, sh_wide);
+        STATS_STAMP(1);
+        const float abs_peak_db = sh_wide.peak_db;  // 6.2 focus peak (fft_process.cpp:142-154)
+        const int peak_bin = sh_wide.peak_idx;
+        if (lane < n_ref) w_dsum[lane] = sh_wide.dsum[lane];
+        // ---- 6.2 focus sum + 6.3 reference windows ----
+        if (lane <= n_ref) {
+            const int lo = sh_geo_lo[lane], hi = sh_geo_hi[lane], n = hi - lo + 1;
+            WinScan ws;
+            ws.sum = sh_wide.sum[lane];
+            ws.best_start = lo;
+            if (n <= 0) {
+                ws.best1k = 0.0f;
+            } else if (n < w1k) {
+                ws.best1k = ws.sum / n;
+            } else {
+                ws.best1k = sh_wide.bv[lane] / w1k;  // as scan_window: RN(max rs / w)
+                ws.best_start = lo + sh_wide.best_e[lane] - w1k + 1;
+            }
+            if (lane == n_ref) {
                 sh_f[0] = db_of(ws.sum / n);  // signalPowerDb (:155)
                 sh_f[1] = ws.best1k;          // focusBest1kLinear (:302)
                 sh_best_start = ws.best_start;
@@ -599,7 +1006,6 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
             }
         }
         __syncthreads();
-        if (!WIDE) STATS_STAMP(1);
         const float signal_power_db = sh_f[0];
         const int valid = (n_ref >= 2);
         rec.peak_bin = peak_bin;
@@ -613,9 +1019,8 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
             st.peak_above_noise_mean_db = st.max_bin_snr_db = st.max_bin_snr_sigma = 0.0f;
             st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
         } else {
-            int n_bottom = 1;
             // std::sort of <= 16 elements in libstdc++ is a (stable) insertion sort: the same order is a sort by
-            // (meanDb, window index); lane i places window i at its rank
+            // (meanDb, window index); thread i places window i at its rank
             if (lane < n_ref) {
                 const float ki = w_mean_db[lane];
                 int rank = 0;
@@ -626,153 +1031,18 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                 order[rank] = lane;
             }
             __syncthreads();
-            if (lane == 0) {
-                float key[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) key[i] = (i < n_ref) ? w_mean_db[order[i]] : INFINITY;
-                const int nb0 = (int)(n_ref * 0.4f);
-                n_bottom = nb0 > 1 ? nb0 : 1;  // <= 4 (n_ref <= 10)
-                // 6.4a (:235-247)
-                float mean = 0.0f;
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (i < n_bottom) mean += key[i];
-                mean /= n_bottom;
-                float gp[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) gp[i] = (i < n_bottom) ? fabsf(key[i] - mean) : INFINITY;
-                const float sigma = fmax_ref(1.4816f * kth_of4(gp, n_bottom / 2), 0.5f);
-                const float snr_db = signal_power_db - mean;
-                st.mean_snr_db = snr_db;
-                st.mean_snr_sigma = snr_db / sigma;
-                sh_nbottom = n_bottom;
-            }
-            __syncthreads();
-            n_bottom = sh_nbottom;
-
+            if (lane == 0) mean_snr_6_4a(w_mean_db, order, n_ref, signal_power_db, st);
             STATS_STAMP(2);
             // ---- 6.4b pooled per-bin dB of the bottom windows, sorted-window order (:252-269) ----
             int cnt = 0;
             float med = 0.0f, per_bin_mean = 0.0f;
-            if constexpr (!WIDE) {
-                // the pool is the bottom windows' staged dB values, window after window in sorted order
-                const float *dbs = stage + stage_pad;
-                for (int j = 0; j < n_bottom; j++) cnt += w_hi[order[j]] - w_lo[order[j]] + 1;
-                // the pool in registers, R values per lane: 8 (c2's 4 x 82 bins) or 24 (c5's 4 x 327)
-                auto reg_pool = [&](auto r_const) {
-                    constexpr int R = decltype(r_const)::value;
-                    // the pool in registers, value q = lane + 64 r: the whole wave gathers it, the sequential sum
-                    // (:259-263) walks it in pool order through v_readlane (no LDS latency in the chain), and the
-                    // select's passes read no memory
-                    int cum[5], base[4];
-                    cum[0] = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const bool in = j < n_bottom;
-                        const int wj = in ? order[j] : 0;
-                        cum[j + 1] = cum[j] + (in ? w_hi[wj] - w_lo[wj] + 1 : 0);
-                        base[j] = (in ? sh_woff[wj] : 0) - cum[j];  // dbs index of pool value q in window j
-                    }
-                    float v[R];
-                    // the pool in order, aligned for lane 0's float4 reads, over the staged bins (dead after the
-                    // scans, whose reads completed before the barrier after the window sort)
-                    float *pl = stage;
-#pragma unroll
-                    for (int r = 0; r < R; r++) {
-                        const int q = lane + WAVE * r;
-                        int bq = base[0];
-#pragma unroll
-                        for (int j = 1; j < 4; j++) bq = (q >= cum[j]) ? base[j] : bq;
-                        v[r] = (q < cnt) ? dbs[q + bq] : 0.0f;
-                    }
-                    __syncthreads();  // the pool may overlap the first dB values: every gather first
-#pragma unroll
-                    for (int r = 0; r < R; r++) {
-                        const int q = lane + WAVE * r;
-                        if (q < ((cnt + 15) & ~15)) pl[q] = v[r];  // zero tail up to a 16-value block
-                    }
-                    __syncthreads();
-                    if (lane == 0) {
-                        // 16 values per block read as four float4, the next block's reads issued before this
-                        // block's adds; the zero tail is not added
-                        float m = 0.0f;
-                        float4 A[4], B[4];
-                        auto rd = [&](float4 (&X)[4], int u) {
-#pragma unroll
-                            for (int i = 0; i < 4; i++) X[i] = *reinterpret_cast<const float4 *>(pl + u + 4 * i);
-                        };
-                        auto add16 = [&](const float4 (&X)[4], int n) {
-                            const float x[16] = {X[0].x, X[0].y, X[0].z, X[0].w, X[1].x, X[1].y, X[1].z, X[1].w,
-                                                 X[2].x, X[2].y, X[2].z, X[2].w, X[3].x, X[3].y, X[3].z, X[3].w};
-                            if (n >= 16) {
-#pragma unroll
-                                for (int i = 0; i < 16; i++) m += x[i];
-                            } else {
-#pragma unroll
-                                for (int i = 0; i < 16; i++)
-                                    if (i < n) m += x[i];
-                            }
-                        };
-                        rd(A, 0);
-                        for (int q = 0; q < cnt; q += 32) {
-                            if (q + 16 < cnt) rd(B, q + 16);
-                            add16(A, cnt - q);
-                            if (q + 16 >= cnt) break;
-                            if (q + 32 < cnt) rd(A, q + 32);
-                            add16(B, cnt - q - 16);
-                        }
-                        sh_f[2] = m / (float)cnt;
-                    }
-                    __syncthreads();
-                    per_bin_mean = sh_f[2];
-                    STATS_STAMP(3);
-#pragma unroll
-                    for (int r = 0; r < R; r++) v[r] = fabsf(v[r] - per_bin_mean);
-                    med = kth_smallest<WG>(
-                        [&](auto f) {
-#pragma unroll
-                            for (int r = 0; r < R; r++)
-                                if (lane + WAVE * r < cnt) f(__float_as_uint(v[r]));
-                        },
-                        cnt / 2, hist, sh_xch);
-                };
-                if (cnt <= 8 * WAVE) {
-                    reg_pool(std::integral_constant<int, 8>{});
-                } else if (cnt <= NARROW_REG_POOL * WAVE) {
-                    reg_pool(std::integral_constant<int, NARROW_REG_POOL>{});
-                } else {
-                    if (lane == 0) {
-                        float m = 0.0f;
-                        for (int j = 0; j < n_bottom; j++) {
-                            const int wj = order[j], len = w_hi[wj] - w_lo[wj] + 1;
-                            const float *d = dbs + sh_woff[wj];
-#pragma unroll 8
-                            for (int i = 0; i < len; i++) m += d[i];
-                        }
-                        sh_f[2] = m / (float)cnt;
-                    }
-                    __syncthreads();
-                    per_bin_mean = sh_f[2];
-                    STATS_STAMP(3);
-                    med = kth_smallest<WG>(
-                        [&](auto f) {
-                            for (int j = 0; j < n_bottom; j++) {
-                                const int wj = order[j], len = w_hi[wj] - w_lo[wj] + 1;
-                                const float *d = dbs + sh_woff[wj];
-                                for (int i = lane; i < len; i += WG) f(__float_as_uint(fabsf(d[i] - per_bin_mean)));
-                            }
-                        },
-                        cnt / 2, hist, sh_xch);
-                }
-            } else if (spec_pool) {
+            if (spec_pool) {
                 // one bottom window: its dB sum came out of the wide scan (same values, same order, from 0); the
                 // pool holds the |dB - mean| gaps directly
                 const int wb = order[0];
                 const int lo = w_lo[wb], hi = w_hi[wb];
                 cnt = hi - lo + 1;
-                if (lane == 0) sh_f[2] = w_dsum[wb] / (float)cnt;
-                __syncthreads();
-                per_bin_mean = sh_f[2];
+                per_bin_mean = w_dsum[wb] / (float)cnt;
                 const float m = per_bin_mean;
                 if (cnt <= REG_POOL * WG) {
                     // gaps in registers: the select's passes read no memory
@@ -803,7 +1073,7 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
                     med = kth_smallest_of<WG>(pool, cnt, cnt / 2, hist, sh_xch);
                 }
             } else {
-                // several bottom windows (wide): pooled in HBM scratch, summed in order by one thread
+                // several bottom windows: pooled in HBM scratch, summed in order by one thread
                 for (int j = 0; j < n_bottom; j++) {
                     const int wj = order[j], len = w_hi[wj] - w_lo[wj] + 1;
                     const float *src = P + w_lo[wj];
@@ -833,99 +1103,14 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(4))) void st
             const float sigma_bin = (cnt > 0) ? fmax_ref(1.4816f * med, 1.0f) : 1.0f;
             if (cnt > 0) st.per_bin_mean = per_bin_mean;
             const float pbm = (cnt > 0) ? per_bin_mean : 0.0f;
-
-            if (lane == 0) {
-                st.peak_above_noise_mean_db = abs_peak_db - pbm;  // :274
-                // 6.4c (:281-288)
-                const float logN = logf((float)g.focus_len);
-                const float sqrt2logN = sqrtf(2.0f * logN);
-                const float gumbel_loc = pbm + sigma_bin * sqrt2logN;
-                const float gumbel_sig = fmax_ref(sigma_bin * 3.14159f / (sqrtf(6.0f) * sqrt2logN), 0.5f);
-                st.max_bin_snr_db = abs_peak_db - gumbel_loc;
-                st.max_bin_snr_sigma = st.max_bin_snr_db / gumbel_sig;
-                // 6.4d (:292-327)
-                float mean1k = 0.0f;
-                for (int i = 0; i < n_bottom; i++) mean1k += w_best1k_db[order[i]];
-                mean1k /= n_bottom;
-                float g1k[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++) g1k[i] = (i < n_bottom) ? fabsf(w_best1k_db[order[i]] - mean1k) : INFINITY;
-                const float sigma_floor_1k = sigma_bin / sqrtf((float)w1k);
-                float sigma1k = 1.4816f * kth_of4(g1k, n_bottom / 2);
-                if (sigma1k < sigma_floor_1k) sigma1k = sigma_floor_1k;
-                if (sigma1k < 0.5f) sigma1k = 0.5f;
-                const float focus_best1k_linear = sh_f[1];
-                if (focus_best1k_linear > 0.0f) {
-                    const float focus_best1k_db = db_of(focus_best1k_linear);
-                    st.best1khz_snr_db = focus_best1k_db - mean1k;
-                    st.best1khz_snr_sigma = st.best1khz_snr_db / sigma1k;
-                    const int best_start = sh_best_start;
-                    st.best1khz_center_freq_hz = (best_start + w1k / 2) * g.freq_per_bin + g.cf_minus_nyq;
-                } else {
-                    st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
-                }
-            }
+            if (lane == 0)
+                snr_6_4cd(g, st, abs_peak_db, pbm, sigma_bin, n_bottom, w_best1k_db, order, sh_f[1], sh_best_start);
         }
-
         STATS_STAMP(5);
-        if (lane == 0) {
-            // ---- 6.5 frequency tracking (:333-361), clock injected ----
-            if (st.tracking_frequency == 0.0f) st.tracking_frequency = g.cf_float;
-            if (st.center_frequency_changed) {
-                st.tracking_frequency = g.cf_float;
-                st.center_frequency_changed = 0;
-            }
-            if (!st.max_peak_set) {
-                st.max_peak_db = -130.0f;
-                st.max_peak_freq = g.cf_float;
-                st.max_peak_set = 1;
-            }
-            if (valid && abs_peak_db > st.max_peak_db) {
-                st.max_peak_db = abs_peak_db;
-                st.max_peak_freq = peak_bin * g.freq_per_bin + g.cf_u32_minus_nyq;
-                st.time_last_max_peak_ms = now_ms;
-            }
-            const int64_t ms_since = now_ms - st.time_last_max_peak_ms;
-            if (st.time_last_update_ms < st.time_last_max_peak_ms && ms_since > 300) {
-                st.tracking_frequency = st.max_peak_freq;
-                st.time_last_update_ms = now_ms;
-                st.max_peak_db = -130.0f;
-            }
-            // ---- 6.6 detection (:365-378) ----
-            const bool above = valid && (st.mean_snr_sigma >= 4.0f);
-            if (above) {
-                if (st.peak_confirmed < 1) st.peak_confirmed++;
-            } else {
-                st.peak_confirmed = 0;
-            }
-            const int flag = (above && st.peak_confirmed >= 1) ? 3 : 0;
-            // det_buf[det_idx] = flag with constant indices (no private-memory indexing)
-            const int d0 = (st.det_idx == 0) ? flag : st.det_buf[0];
-            const int d1 = (st.det_idx == 1) ? flag : st.det_buf[1];
-            const int d2 = (st.det_idx == 2) ? flag : st.det_buf[2];
-            st.det_buf[0] = d0;
-            st.det_buf[1] = d1;
-            st.det_buf[2] = d2;
-            st.det_idx = (st.det_idx + 1) % 3;
-            int m = d0;
-            if (d1 > m) m = d1;
-            if (d2 > m) m = d2;
-            st.detection_flag_sent = m;
-        }
+        if (lane == 0) track_detect_6_5_6_6(g, st, valid, abs_peak_db, peak_bin, now_ms);
     }
-
     if (lane == 0) {
-        rec.tracking_frequency = (int64_t)roundf(st.tracking_frequency);
-        rec.mean_snr_db = st.mean_snr_db;
-        rec.mean_snr_sigma = st.mean_snr_sigma;
-        rec.peak_above_noise_mean_db = st.peak_above_noise_mean_db;
-        rec.max_bin_snr_db = st.max_bin_snr_db;
-        rec.max_bin_snr_sigma = st.max_bin_snr_sigma;
-        rec.best1khz_snr_db = st.best1khz_snr_db;
-        rec.best1khz_snr_sigma = st.best1khz_snr_sigma;
-        rec.best1khz_center_freq_hz = st.best1khz_center_freq_hz;
-        rec.per_bin_mean = st.per_bin_mean;
-        rec.detection_flag = st.detection_flag_sent;
+        finish_record(rec, st);
         if (records) records[frame] = rec;
         state[frame] = st;
     }
@@ -959,19 +1144,37 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
         size_t lds = sizeof(float) * (size_t)RING_FLOATS;
         if (SDRG_STATS_STAMPS && getenv("SDRG_STATS_LDS_KB")) {  // diagnostic: fewer frames per CU
             lds = (size_t)atoi(getenv("SDRG_STATS_LDS_KB")) * 1024;
-            hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel<WIDE_WG>), (int)lds);
+            hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_wide_kernel), (int)lds);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(stats_kernel<WIDE_WG>, dim3(n_frames), dim3(WIDE_WG), lds, stream, spectra, geo, now_ms,
-                           state, records, gpool, pool_stride);
+        hipLaunchKernelGGL(stats_wide_kernel, dim3(n_frames), dim3(WIDE_WG), lds, stream, spectra, geo, now_ms, state,
+                           records, gpool, pool_stride);
     } else {
-        // the staged windows' bins (later the pool in order, + a 16-value zero tail), then their dB values
-        const int staged = (stage_bins(geo) + 3) & ~3;
-        const size_t lds = sizeof(float) * (size_t)(2 * staged + 16);
-        hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_kernel<WAVE>), (2 * STAGE_MAX + 16) * 4);
+        // per frame: the staged windows' bins (later the pool in order, + a 16-value zero tail), their dB values.  One frame per wave: 2 or 4 (SDRG_STATS_FPW, lab) measured slower -- a wave's phases are
+        // latency-bound, and fewer waves hide less of it
+        const int gf = 2 * ((stage_bins(geo) + 3) & ~3) + 16;
+        const size_t per = sizeof(float) * (size_t)gf;
+        static const int fpw_lab = [] {
+            const char *v = getenv("SDRG_STATS_FPW");
+            const int f = v ? atoi(v) : 1;
+            return (f == 2 || f == 4) ? f : 1;
+        }();
+        const int fpw = (fpw_lab * per <= 48 * 1024) ? fpw_lab : 1;
+        const int grid = (n_frames + fpw - 1) / fpw;
+        const void *k = fpw == 4 ? reinterpret_cast<const void *>(stats_narrow_kernel<4>)
+                      : fpw == 2 ? reinterpret_cast<const void *>(stats_narrow_kernel<2>)
+                                 : reinterpret_cast<const void *>(stats_narrow_kernel<1>);
+        hipError_t e = ensure_dynamic_lds(k, (2 * STAGE_MAX + 16) * 4);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(stats_kernel<WAVE>, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms, state,
-                           records, nullptr, 0);
+        if (fpw == 4)
+            hipLaunchKernelGGL(stats_narrow_kernel<4>, dim3(grid), dim3(WAVE), 4 * per, stream, spectra, geo, now_ms,
+                               state, records, n_frames, gf);
+        else if (fpw == 2)
+            hipLaunchKernelGGL(stats_narrow_kernel<2>, dim3(grid), dim3(WAVE), 2 * per, stream, spectra, geo, now_ms,
+                               state, records, n_frames, gf);
+        else
+            hipLaunchKernelGGL(stats_narrow_kernel<1>, dim3(grid), dim3(WAVE), per, stream, spectra, geo, now_ms, state,
+                               records, n_frames, gf);
     }
     if (SDRG_STATS_STAMPS) {  // diagnostic build: mean cycles per phase over the frames of this call
         std::vector<unsigned long long> h((size_t)STAMP_PHASES * 8192);
@@ -986,8 +1189,8 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
                 d[6] += (double)t[7];
                 d[7] += (double)t[8];
             }
-            fprintf(stderr, "[stats stamps] cycles/frame: scans %.0f (wide busy: chain wave / record wave / producers, narrow: "
-                            "focus peak / stage copy: %.0f %.0f %.0f) | "
+            fprintf(stderr, "[stats stamps] cycles/frame: scans %.0f (wide busy: chain wave / record wave / producers; narrow: "
+                            "staging copy first: %.0f %.0f %.0f) | "
                             "sort+6.4a %.0f | pool %.0f | select %.0f | tail %.0f\n", d[0] / nf, d[5] / nf, d[6] / nf,
                     d[7] / nf, d[1] / nf, d[2] / nf, d[3] / nf, d[4] / nf);
         }
