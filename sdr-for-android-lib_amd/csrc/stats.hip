@@ -555,122 +555,89 @@ extern "C" __device__ uint32_t __ockl_wfred_and_u32(uint32_t);
 extern "C" __device__ uint32_t __ockl_wfred_or_u32(uint32_t);
 extern "C" __device__ int __ockl_wfscan_add_i32(int, bool);
 
-// k-th smallest for FPW frames per wave: lane group fg (G = 64 / FPW lanes) selects in its own values (visit
-// calls f(bits) for the values this lane holds; groups with active == false take no part).  The same radix
-// select as kth_smallest, with a 256-bin histogram per group and a group-wide scan (256 / G bins per lane).
-template <int G, class Visit>
-__device__ float kth_smallest_group(Visit visit, int k, bool active, int (*hist)[256], uint32_t (*xch)[2]) {
-    constexpr int FPW = WAVE / G, B = 256 / G;
-    const int lane = threadIdx.x, fg = lane / G, gl = lane % G;
-    int *h = hist[fg];
+// k-th smallest (0-based) of the non-negative floats one wave holds (visit(f) calls f(bits) for each value
+// this lane holds): the radix select of kth_smallest with the device library's DPP wave operations for the
+// AND/OR reduction and the bucket scan (no LDS round trips), 4 histogram bins per lane.
+template <class Visit>
+__device__ float kth_smallest_wave(Visit visit, int k, int *hist, uint32_t *xch) {
+    const int lane = threadIdx.x;
     uint32_t band = 0xffffffffu, bor = 0u;
-    if (active)
-        visit([&](uint32_t b) {
-            band &= b;
-            bor |= b;
-        });
-    if constexpr (G == WAVE) {  // DPP wave reductions (no LDS round trips)
-        band = __ockl_wfred_and_u32(band);
-        bor = __ockl_wfred_or_u32(bor);
-    } else {
-        for (int off = G / 2; off > 0; off >>= 1) {  // xor partners stay inside the aligned group
-            band &= (uint32_t)__shfl_xor((int)band, off);
-            bor |= (uint32_t)__shfl_xor((int)bor, off);
-        }
-    }
+    visit([&](uint32_t b) {
+        band &= b;
+        bor |= b;
+    });
+    band = __ockl_wfred_and_u32(band);
+    bor = __ockl_wfred_or_u32(bor);
     const uint32_t diff = band ^ bor;
-    int top = (active && diff != 0) ? 31 - __clz(diff) : -1;  // highest bit where the values differ
-    uint32_t mask = (top < 0 || top >= 31) ? 0u : ~((2u << top) - 1u);
-    uint32_t prefix = top < 0 ? band : band & mask;  // top < 0: every value equal (or no frame)
-    while (__ballot(top >= 0)) {
-        const bool on = top >= 0;
+    if (diff == 0) return __uint_as_float(band);  // every value equal
+    int top = 31 - __clz(diff);                   // highest bit where the values differ
+    uint32_t mask = top >= 31 ? 0u : ~((2u << top) - 1u);
+    uint32_t prefix = band & mask;
+    while (top >= 0) {
         const int lo = top >= 7 ? top - 7 : 0;
-        const uint32_t dm = on ? (1u << (top - lo + 1)) - 1u : 0u;
-#pragma unroll
-        for (int i = 0; i < B; i += 4) *reinterpret_cast<int4 *>(&h[gl * B + i]) = make_int4(0, 0, 0, 0);
+        const uint32_t dm = (1u << (top - lo + 1)) - 1u;
+        *reinterpret_cast<int4 *>(&hist[4 * lane]) = make_int4(0, 0, 0, 0);
         __syncthreads();
-        if (on)
-            visit([&](uint32_t b) {
-                if ((b & mask) == prefix) atomicAdd(&h[(b >> lo) & dm], 1);
-            });
+        visit([&](uint32_t b) {
+            if ((b & mask) == prefix) atomicAdd(&hist[(b >> lo) & dm], 1);
+        });
         __syncthreads();
-        int hv[B];
+        const int4 h = *reinterpret_cast<const int4 *>(&hist[4 * lane]);
+        const int own = h.x + h.y + h.z + h.w;
+        const int incl = __ockl_wfscan_add_i32(own, true);  // DPP inclusive scan
+        const unsigned long long over = __ballot(incl > k);  // non-empty: k < number of candidates
+        const int L = __ffsll((long long)over) - 1;
+        if (lane == L) {
+            int acc = incl - own;
+            const int hv[4] = {h.x, h.y, h.z, h.w};
+            int j = 3;  // the lane's last bin unless an earlier one already passes k
 #pragma unroll
-        for (int i = 0; i < B; i += 4) {
-            const int4 q = *reinterpret_cast<const int4 *>(&h[gl * B + i]);
-            hv[i] = q.x;
-            hv[i + 1] = q.y;
-            hv[i + 2] = q.z;
-            hv[i + 3] = q.w;
-        }
-        int own = 0;
+            for (int t = 2; t >= 0; t--) {
+                int before = acc;
 #pragma unroll
-        for (int i = 0; i < B; i++) own += hv[i];
-        int incl = own;
-        if constexpr (G == WAVE) {
-            incl = __ockl_wfscan_add_i32(own, true);  // DPP inclusive scan
-        } else {
-#pragma unroll
-            for (int off = 1; off < G; off <<= 1) {
-                const int v = __shfl_up(incl, off);
-                if (gl >= off) incl += v;
+                for (int u = 0; u < t; u++) before += hv[u];
+                if (before + hv[t] > k) j = t;
             }
-        }
-        const unsigned long long over = __ballot(on && incl > k);  // per group non-empty: k < candidates
-        const int L = __ffsll((long long)((over >> (fg * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1)))) - 1;
-        if (on && gl == L) {
-            int acc = incl - own, j = B - 1;
-            bool found = false;
 #pragma unroll
-            for (int t = 0; t < B; t++) {  // the first of the lane's bins that passes k
-                const bool here = !found && acc + hv[t] > k;
-                j = here ? t : j;
-                found = found || here;
-                acc += found ? 0 : hv[t];
-            }
-            xch[fg][0] = (uint32_t)(L * B + j);
-            xch[fg][1] = (uint32_t)acc;
+            for (int u = 0; u < 3; u++)
+                if (u < j) acc += hv[u];
+            xch[0] = (uint32_t)(4 * L + j);
+            xch[1] = (uint32_t)acc;
         }
         __syncthreads();
-        if (on) {
-            const uint32_t d = xch[fg][0];
-            k -= (int)xch[fg][1];
-            prefix |= d << lo;
-            mask |= dm << lo;
-            top = lo - 1;
-        }
+        k -= (int)xch[1];
+        prefix |= xch[0] << lo;
+        mask |= dm << lo;
+        top = lo - 1;
         __syncthreads();
     }
-    (void)FPW;
     return __uint_as_float(prefix);
 }
 
-// Narrow statistics, FPW frames per wave (lane group fg = lane / G of G = 64 / FPW lanes holds frame
-// blockIdx.x * FPW + fg).  Every window's bins are staged compactly into the group's LDS region (window q at
-// sh_woff[q]) with their dB values, all of a lane's loads in flight at once; the focus peak is evaluated during
-// that copy.  The order-free work (copy, dB, pooled gaps, select) runs across the group's lanes; the
-// reference's sequential sums run one lane per window (the window scans) or per frame (the pooled mean, the
-// scalar tail) -- and those, the chains that leave most of a wave's lanes idle, serve FPW frames per
-// instruction.  gf: floats of LDS per group.
-template <int FPW>
+// Narrow statistics, one wave per frame.  Every window's bins are staged compactly into LDS (window q at
+// sh_woff[q]), all of a lane's loads in flight at once; the focus peak's dB values are evaluated during that
+// copy (the other bins need no dB until the pool).  The reference's sequential sums run one lane per window
+// (the window scans) or per frame (the pooled mean, the scalar tail); the order-free work (copy, dB, pooled
+// gaps, select) runs across the lanes.  LDS per frame: the staged bins, over which the pool is laid out in
+// order once the scans are done (R > 0: pool values <= R per lane, held in registers for the select), or, for
+// pools beyond 24 x 64 values (R == 0), a pool region after them.  Small on purpose: beside the SSB pipeline
+// (84.5 KiB of LDS per CU) the frames that fit at once set the kernel's time.
+template <int R>
 __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restrict__ spectra, StatsGeometry g,
                                                             int64_t now_ms, StatsState *__restrict__ state,
-                                                            sdrg_frame_record *__restrict__ records, int n_frames,
-                                                            int gf) {
-    constexpr int G = WAVE / FPW;
-    extern __shared__ __attribute__((aligned(16))) float dyn[];
+                                                            sdrg_frame_record *__restrict__ records) {
+    extern __shared__ __attribute__((aligned(16))) float stage[];
     __shared__ int sh_woff[12];
     __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
-    __shared__ __attribute__((aligned(16))) int hist[FPW][256];
-    __shared__ uint32_t sh_xch[FPW][2];
-    __shared__ float w_mean_db[FPW][10], w_best1k_db[FPW][10];
-    __shared__ int order[FPW][10];
-    __shared__ float sh_f[FPW][4];
-    __shared__ int sh_best_start[FPW];
+    __shared__ __attribute__((aligned(16))) int hist[256];
+    __shared__ uint32_t sh_xch[2];
+    __shared__ float w_mean_db[10], w_best1k_db[10];
+    __shared__ int order[10];
+    __shared__ float sh_f[4];
+    __shared__ int sh_best_start;
 
-    const int lane = threadIdx.x, fg = lane / G, gl = lane % G;
-    const int frame = blockIdx.x * FPW + fg;
-    const bool active = frame < n_frames;
+    const int lane = threadIdx.x;
+    const size_t frame = blockIdx.x;
     const int n_ref = g.n_ref;
 #pragma unroll
     for (int i = 0; i < 10; i++) {  // constant kernarg indices (a lane-indexed kernarg array would go to scratch)
@@ -691,11 +658,8 @@ __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restr
     }
     __syncthreads();
     const int stage_total = sh_woff[n_ref + 1], stage_pad = (stage_total + 3) & ~3;
-    float *stage = dyn + fg * gf;
-    float *dbs = stage + stage_pad;
-    const float *P = spectra + (size_t)(active ? frame : 0) * g.n;
-    StatsState st{};
-    if (active) st = state[frame];
+    const float *P = spectra + frame * (size_t)g.n;
+    StatsState st = state[frame];
     if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
     sdrg_frame_record rec;
     __builtin_memset(&rec, 0, sizeof(rec));  // tail padding included: records compare and gather as bytes
@@ -716,34 +680,32 @@ __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restr
 #pragma unroll
             for (int k = 0; k < 10; k++) wo[k] = (k < n_ref) ? sh_woff[k + 1] : 0x7fffffff;
             const int foff = sh_woff[n_ref];
-            const int lim = active ? stage_total : 0;
-            for (int base = gl; base < lim; base += 16 * G) {
+            for (int base = lane; base < stage_total; base += 16 * WAVE) {
                 float v[16];
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
-                    const int i = base + G * u;
+                    const int i = base + WAVE * u;
                     int d = dl[0];
 #pragma unroll
                     for (int k = 0; k < 10; k++) d = (i >= wo[k]) ? dl[k + 1] : d;
-                    v[u] = (i < lim) ? P[i + d] : 0.0f;
+                    v[u] = (i < stage_total) ? P[i + d] : 0.0f;
                 }
 #pragma unroll
                 for (int u = 0; u < 16; u++) {
-                    const int i = base + G * u;
-                    if (i < lim) {
+                    const int i = base + WAVE * u;
+                    if (i < stage_total) stage[i] = v[u];
+                    // the focus window is the last: a lane sees its bins in increasing order, strict > keeps
+                    // each lane's first maximum
+                    if (i >= foff && i < stage_total) {
                         const float d = db_of(v[u]);
-                        stage[i] = v[u];
-                        dbs[i] = d;
-                        // the focus window is the last: a lane sees its bins in increasing order, strict >
-                        // keeps each lane's first maximum
-                        if (i >= foff && d > best) {
+                        if (d > best) {
                             best = d;
                             bidx = g.focus_lo + (i - foff);
                         }
                     }
                 }
             }
-            for (int off = G / 2; off > 0; off >>= 1) {  // first maximum over the group (lower bin on ties)
+            for (int off = WAVE / 2; off > 0; off >>= 1) {  // first maximum over the lanes (lower bin on ties)
                 const float ob = __shfl_xor(best, off);
                 const int oi = __shfl_xor(bidx, off);
                 if (ob > best || (ob == best && oi < bidx)) {
@@ -758,22 +720,22 @@ __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restr
         const float abs_peak_db = best;
         const int peak_bin = (bidx == 0x7fffffff) ? g.focus_lo : bidx;
 
-        // ---- 6.2 focus sum + 6.3 reference windows: lane gl scans window gl (the focus is window n_ref) ----
-        if (active && gl <= n_ref) {
-            const int lo = sh_geo_lo[gl], hi = sh_geo_hi[gl], n = hi - lo + 1;
-            const WinScan ws = scan_window(stage + sh_woff[gl], lo, hi, w1k);
-            if (gl == n_ref) {
-                sh_f[fg][0] = db_of(ws.sum / n);  // signalPowerDb (:155)
-                sh_f[fg][1] = ws.best1k;          // focusBest1kLinear (:302)
-                sh_best_start[fg] = ws.best_start;
+        // ---- 6.2 focus sum + 6.3 reference windows: lane q scans window q (the focus is window n_ref) ----
+        if (lane <= n_ref) {
+            const int lo = sh_geo_lo[lane], hi = sh_geo_hi[lane], n = hi - lo + 1;
+            const WinScan ws = scan_window(stage + sh_woff[lane], lo, hi, w1k);
+            if (lane == n_ref) {
+                sh_f[0] = db_of(ws.sum / n);  // signalPowerDb (:155)
+                sh_f[1] = ws.best1k;          // focusBest1kLinear (:302)
+                sh_best_start = ws.best_start;
             } else {
-                w_mean_db[fg][gl] = db_of(ws.sum / n);
-                w_best1k_db[fg][gl] = db_of(ws.best1k);
+                w_mean_db[lane] = db_of(ws.sum / n);
+                w_best1k_db[lane] = db_of(ws.best1k);
             }
         }
         __syncthreads();
         STATS_STAMP(1);
-        const float signal_power_db = sh_f[fg][0];
+        const float signal_power_db = sh_f[0];
         const int valid = (n_ref >= 2);
         rec.peak_bin = peak_bin;
         rec.abs_peak_db = abs_peak_db;
@@ -787,137 +749,122 @@ __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restr
             st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
         } else {
             // std::sort of <= 16 elements in libstdc++ is a (stable) insertion sort: the same order is a sort by
-            // (meanDb, window index); lane gl places window gl at its rank
-            if (active && gl < n_ref) {
-                const float ki = w_mean_db[fg][gl];
+            // (meanDb, window index); lane i places window i at its rank
+            if (lane < n_ref) {
+                const float ki = w_mean_db[lane];
                 int rank = 0;
                 for (int k = 0; k < n_ref; k++) {
-                    const float kk = w_mean_db[fg][k];
-                    rank += (kk < ki || (kk == ki && k < gl)) ? 1 : 0;
+                    const float kk = w_mean_db[k];
+                    rank += (kk < ki || (kk == ki && k < lane)) ? 1 : 0;
                 }
-                order[fg][rank] = gl;
+                order[rank] = lane;
             }
             __syncthreads();
             const int n_bottom = n_bottom_of(n_ref);
-            if (active && gl == 0) mean_snr_6_4a(w_mean_db[fg], order[fg], n_ref, signal_power_db, st);
+            if (lane == 0) mean_snr_6_4a(w_mean_db, order, n_ref, signal_power_db, st);
             STATS_STAMP(2);
 
             // ---- 6.4b pooled per-bin dB of the bottom windows, sorted-window order (:252-269) ----
-            int cnt = 0, cum[5], basej[4];
+            // pool value q lies in bottom window j (cum[j] <= q < cum[j + 1]) at staged bin q + basej[j]
+            int cum[5], basej[4];
             cum[0] = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const bool in = j < n_bottom;
-                const int wj = in ? order[fg][j] : 0;
+                const int wj = in ? order[j] : 0;
                 cum[j + 1] = cum[j] + (in ? sh_geo_hi[wj] - sh_geo_lo[wj] + 1 : 0);
-                basej[j] = (in ? sh_woff[wj] : 0) - cum[j];  // dbs index of pool value q in window j
+                basej[j] = (in ? sh_woff[wj] : 0) - cum[j];
             }
-            cnt = cum[4];
-            float med = 0.0f, per_bin_mean = 0.0f;
-            // the pool in registers (value q = gl + G r) when it fits, else visited in place
-            auto pooled = [&](auto r_const) {
-                constexpr int R = decltype(r_const)::value;
-                float v[R];
+            const int cnt = cum[4];
+            // as a sum of steps (a select chain over basej[] becomes an indexed load from scratch)
+            const int d1 = basej[1] - basej[0], d2 = basej[2] - basej[1], d3 = basej[3] - basej[2];
+            auto staged_of = [&](int q) {
+                return q + basej[0] + (q >= cum[1] ? d1 : 0) + (q >= cum[2] ? d2 : 0) + (q >= cum[3] ? d3 : 0);
+            };
+            // the pool in order (zero tail up to a 16-value block), for lane 0's float4 reads: over the staged
+            // bins once every lane has read them (R > 0), or in its own region after them (R == 0)
+            float *pl = R > 0 ? stage : stage + stage_pad;
+            float v[R > 0 ? R : 1];
+            if constexpr (R > 0) {
 #pragma unroll
                 for (int r = 0; r < R; r++) {
-                    const int q = gl + G * r;
-                    int bq = basej[0];
-#pragma unroll
-                    for (int j = 1; j < 4; j++) bq = (q >= cum[j]) ? basej[j] : bq;
-                    v[r] = (active && q < cnt) ? dbs[q + bq] : 0.0f;
-                }
-                // the pool in order, for lane 0's float4 reads, over the staged bins (dead since the scans); only a
-                // pool reaching the dB values waits for every lane's gather first
-                float *pl = stage;
-                if (((cnt + 15) & ~15) > stage_pad) __syncthreads();
-#pragma unroll
-                for (int r = 0; r < R; r++) {
-                    const int q = gl + G * r;
-                    if (active && q < ((cnt + 15) & ~15)) pl[q] = v[r];  // zero tail up to a 16-value block
+                    const int q = lane + WAVE * r;
+                    v[r] = 0.0f;
+                    if (q < cnt) v[r] = db_of(stage[staged_of(q)]);
                 }
                 __syncthreads();
-                if (active && gl == 0) {
-                    // the sequential sum (:259-263), 16 values per block read as four float4 one block ahead
-                    float m = 0.0f;
-                    float4 A[4], Bv[4];
-                    auto rd = [&](float4 (&X)[4], int u) {
 #pragma unroll
-                        for (int i = 0; i < 4; i++) X[i] = *reinterpret_cast<const float4 *>(pl + u + 4 * i);
-                    };
-                    auto add16 = [&](const float4 (&X)[4], int n) {
-                        const float x[16] = {X[0].x, X[0].y, X[0].z, X[0].w, X[1].x, X[1].y, X[1].z, X[1].w,
-                                             X[2].x, X[2].y, X[2].z, X[2].w, X[3].x, X[3].y, X[3].z, X[3].w};
-                        if (n >= 16) {
+                for (int r = 0; r < R; r++) {
+                    const int q = lane + WAVE * r;
+                    if (q < ((cnt + 15) & ~15)) pl[q] = v[r];
+                }
+            } else {
+                for (int q = lane; q < ((cnt + 15) & ~15); q += WAVE) pl[q] = q < cnt ? db_of(stage[staged_of(q)]) : 0.0f;
+            }
+            __syncthreads();
+            if (lane == 0) {
+                // the sequential sum (:259-263), 16 values per block read as four float4 one block ahead; the
+                // zero tail is not added
+                float m = 0.0f;
+                float4 A[4], B[4];
+                auto rd = [&](float4 (&X)[4], int u) {
 #pragma unroll
-                            for (int i = 0; i < 16; i++) m += x[i];
-                        } else {
+                    for (int i = 0; i < 4; i++) X[i] = *reinterpret_cast<const float4 *>(pl + u + 4 * i);
+                };
+                auto add16 = [&](const float4 (&X)[4], int n) {
+                    const float x[16] = {X[0].x, X[0].y, X[0].z, X[0].w, X[1].x, X[1].y, X[1].z, X[1].w,
+                                         X[2].x, X[2].y, X[2].z, X[2].w, X[3].x, X[3].y, X[3].z, X[3].w};
+                    if (n >= 16) {
 #pragma unroll
-                            for (int i = 0; i < 16; i++)
-                                if (i < n) m += x[i];
-                        }
-                    };
-                    rd(A, 0);
-                    for (int q = 0; q < cnt; q += 32) {
-                        if (q + 16 < cnt) rd(Bv, q + 16);
-                        add16(A, cnt - q);
-                        if (q + 16 >= cnt) break;
-                        if (q + 32 < cnt) rd(A, q + 32);
-                        add16(Bv, cnt - q - 16);
+                        for (int i = 0; i < 16; i++) m += x[i];
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 16; i++)
+                            if (i < n) m += x[i];
                     }
-                    sh_f[fg][2] = m / (float)cnt;
+                };
+                rd(A, 0);
+                for (int q = 0; q < cnt; q += 32) {
+                    if (q + 16 < cnt) rd(B, q + 16);
+                    add16(A, cnt - q);
+                    if (q + 16 >= cnt) break;
+                    if (q + 32 < cnt) rd(A, q + 32);
+                    add16(B, cnt - q - 16);
                 }
-                __syncthreads();
-                per_bin_mean = sh_f[fg][2];
-                STATS_STAMP(3);
+                sh_f[2] = m / (float)cnt;
+            }
+            __syncthreads();
+            const float per_bin_mean = sh_f[2];
+            STATS_STAMP(3);
+            float med;
+            if constexpr (R > 0) {
 #pragma unroll
                 for (int r = 0; r < R; r++) v[r] = fabsf(v[r] - per_bin_mean);
-                med = kth_smallest_group<G>(
+                med = kth_smallest_wave(
                     [&](auto f) {
 #pragma unroll
                         for (int r = 0; r < R; r++)
-                            if (gl + G * r < cnt) f(__float_as_uint(v[r]));
+                            if (lane + WAVE * r < cnt) f(__float_as_uint(v[r]));
                     },
-                    cnt / 2, active, hist, sh_xch);
-            };
-            if (cnt <= 8 * G) {
-                pooled(std::integral_constant<int, 8>{});
-            } else if (cnt <= NARROW_REG_POOL * G) {
-                pooled(std::integral_constant<int, NARROW_REG_POOL>{});
+                    cnt / 2, hist, sh_xch);
             } else {
-                if (active && gl == 0) {
-                    float m = 0.0f;
-                    for (int j = 0; j < n_bottom; j++) {
-                        const int wj = order[fg][j], len = sh_geo_hi[wj] - sh_geo_lo[wj] + 1;
-                        const float *d = dbs + sh_woff[wj];
-#pragma unroll 8
-                        for (int i = 0; i < len; i++) m += d[i];
-                    }
-                    sh_f[fg][2] = m / (float)cnt;
-                }
-                __syncthreads();
-                per_bin_mean = sh_f[fg][2];
-                med = kth_smallest_group<G>(
+                med = kth_smallest_wave(
                     [&](auto f) {
-                        for (int j = 0; j < n_bottom; j++) {
-                            const int wj = order[fg][j], len = sh_geo_hi[wj] - sh_geo_lo[wj] + 1;
-                            const float *d = dbs + sh_woff[wj];
-                            for (int i = gl; i < len; i += G) f(__float_as_uint(fabsf(d[i] - per_bin_mean)));
-                        }
+                        for (int q = lane; q < cnt; q += WAVE) f(__float_as_uint(fabsf(pl[q] - per_bin_mean)));
                     },
-                    cnt / 2, active, hist, sh_xch);
+                    cnt / 2, hist, sh_xch);
             }
             STATS_STAMP(4);
             const float sigma_bin = (cnt > 0) ? fmax_ref(1.4816f * med, 1.0f) : 1.0f;
             if (cnt > 0) st.per_bin_mean = per_bin_mean;
             const float pbm = (cnt > 0) ? per_bin_mean : 0.0f;
-            if (active && gl == 0)
-                snr_6_4cd(g, st, abs_peak_db, pbm, sigma_bin, n_bottom, w_best1k_db[fg], order[fg], sh_f[fg][1],
-                          sh_best_start[fg]);
+            if (lane == 0)
+                snr_6_4cd(g, st, abs_peak_db, pbm, sigma_bin, n_bottom, w_best1k_db, order, sh_f[1], sh_best_start);
         }
         STATS_STAMP(5);
-        if (active && gl == 0) track_detect_6_5_6_6(g, st, valid, abs_peak_db, peak_bin, now_ms);
+        if (lane == 0) track_detect_6_5_6_6(g, st, valid, abs_peak_db, peak_bin, now_ms);
     }
-    if (active && gl == 0) {
+    if (lane == 0) {
         finish_record(rec, st);
         if (records) records[frame] = rec;
         state[frame] = st;
@@ -1150,31 +1097,25 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
         hipLaunchKernelGGL(stats_wide_kernel, dim3(n_frames), dim3(WIDE_WG), lds, stream, spectra, geo, now_ms, state,
                            records, gpool, pool_stride);
     } else {
-        // per frame: the staged windows' bins (later the pool in order, + a 16-value zero tail), their dB values.  One frame per wave: 2 or 4 (SDRG_STATS_FPW, lab) measured slower -- a wave's phases are
-        // latency-bound, and fewer waves hide less of it
-        const int gf = 2 * ((stage_bins(geo) + 3) & ~3) + 16;
-        const size_t per = sizeof(float) * (size_t)gf;
-        static const int fpw_lab = [] {
-            const char *v = getenv("SDRG_STATS_FPW");
-            const int f = v ? atoi(v) : 1;
-            return (f == 2 || f == 4) ? f : 1;
-        }();
-        const int fpw = (fpw_lab * per <= 48 * 1024) ? fpw_lab : 1;
-        const int grid = (n_frames + fpw - 1) / fpw;
-        const void *k = fpw == 4 ? reinterpret_cast<const void *>(stats_narrow_kernel<4>)
-                      : fpw == 2 ? reinterpret_cast<const void *>(stats_narrow_kernel<2>)
-                                 : reinterpret_cast<const void *>(stats_narrow_kernel<1>);
-        hipError_t e = ensure_dynamic_lds(k, (2 * STAGE_MAX + 16) * 4);
+        // the staged windows' bins, over which the pool is laid out in order (R > 0), or followed by a pool
+        // region (R == 0: pools beyond 24 x 64 values); + a 16-value zero tail
+        const int staged = (stage_bins(geo) + 3) & ~3, pool16 = (geo.max_pool + 15) & ~15;
+        const int R = pool16 <= 8 * WAVE ? 8 : pool16 <= NARROW_REG_POOL * WAVE ? NARROW_REG_POOL : 0;
+        const size_t lds = sizeof(float) * (size_t)(R > 0 ? std::max(staged, pool16) + 16 : staged + pool16 + 16);
+        const void *k = R == 8 ? reinterpret_cast<const void *>(stats_narrow_kernel<8>)
+                      : R > 0 ? reinterpret_cast<const void *>(stats_narrow_kernel<NARROW_REG_POOL>)
+                              : reinterpret_cast<const void *>(stats_narrow_kernel<0>);
+        hipError_t e = ensure_dynamic_lds(k, (int)lds);
         if (e != hipSuccess) return e;
-        if (fpw == 4)
-            hipLaunchKernelGGL(stats_narrow_kernel<4>, dim3(grid), dim3(WAVE), 4 * per, stream, spectra, geo, now_ms,
-                               state, records, n_frames, gf);
-        else if (fpw == 2)
-            hipLaunchKernelGGL(stats_narrow_kernel<2>, dim3(grid), dim3(WAVE), 2 * per, stream, spectra, geo, now_ms,
-                               state, records, n_frames, gf);
+        if (R == 8)
+            hipLaunchKernelGGL(stats_narrow_kernel<8>, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms,
+                               state, records);
+        else if (R > 0)
+            hipLaunchKernelGGL(stats_narrow_kernel<NARROW_REG_POOL>, dim3(n_frames), dim3(WAVE), lds, stream, spectra,
+                               geo, now_ms, state, records);
         else
-            hipLaunchKernelGGL(stats_narrow_kernel<1>, dim3(grid), dim3(WAVE), per, stream, spectra, geo, now_ms, state,
-                               records, n_frames, gf);
+            hipLaunchKernelGGL(stats_narrow_kernel<0>, dim3(n_frames), dim3(WAVE), lds, stream, spectra, geo, now_ms,
+                               state, records);
     }
     if (SDRG_STATS_STAMPS) {  // diagnostic build: mean cycles per phase over the frames of this call
         std::vector<unsigned long long> h((size_t)STAMP_PHASES * 8192);

@@ -8,7 +8,7 @@ HIP="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -munsafe-fp-
 # SPECTRUM_SRC: an alternative spectrum.hip (A/B of a kernel change in one GPU session)
 $HIP -I$D/csrc -Iinclude -c ${SPECTRUM_SRC:-$D/csrc/spectrum.hip} -o $B/spectrum.o
 $HIP -c $D/csrc/fftany.hip -o $B/fftany.o
-$HIP -ffp-contract=off -fno-slp-vectorize -c $D/csrc/stats.hip -o $B/stats.o
+$HIP -I$D/csrc -Iinclude -ffp-contract=off -fno-slp-vectorize -c ${STATS_SRC:-$D/csrc/stats.hip} -o $B/stats.o
 $HIP -ffp-contract=off -fno-slp-vectorize -c $D/csrc/ssb.hip -o $B/ssb.o
 $HIP -ffp-contract=off -c $D/csrc/pulse.hip -o $B/pulse.o
 make -s -C $D  # host objects
