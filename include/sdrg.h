@@ -134,12 +134,14 @@ typedef struct sdrg_callbacks {
 } sdrg_callbacks;
 
 /* Per-kernel device times of the last process call, from hipEvents recorded on the stream each
- * kernel was launched on (only filled while profiling is enabled). */
+ * kernel was launched on (only filled while profiling is enabled).  Pipelined, the SSB chain's start marker
+ * would sit on the step's critical path, so only every 8th call measures ssb_ms (0 on the others; the
+ * timing statistics average the measured ones). */
 typedef struct sdrg_timings {
     float spectrum_ms;   /* unpack + FFT + |X|^2 + fftshift kernel */
     float stats_ms;      /* signal-strength kernel (+ spectral pulse detector when requested) */
     float ssb_ms;        /* whole SSB chain (all its kernels, + audio pulse detector when requested) */
-    float total_ms;      /* first launch start -> last kernel end, across both streams */
+    float total_ms;      /* call start -> end of the main stream's work; joined calls include the SSB stream */
 } sdrg_timings;
 
 /* ------------------------------------------------------------------------------------------------

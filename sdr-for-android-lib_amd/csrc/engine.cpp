@@ -118,6 +118,7 @@ struct PinnedVec {
 struct EvSet {
     hipEvent_t t0 = nullptr, spec = nullptr, stats = nullptr, ssb0 = nullptr, ssb1 = nullptr, end = nullptr;
     bool has_spec = false, has_stats = false, has_ssb = false, pending = false;
+    bool ssb_timed = false;  // ssb0 recorded: this call's SSB duration is measured
 };
 
 }  // namespace
@@ -143,7 +144,8 @@ struct sdrg_engine {
     // input release: recorded after the last kernel of a call that reads its iq buffer on each stream (the
     // spectrum on s_main, the SSB pipeline on s_ssb); sdrg_engine_input_released / _wait_input_released
     hipEvent_t ev_in_main = nullptr, ev_in_ssb = nullptr;
-    bool in_main_recorded = false, in_ssb_recorded = false;
+    // the markers the last call recorded after its iq readers (ev_in_* or the profiling ring's events)
+    hipEvent_t last_in_main = nullptr, last_in_ssb = nullptr;
     // profiling: a ring of event sets so consecutive calls are timed without host synchronisation
     static constexpr int RING = 64;
     EvSet ring[RING];
@@ -152,7 +154,8 @@ struct sdrg_engine {
     bool profiling = false;
     sdrg_timings last_timings{};
     double sum_spec = 0, sum_stats = 0, sum_ssb = 0, sum_total = 0;
-    int n_acc = 0;
+    int n_acc = 0, n_ssb = 0;
+    int calls_profiled = 0;
 
     // device state / buffers
     StatsState *d_stats = nullptr;
@@ -270,10 +273,10 @@ int32_t fold_slot(sdrg_engine *e, int slot) {
         t.spectrum_ms = ms;
     }
     if (ev.has_stats) {
-        HIP_TRY(hipEventElapsedTime(&ms, ev.has_spec ? ev.spec : ev.t0, ev.stats));
+        HIP_TRY(hipEventElapsedTime(&ms, ev.has_spec ? ev.spec : ev.t0, ev.end));
         t.stats_ms = ms;
     }
-    if (ev.has_ssb) {
+    if (ev.has_ssb && ev.ssb_timed) {
         // pipelined calls never join the SSB stream into ev.end's stream: wait for its own end event
         HIP_TRY(hipEventSynchronize(ev.ssb1));
         HIP_TRY(hipEventElapsedTime(&ms, ev.ssb0, ev.ssb1));
@@ -285,7 +288,10 @@ int32_t fold_slot(sdrg_engine *e, int slot) {
     if (slot == e->ring_last) e->last_timings = t;
     e->sum_spec += t.spectrum_ms;
     e->sum_stats += t.stats_ms;
-    e->sum_ssb += t.ssb_ms;
+    if (ev.has_ssb && ev.ssb_timed) {
+        e->sum_ssb += t.ssb_ms;
+        e->n_ssb++;
+    }
     e->sum_total += t.total_ms;
     e->n_acc++;
     return SDRG_OK;
@@ -501,8 +507,18 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         ev->has_spec = do_spec;
         ev->has_stats = do_stats;
         ev->has_ssb = do_ssb;
-        HIP_TRY(hipEventRecord(ev->t0, e->s_main));
+        // the SSB start marker sits on the SSB stream between the fork and the pipeline; pipelined, that
+        // stream is the step's critical path, so only every 8th call carries one (its mean is the sample's)
+        ev->ssb_timed = do_ssb && (!(e->pipelined && !join) || e->calls_profiled % 8 == 0);
+        e->calls_profiled++;
     }
+    // Markers: every event recorded between two kernels of a stream costs that stream a gap (several us
+    // measured), so a call records at most one at its start on the main stream (the SSB fork and the timing
+    // origin), one after the spectrum (timing only), and one at the end of each stream's work (input release,
+    // join, timing).  Profiling uses the ring's timing events for these; otherwise untimed ones.
+    hipEvent_t mk_start = prof ? ev->t0 : e->ev_fork;
+    hipEvent_t mk_main_end = prof ? ev->end : e->ev_in_main;
+    hipEvent_t mk_ssb_end = prof ? ev->ssb1 : e->ev_in_ssb;
     // The spectrum kernel runs alone on the whole chip first (it is HBM-bound and persistent, two
     // workgroups per CU); the SSB pipeline (latency-bound, one workgroup per CU) then runs beside the
     // statistics kernel on a forked stream.  Measured: the same step time as running the spectrum beside
@@ -511,10 +527,8 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     // joined at its end, so this call's SSB pipeline and the next call's spectrum share the chip as the
     // other's workgroups retire (steady state measured in tools/overlap_lab.py).
     const bool early_fork = e->pipelined && !join;
-    if (do_ssb && early_fork) {
-        HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));  // orders the SSB after the caller's producer work
-        HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
-    }
+    if (prof || (do_ssb && early_fork)) HIP_TRY(hipEventRecord(mk_start, e->s_main));
+    if (do_ssb && early_fork) HIP_TRY(hipStreamWaitEvent(e->s_ssb, mk_start, 0));  // after the caller's producer work
     // the spectrum / statistics stream: s_main, or the CU-split stream forked from it
     const bool split = e->s_spec && (do_spec || do_stats);
     hipStream_t sm = split ? e->s_spec : e->s_main;
@@ -526,14 +540,13 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, sm, do_ssb && early_fork && !split,
                                 split ? e->spec_cus : 0));
         if (prof) HIP_TRY(hipEventRecord(ev->spec, sm));
-        HIP_TRY(hipEventRecord(e->ev_in_main, sm));  // the spectrum is the main stream's last iq reader
     }
     if (do_ssb) {  // fork
         if (!early_fork) {
             HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
             HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
         }
-        if (prof) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
+        if (prof && ev->ssb_timed) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
         // AudioPulseDetector::process(pcm) after processSSB_opt (ssb_processor.cpp:109): its per-sample front
         // end runs inside the SSB kernel on the PCM it produces, the detector right after
         AudioFront af;
@@ -543,13 +556,12 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         }
         HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_chunk_table, e->d_ssb, e->d_ssb_scratch, pcm,
                            do_ap ? &af : nullptr, e->s_ssb));
-        HIP_TRY(hipEventRecord(e->ev_in_ssb, e->s_ssb));  // the SSB pipeline has read every raw sample
         if (do_ap) {
             int32_t rc = pulse_bank_audio_detect(&e->audio_bank, e->audio_bank.d_out, e->s_ssb);
             if (rc) return rc;
         }
-        if (prof) HIP_TRY(hipEventRecord(ev->ssb1, e->s_ssb));
-        HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
+        // the SSB stream's end marker: input release (the SSB pipeline, an iq reader, is done), join, timing
+        HIP_TRY(hipEventRecord(mk_ssb_end, e->s_ssb));
     }
     if (do_stats) {
         HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->d_pool, sm));
@@ -558,15 +570,16 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
                                              (int)sizeof(sdrg_frame_record), e->spec_bank.d_out, sm);
             if (rc) return rc;
         }
-        if (prof) HIP_TRY(hipEventRecord(ev->stats, sm));
     }
+    // the main stream's end marker: input release (the spectrum reads iq), timing; joined calls place it after
+    // the join, so total_ms spans both streams
     if (split) {
         HIP_TRY(hipEventRecord(e->ev_join_spec, e->s_spec));
         HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join_spec, 0));
     }
-    if (do_ssb && !early_fork) HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));  // join
+    if (do_ssb && !early_fork) HIP_TRY(hipStreamWaitEvent(e->s_main, mk_ssb_end, 0));  // join
+    if (do_spec || prof) HIP_TRY(hipEventRecord(mk_main_end, e->s_main));
     if (prof) {
-        HIP_TRY(hipEventRecord(ev->end, e->s_main));
         ev->pending = true;
         e->ring_last = e->ring_next;
         e->ring_next = (e->ring_next + 1) % sdrg_engine::RING;
@@ -577,8 +590,8 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         e->nco_phase = nco_next;
     }
     if (do_stats) e->cf_changed_pending = false;
-    e->in_main_recorded = e->in_main_recorded || do_spec;
-    e->in_ssb_recorded = e->in_ssb_recorded || do_ssb;
+    if (do_spec) e->last_in_main = mk_main_end;
+    if (do_ssb) e->last_in_ssb = mk_ssb_end;
     return SDRG_OK;
 }
 
@@ -725,9 +738,16 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         }
     }
     configure_fft(e);
+    // stream-to-stream ordering events on one device: no system-scope fence needed (lab: SDRG_EVENT_FENCE=1
+    // restores the default system-scope release/acquire)
+    static const unsigned ev_flags = [] {
+        const char *v = getenv("SDRG_EVENT_FENCE");
+        return (v && atoi(v) == 1) ? (unsigned)hipEventDisableTiming
+                                   : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
+    }();
     hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join, &e->ev_in_main, &e->ev_in_ssb};
     for (auto p : evs)
-        if (hipEventCreateWithFlags(p, hipEventDisableTiming) != hipSuccess)
+        if (hipEventCreateWithFlags(p, ev_flags) != hipSuccess)
             return cleanup(fail(SDRG_E_HIP, "hipEventCreate failed"));
     rc = alloc_state(e);
     if (rc) return cleanup(rc);
@@ -800,7 +820,7 @@ int32_t sdrg_engine_set_samples_per_reading(sdrg_engine *e, int32_t n) {
 int32_t sdrg_engine_input_released(const sdrg_engine *e, int32_t *released) {
     if (!e || !released) return fail(SDRG_E_INVALID, "null argument");
     *released = 1;
-    hipEvent_t evs[] = {e->in_main_recorded ? e->ev_in_main : nullptr, e->in_ssb_recorded ? e->ev_in_ssb : nullptr};
+    hipEvent_t evs[] = {e->last_in_main, e->last_in_ssb};
     for (hipEvent_t ev : evs) {
         if (!ev) continue;
         const hipError_t q = hipEventQuery(ev);
@@ -818,8 +838,8 @@ int32_t sdrg_engine_wait_input_released(sdrg_engine *e, void *hip_stream) {
     DeviceScope dscope(e->device);
     HIP_TRY(dscope.error());
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : e->s_main;
-    if (e->in_main_recorded && s != e->s_main) HIP_TRY(hipStreamWaitEvent(s, e->ev_in_main, 0));
-    if (e->in_ssb_recorded) HIP_TRY(hipStreamWaitEvent(s, e->ev_in_ssb, 0));
+    if (e->last_in_main && s != e->s_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));
+    if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
     return SDRG_OK;
 }
 
@@ -1078,8 +1098,9 @@ int32_t sdrg_engine_set_profiling(sdrg_engine *e, int32_t enabled) {
     HIP_TRY(dscope.error());
     if (enabled && !e->ring_created) {
         for (auto &r : e->ring) {
+            // timing only: no system-scope fence (its cache writeback would widen the gaps it measures)
             hipEvent_t *rev[] = {&r.t0, &r.spec, &r.stats, &r.ssb0, &r.ssb1, &r.end};
-            for (hipEvent_t *p : rev) HIP_TRY(hipEventCreate(p));
+            for (hipEvent_t *p : rev) HIP_TRY(hipEventCreateWithFlags(p, hipEventDisableSystemFence));
         }
         e->ring_created = true;
     }
@@ -1105,7 +1126,7 @@ int32_t sdrg_engine_get_timing_stats(const sdrg_engine *ce, sdrg_timings *mean, 
     const double k = e->n_acc > 0 ? 1.0 / e->n_acc : 0.0;
     mean->spectrum_ms = (float)(e->sum_spec * k);
     mean->stats_ms = (float)(e->sum_stats * k);
-    mean->ssb_ms = (float)(e->sum_ssb * k);
+    mean->ssb_ms = (float)(e->n_ssb > 0 ? e->sum_ssb / e->n_ssb : 0.0);
     mean->total_ms = (float)(e->sum_total * k);
     if (count) *count = e->n_acc;
     return SDRG_OK;
@@ -1116,7 +1137,7 @@ int32_t sdrg_engine_reset_timing_stats(sdrg_engine *e) {
     int32_t rc = fold_all(e);
     if (rc) return rc;
     e->sum_spec = e->sum_stats = e->sum_ssb = e->sum_total = 0;
-    e->n_acc = 0;
+    e->n_acc = e->n_ssb = 0;
     return SDRG_OK;
 }
 
