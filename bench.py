@@ -37,9 +37,12 @@ B = 4096
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 ALG_BYTES_PER_SAMPLE = {"spectrum": 6.0}  # CS8: 2 B in + 4 B fftshifted float32 power out
 N_INPUTS = 3  # distinct input batches rotated per step: 3 x 128 MiB > the 256 MiB Infinity Cache
-# SSB latency floor: the low-pass recurrence's dependent chain, measured in-kernel at 39 cycles per sample
-# (s_memtime stamps), at the chip's 2.4 GHz maximum clock: no schedule finishes a frame sooner
-SSB_CHAIN_CYCLES = 39
+# SSB floor: the sample-serial low-pass wave's own instruction issue.  Per sample it issues 6 VALU instructions
+# (the packed product of the previous output, 4 dependent adds, the packed product of the output before it) and
+# 0.5 LDS instructions (a 16-byte read and write per 4 samples); one wave issues at most one instruction per
+# 4 cycles and a dependent VALU op completes in 4 (tools/lab/lat.hip, dep_add.hip), so no
+# bit-exact schedule runs the recurrence faster than 26 cycles per sample at the chip's 2.4 GHz maximum clock
+SSB_CHAIN_CYCLES = 26
 MAX_CLOCK_GHZ = 2.4
 
 
@@ -437,9 +440,9 @@ def main() -> int:
         floor_ms = n * SSB_CHAIN_CYCLES / (MAX_CLOCK_GHZ * 1e9) * 1e3
         out["ssb_latency_floor"] = {
             "kernel": "ssb_pipe_kernel (the reference's sample-serial SSB chain, bit-exact)",
-            "bound": "latency", "floor_ms": round(floor_ms, 4),
-            "basis": f"{n} samples x {SSB_CHAIN_CYCLES} cycles (the low-pass recurrence's dependent chain, "
-                     f"measured in-kernel) / {MAX_CLOCK_GHZ} GHz max clock",
+            "bound": "serial issue", "floor_ms": round(floor_ms, 4),
+            "basis": f"{n} samples x {SSB_CHAIN_CYCLES} cycles (the low-pass wave's 6 VALU + 0.5 LDS instructions "
+                     f"per sample at one instruction per 4 cycles, tools/lab/lat.hip) / {MAX_CLOCK_GHZ} GHz max clock",
             "ssb_ms_alone": round(ssb_iso_ms, 4), "frac_alone": round(floor_ms / ssb_iso_ms, 4),
             "ssb_ms_coresident": round(ts["ssb_ms"], 4),
             "frac_coresident": round(floor_ms / ts["ssb_ms"], 4) if ts["ssb_ms"] > 0 else None}

@@ -10,6 +10,7 @@ PROG[spec]="--stages spectrum --calls 10"
 PROG[c2]="--stages spectrum+stats --calls 10"
 PROG[c5]="--stages spectrum+stats --n 65536 --fmt CS16 --streams 1024 --focus 200 --calls 4"
 PROG[c3]="--stages all --pipelined 1 --calls 12"
+PROG[ssb]="--stages ssb --calls 10"
 PASS_a="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU"
 PASS_b="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
 PASS_c="SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE SQ_INSTS_LDS_ATOMIC SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_LDS GRBM_GUI_ACTIVE GRBM_COUNT"

@@ -18,7 +18,7 @@ from collections import defaultdict
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r1"
 OUT = "profiles"
 os.makedirs(OUT, exist_ok=True)
-ENGINE = ("spectrum16k_kernel", "spectrum_kernel", "stats_kernel", "ssb_pipe_kernel", "four_step_a", "four_step_b", "ssb_chain_kernel",
+ENGINE = ("spectrum16k_kernel", "spectrum_kernel", "stats_narrow_kernel", "stats_wide_kernel", "stats_kernel", "ssb_pipe_kernel", "four_step_a", "four_step_b", "ssb_chain_kernel",
           "ssb_fir_kernel", "ssb_eq_kernel", "spectral_pulse_kernel", "audio_pulse_kernel", "audio_front_kernel",
           "pulse_reset_kernel")
 
@@ -48,20 +48,27 @@ if stats_csv:
     for r in csv.DictReader(open(stats_csv[0])):
         lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                      f"{float(r['MinNs']) / 1e3:.1f} | {float(r['MaxNs']) / 1e3:.1f} | {r['Percentage']} |")
-# per-launch durations of the roofline kernel from the trace: bench.py runs 3 warmup steps, the timed steps,
-# then 10 isolated spectrum-only launches; split them so each can be compared with the bench line's numbers
+# per-launch durations of the roofline kernel from the trace, split by whether the launch overlapped an SSB
+# pipeline launch (the pipelined schedule: co-resident) or ran with no SSB work on the chip (the isolated leg
+# and the FFT + statistics labelled leg)
 trace_csv = glob.glob(f"gpurun_out/prof_{TAG}/**/*kernel_trace.csv", recursive=True)
 if trace_csv:
-    rows = [r for r in csv.DictReader(open(trace_csv[0])) if "spectrum16k_kernel" in r["Kernel_Name"]]
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
-    if len(d) > 13:
-        timed, iso = d[3:-10], d[-10:]
+    allr = list(csv.DictReader(open(trace_csv[0])))
+    iv = lambda r: (int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+    ssb = [iv(r) for r in allr if "ssb_pipe_kernel" in r["Kernel_Name"]]
+    co, alone = [], []
+    for r in allr:
+        if "spectrum16k_kernel" not in r["Kernel_Name"]:
+            continue
+        s0, e0 = iv(r)
+        (co if any(s < e0 and s0 < e for s, e in ssb) else alone).append((e0 - s0) / 1e3)
+    if co and alone:
         lines += ["", "## spectrum16k_kernel launch durations from the kernel trace", "",
-                  f"* timed region ({len(timed)} launches, pipelined with the SSB stages): "
-                  f"avg {sum(timed) / len(timed):.1f} us",
-                  f"* isolated pass after it ({len(iso)} launches, the kernel alone): avg {sum(iso) / len(iso):.1f} us",
-                  "* the bench line's `roofline` / `roofline_isolated` use the same two sets, timed with HIP events"]
+                  f"* beside an SSB pipeline launch ({len(co)} launches, the pipelined schedule): "
+                  f"avg {sum(co) / len(co):.1f} us",
+                  f"* with no SSB work on the chip ({len(alone)} launches: the isolated leg and the FFT + statistics "
+                  f"labelled leg): avg {sum(alone) / len(alone):.1f} us",
+                  "* the bench line's `roofline` / `roofline_isolated` time the same two situations with HIP events"]
 bench = None
 blog = f"gpurun_out/bench_{TAG}.log"
 if os.path.exists(blog):

@@ -17,7 +17,8 @@ def kname(full):
         return None
     return full.replace("void ", "").replace("sdrg::(anonymous namespace)::", "").replace("sdrg::", "").split("(")[0][:70]
 progs = {"spec": "spectrum alone (4096 x 16384 CS8, 10 calls)", "c2": "spectrum + stats (4096 x 16384, 5 kHz)",
-         "c5": "spectrum + stats (1024 x 65536 CS16, 200 kHz)", "c3": "all stages pipelined (the c3 step, co-resident)"}
+         "c5": "spectrum + stats (1024 x 65536 CS16, 200 kHz)", "c3": "all stages pipelined (the c3 step, co-resident)",
+         "ssb": "SSB stage alone (4096 x 16384 CS8, 10 calls)"}
 print(f"# SQ counters ({tag}): rocprofv3 --kernel-trace --pmc, one pass per group (tools/gpu_sq_profile.sh)\n")
 for p, desc in progs.items():
     acc = defaultdict(lambda: defaultdict(list))
