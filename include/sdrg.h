@@ -401,13 +401,22 @@ int32_t sdrg_engine_synchronize(sdrg_engine *eng);
  * are ordered after each call without a host synchronisation.  Synchronises the previous stream first.
  * The stream must outlive the engine (or be unset with NULL before it is destroyed). */
 int32_t sdrg_engine_set_stream(sdrg_engine *eng, void *hip_stream);
-/* Pipelining across calls (default off).  When on, sdrg_engine_process_device forks the SSB stages at the
- * start of each call and does not join them into the main stream at its end, so a call's SSB pipeline runs
- * beside the next call's spectrum.  The spectrum / statistics / spectral-pulse outputs are ordered on the
- * main stream as usual; the PCM and audio-pulse outputs are complete after sdrg_engine_synchronize (or
- * after the next call's SSB stage starts, which follows them on the SSB stream).  process_host always joins.
- * The input buffer stays in use until the SSB stage has read it: see sdrg_engine_input_released below. */
-int32_t sdrg_engine_set_pipelining(sdrg_engine *eng, int32_t on);
+/* Pipelining across calls (default SDRG_PIPELINE_OFF).  Pipelined, sdrg_engine_process_device forks the SSB
+ * stages at the start of each call and does not join them into the main stream at its end, so a call's SSB
+ * pipeline runs beside the next call's spectrum.  The spectrum / statistics / spectral-pulse outputs are
+ * ordered on the main stream as usual; the PCM and audio-pulse outputs are complete after
+ * sdrg_engine_synchronize (or after the next call's SSB stage starts, which follows them on the SSB stream).
+ * process_host always joins.  The input buffer stays in use until the SSB stage has read it: see
+ * sdrg_engine_input_released below.
+ *   SDRG_PIPELINE_ON: the SSB stage of a call starts after the work enqueued on the main stream before the
+ *     call (the caller's producer work on iq), as the spectrum does.
+ *   SDRG_PIPELINE_INPUTS_READY: the caller guarantees that iq is complete when the call is made (written by
+ *     host-synchronised copies or earlier, already-finished work, e.g. a resident ring of input frames); the
+ *     SSB stage then does not wait for the main stream at all, which saves its stream one cross-stream wait
+ *     per call.  Work the caller enqueues on the main stream that writes iq is NOT waited for in this mode.
+ * Any other value returns SDRG_E_INVALID. */
+enum { SDRG_PIPELINE_OFF = 0, SDRG_PIPELINE_ON = 1, SDRG_PIPELINE_INPUTS_READY = 2 };
+int32_t sdrg_engine_set_pipelining(sdrg_engine *eng, int32_t mode);
 /* The INPUT of a call: the kernels read `iq` asynchronously after sdrg_engine_process_device returns -- the
  * spectrum on the main stream and the SSB pipeline on its own stream, which in pipelined mode runs on past the
  * call, beside the next call's spectrum.  The caller must not overwrite or free `iq` until the call has released

@@ -194,6 +194,7 @@ struct sdrg_engine {
     PinnedVec<sdrg_pulse_output> h_pspec, h_paudio;
     bool cf_changed_pending = false;
     bool pipelined = false;  // sdrg_engine_set_pipelining: no join of the SSB stream per call
+    bool inputs_ready = false;  // SDRG_PIPELINE_INPUTS_READY: no fork wait on the main stream either
     // NCO/short-FIR SSB variant (sdrg_engine_set_ssb_variant; a build extension, off by default)
     double nco_hz = 0.0;
     int fir_taps = 0;            // 0: the reference's 255
@@ -527,8 +528,12 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     // joined at its end, so this call's SSB pipeline and the next call's spectrum share the chip as the
     // other's workgroups retire (steady state measured in tools/overlap_lab.py).
     const bool early_fork = e->pipelined && !join;
-    if (prof || (do_ssb && early_fork)) HIP_TRY(hipEventRecord(mk_start, e->s_main));
-    if (do_ssb && early_fork) HIP_TRY(hipStreamWaitEvent(e->s_ssb, mk_start, 0));  // after the caller's producer work
+    // the fork: the SSB stage waits for what the caller enqueued on the main stream before this call (its
+    // producer work on iq) -- unless the caller declared its inputs complete at call time
+    // (SDRG_PIPELINE_INPUTS_READY), which saves the SSB stream a cross-stream wait per call (measured ~20 us)
+    const bool fork_wait = do_ssb && early_fork && !e->inputs_ready;
+    if (prof || fork_wait) HIP_TRY(hipEventRecord(mk_start, e->s_main));
+    if (fork_wait) HIP_TRY(hipStreamWaitEvent(e->s_ssb, mk_start, 0));
     // the spectrum / statistics stream: s_main, or the CU-split stream forked from it
     const bool split = e->s_spec && (do_spec || do_stats);
     hipStream_t sm = split ? e->s_spec : e->s_main;
@@ -924,7 +929,10 @@ int32_t sdrg_engine_set_pipelining(sdrg_engine *e, int32_t on) {
         HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
         HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));
     }
-    e->pipelined = on != 0;
+    if (on != SDRG_PIPELINE_OFF && on != SDRG_PIPELINE_ON && on != SDRG_PIPELINE_INPUTS_READY)
+        return fail(SDRG_E_INVALID, "pipelining mode must be 0, 1 or 2, got %d", on);
+    e->pipelined = on != SDRG_PIPELINE_OFF;
+    e->inputs_ready = on == SDRG_PIPELINE_INPUTS_READY;
     return SDRG_OK;
 }
 

@@ -29,6 +29,7 @@ LIB_PATH = os.environ.get("SDRG_LIB_PATH") or os.path.join(PKG, "lib", "libsdrg.
 CF32, CS8, CU8, CS16, CS12 = 0, 1, 2, 3, 4
 STAGE_SPECTRUM, STAGE_STATS, STAGE_SSB, STAGE_HOT_PATH = 1, 2, 4, 7
 STAGE_SPECTRAL_PULSE, STAGE_AUDIO_PULSE, STAGE_ALL = 8, 16, 31
+PIPELINE_OFF, PIPELINE_ON, PIPELINE_INPUTS_READY = 0, 1, 2  # sdrg_engine_set_pipelining modes
 PULSE_SPECTRAL, PULSE_AUDIO = 0, 1
 STATUS = {0: "SDRG_OK", -1: "SDRG_E_INVALID", -2: "SDRG_E_UNSUPPORTED", -3: "SDRG_E_NOMEM", -4: "SDRG_E_HIP",
           -5: "SDRG_E_NODEVICE"}
@@ -504,9 +505,10 @@ class Engine:
     def synchronize(self) -> None:
         _check(load().sdrg_engine_synchronize(self._h), "synchronize")
 
-    def set_pipelining(self, on: bool) -> None:
-        """Overlap each call's SSB stages with the next call's spectrum (see include/sdrg.h)."""
-        _check(load().sdrg_engine_set_pipelining(self._h, int(on)), "set_pipelining")
+    def set_pipelining(self, mode) -> None:
+        """Overlap each call's SSB stages with the next call's spectrum (see include/sdrg.h): False/PIPELINE_OFF,
+        True/PIPELINE_ON, or PIPELINE_INPUTS_READY (iq complete at call time: no wait on the main stream)."""
+        _check(load().sdrg_engine_set_pipelining(self._h, int(mode)), "set_pipelining")
 
     def set_ssb_variant(self, nco_hz: float = 0.0, fir_taps: int = 0) -> None:
         """BUILD EXTENSION (not a reference interface): NCO mixer at nco_hz before the SSB chain and a

@@ -143,6 +143,18 @@ def test_rejected_call_freezes_nothing(S, O):
     eng.close()
 
 
+def test_pipelining_modes(S, O):
+    """sdrg_engine_set_pipelining takes SDRG_PIPELINE_OFF / _ON / _INPUTS_READY; anything else is SDRG_E_INVALID
+    and leaves the mode unchanged (the next pipelined calls still equal the joined schedule: test_gpu_parity)."""
+    eng = engine(S, N, FS, 2)
+    for mode in (S.PIPELINE_OFF, S.PIPELINE_ON, S.PIPELINE_INPUTS_READY, S.PIPELINE_OFF):
+        eng.set_pipelining(mode)
+    for bad in (-1, 3, 7):
+        with pytest.raises(S.SdrgError):
+            eng.set_pipelining(bad)
+    eng.close()
+
+
 def test_set_sample_rate_is_bridge_config_only(S, O):
     """setSampleRate (:931-953) changes BridgeConfig only: the SSB chain sees the new rate from the next frame
     (handed the bridge's rate per frame, :441-442), the statistics keep FFTProcessor::config_'s rate until the next

@@ -316,7 +316,8 @@ def test_ingest_cs12_reads_to_engine(S, O):
 
 def test_pipelined_calls_equal_joined_calls(S, O):
     """sdrg_engine_set_pipelining: each call's SSB stages overlap the next call's spectrum; after synchronize
-    every output (spectra, records, PCM, both pulse detectors) equals the joined schedule bit for bit."""
+    every output (spectra, records, PCM, both pulse detectors) equals the joined schedule bit for bit, in both
+    pipelined modes (the SSB stage forked from the main stream, and the inputs-ready mode with no fork)."""
     import torch
     n, fs, B, F = 16384, 2_000_000, 256, 4
     dev = torch.device("cuda:0")
@@ -324,7 +325,7 @@ def test_pipelined_calls_equal_joined_calls(S, O):
                                                       seed=100 * f + b)[0] for b in range(B)])).to(dev)
             for f in range(F)]
     outs = {}
-    for mode in (False, True):
+    for mode in (S.PIPELINE_OFF, S.PIPELINE_ON, S.PIPELINE_INPUTS_READY):
         eng = engine(S, n, fs, B)
         eng.set_pipelining(mode)
         spec = [torch.empty((B, n), dtype=torch.float32, device=dev) for _ in range(F)]
@@ -338,6 +339,8 @@ def test_pipelined_calls_equal_joined_calls(S, O):
         sp, au = eng.pulse_outputs()
         outs[mode] = (torch.stack(spec).cpu(), torch.stack(rec).cpu(), torch.stack(pcm).cpu(), sp, au)
         eng.close()
-    a, b = outs[False], outs[True]
-    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
-    assert a[3].tobytes() == b[3].tobytes() and a[4].tobytes() == b[4].tobytes()
+    a = outs[S.PIPELINE_OFF]
+    for mode in (S.PIPELINE_ON, S.PIPELINE_INPUTS_READY):
+        b = outs[mode]
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]), mode
+        assert a[3].tobytes() == b[3].tobytes() and a[4].tobytes() == b[4].tobytes(), mode
