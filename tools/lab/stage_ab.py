@@ -13,7 +13,7 @@ iqs = [bench.synth_device_frames(torch, dev, bench.B, seed=7 + k, n=bench.N, cs1
 spec = torch.empty((bench.B, bench.N), dtype=torch.float32, device=dev)
 rec = torch.zeros((bench.B, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
 pcm = torch.empty((bench.B, eng.pcm_len), dtype=torch.int16, device=dev)
-eng.set_pipelining(True)
+eng.set_pipelining(int(os.environ.get("LAB_PIPE_MODE", "2")))
 now = [1000]
 def run(k, stages, prof=False):
     eng.set_profiling(prof)
@@ -27,7 +27,7 @@ def run(k, stages, prof=False):
 legs = {"all": sdrg.STAGE_ALL, "no spectral pulse": sdrg.STAGE_ALL & ~sdrg.STAGE_SPECTRAL_PULSE,
         "no audio pulse": sdrg.STAGE_ALL & ~sdrg.STAGE_AUDIO_PULSE, "no pulse": sdrg.STAGE_HOT_PATH}
 for st in legs.values():
-    run(10, st)
+    run(60, st)
 for rep in range(3):
     print("  ".join(f"{name} {run(50, st):.4f}" for name, st in legs.items()), flush=True)
 for name, st in legs.items():  # per-kernel device times (events), profiled run

@@ -15,7 +15,7 @@ iqs = [bench.synth_device_frames(torch, dev, bench.B, seed=7 + k, n=bench.N, cs1
 spec = torch.empty((bench.B, bench.N), dtype=torch.float32, device=dev)
 rec = torch.zeros((bench.B, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
 pcm = torch.empty((bench.B, eng.pcm_len), dtype=torch.int16, device=dev)
-eng.set_pipelining(True)
+eng.set_pipelining(int(os.environ.get("LAB_PIPE_MODE", "2")))
 now = [1000]
 def run(k, prof):
     eng.set_profiling(prof)

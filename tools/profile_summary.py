@@ -43,7 +43,7 @@ stats_csv = glob.glob(f"gpurun_out/prof_{TAG}/**/*kernel_stats.csv", recursive=T
 lines = [f"# Round profile {TAG}", ""]
 if stats_csv:
     shutil.copy(stats_csv[0], f"{OUT}/{TAG}_kernel_stats.csv")
-    lines += ["## rocprofv3 --kernel-trace --stats (bench.py --steps 20 --warmup 3 --no-cpu-baseline, defaults)", "",
+    lines += ["## rocprofv3 --kernel-trace --stats (bench.py --steps 40 --warmup 50 --no-cpu-baseline, defaults)", "",
               "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
     for r in csv.DictReader(open(stats_csv[0])):
         lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
