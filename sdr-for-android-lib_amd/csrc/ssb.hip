@@ -23,6 +23,7 @@
 
 #include "pulse_front.h"
 #include "sdrg_internal.h"
+#include "ssb_lpf_asm.h"
 #include "ssb_math.h"
 
 #pragma clang fp contract(off)
@@ -314,6 +315,10 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 //   SIMD2: AGC,  desired (1/4),     desired (1/4)
 //   SIMD3: load, FIR (slot group 0), FIR (slot group 1)
 // ================================================================================================
+// the low-pass wave's full chunks as one hand-scheduled asm block (1) or through row_pipeline (0)
+#ifndef SDRG_LPF_ASM
+#define SDRG_LPF_ASM 1
+#endif
 constexpr int PG = 16;          // streams per workgroup
 // serial roles (bit 0 DC, 1 LPF, 2 AGC) that run on all 64 lanes (16 copies of the 16 streams) instead of the
 // first 16: a dependent VALU chain issues faster with the full EXEC mask, while the LDS reads of 16 copies cost
@@ -379,6 +384,11 @@ struct PipeLds {
 };
 // NCO variant only, in dynamic LDS: the phasor tables, then the current chunk's CH phasors {re, im}
 constexpr int NCO_LDS_BYTES = (2 * 1024 * 2 + 2 * CH) * 4;
+
+// LDS byte address of a pointer into the workgroup's LDS (for asm operands)
+__device__ __forceinline__ uint32_t lds_addr(const float *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)p;
+}
 
 // Workgroup barrier that orders LDS only.  __syncthreads() is a workgroup release/acquire, which makes
 // every wave drain ALL its outstanding memory operations (s_waitcnt vmcnt(0)) first - the loader's
@@ -627,7 +637,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                     }
                 } else
 #endif
-                if (lim == CH) {
+                if (lim == CH && SDRG_LPF_ASM && !(SDRG_SERIAL_FULL_EXEC & 2)) {
+                    // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
+                    f2v z = {z1, z2};
+                    const uint32_t src = lds_addr(&L.a[c & 1][my_s * ROW]), dst = lds_addr(&L.y[c & 3][my_s * ROW]);
+                    asm volatile(SDRG_LPF_CHUNK_ASM
+                                 : [z] "+v"(z)
+                                 : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
+                                 : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+                    z1 = z.x;
+                    z2 = z.y;
+                } else if (lim == CH) {
                     row_pipeline(&L.a[c & 1][my_s * ROW], &L.y[c & 3][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                         for (int q = 0; q < SB; q++) {

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
+#include "../../sdr-for-android-lib_amd/csrc/ssb_lpf_asm.h"
+
 typedef float f2v __attribute__((ext_vector_type(2)));
 #pragma clang fp contract(off)
 
@@ -20,7 +22,25 @@ __global__ void k(unsigned long long *out, const float *xs) {
     unsigned long long dt = 0;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int c = 0; c < NCH; c++) {
-        if (w == 0 && (MODE < 3 || lane < 16)) {
+        if (MODE >= 4 && w == 0 && ((MODE != 6 && MODE != 8 && MODE != 9) || lane < 16)) {
+            // the product's hand-scheduled chunk (csrc/ssb_lpf_asm.h): 4 = 64 lanes alone, 5 = 64 lanes + barrier,
+            // 6 = 16 lanes + barrier
+            f2v z = {z1, z2};
+            const uint32_t src = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)&lds[c & 1][(lane & 15) * ROW];
+            const uint32_t dst = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float *)&lds[(c + 1) & 1][(lane & 15) * ROW];
+            if constexpr (MODE == 9) {  // VALU on all 64 lanes, LDS on the caller's 16 (SPLIT), + barrier
+                unsigned long long sv;
+                asm volatile(SDRG_LPF_CHUNK_SPLIT_ASM : [z] "+v"(z), [sv] "=&s"(sv) : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
+                             : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+            } else if constexpr (MODE >= 7)  // register data only: 7 = 64 lanes, 8 = 16 lanes (+ barrier, 12 waves)
+                asm volatile(SDRG_LPF_CHUNK_NOLDS_ASM : [z] "+v"(z) : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
+                             : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+            else
+                asm volatile(SDRG_LPF_CHUNK_ASM : [z] "+v"(z) : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
+                             : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+            z1 = z.x;
+            z2 = z.y;
+        } else if (MODE < 4 && w == 0 && (MODE < 3 || lane < 16)) {
             float v[CH];
             const float *src = &lds[c & 1][(lane & 15) * ROW];
             if constexpr (MODE == 0) {
@@ -49,7 +69,7 @@ __global__ void k(unsigned long long *out, const float *xs) {
                 for (int q = 0; q < CH; q += 4) *reinterpret_cast<float4 *>(dst + q) = make_float4(v[q], v[q + 1], v[q + 2], v[q + 3]);
             }
         }
-        if constexpr (MODE >= 2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (MODE >= 2 && MODE != 4) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     dt = __builtin_amdgcn_s_memtime() - t0;
     if (threadIdx.x == 0) out[0] = dt;
@@ -76,5 +96,14 @@ int main() {
     run<2>("LDS row in/out + barrier", d, xs, 1);
     run<2>("LDS row in/out + barrier", d, xs, 12);
     run<3>("LDS + barrier, 16 lanes", d, xs, 12);
+    run<4>("asm chunk, 64 lanes", d, xs, 1);
+    run<5>("asm chunk + barrier, 64 lanes", d, xs, 12);
+    run<6>("asm chunk + barrier, 16 lanes", d, xs, 12);
+    run<7>("asm chunk no LDS + barrier, 64 lanes", d, xs, 12);
+    run<8>("asm chunk no LDS + barrier, 16 lanes", d, xs, 12);
+    run<9>("asm split (VALU 64, LDS 16) + barrier", d, xs, 12);
+    run<9>("asm split (VALU 64, LDS 16) + barrier", d, xs, 1);
+    run<6>("asm chunk + barrier, 16 lanes", d, xs, 1);
+    run<8>("asm chunk no LDS + barrier, 16 lanes", d, xs, 1);
     return 0;
 }
