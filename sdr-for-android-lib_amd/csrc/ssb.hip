@@ -315,9 +315,14 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 //   SIMD2: AGC,  desired (1/4),     desired (1/4)
 //   SIMD3: load, FIR (slot group 0), FIR (slot group 1)
 // ================================================================================================
-// the low-pass wave's full chunks as one hand-scheduled asm block (1) or through row_pipeline (0)
+// the low-pass wave's full chunks as one hand-scheduled asm block (1; 2: its VALU on all 64 lanes, the LDS
+// operations on the 16 stream lanes) or through row_pipeline (0)
 #ifndef SDRG_LPF_ASM
 #define SDRG_LPF_ASM 1
+#endif
+// the AGC gain wave's chunks as one hand-scheduled asm block (1) or through row_pipeline (0)
+#ifndef SDRG_AGC_ASM
+#define SDRG_AGC_ASM 1
 #endif
 constexpr int PG = 16;          // streams per workgroup
 // serial roles (bit 0 DC, 1 LPF, 2 AGC) that run on all 64 lanes (16 copies of the 16 streams) instead of the
@@ -641,10 +646,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                     // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                     f2v z = {z1, z2};
                     const uint32_t src = lds_addr(&L.a[c & 1][my_s * ROW]), dst = lds_addr(&L.y[c & 3][my_s * ROW]);
-                    asm volatile(SDRG_LPF_CHUNK_ASM
-                                 : [z] "+v"(z)
-                                 : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
-                                 : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+                    if (SDRG_LPF_ASM == 2) {  // VALU on all 64 lanes, LDS on the 16 stream lanes
+                        unsigned long long sv;
+                        asm volatile(SDRG_LPF_CHUNK_SPLIT_ASM
+                                     : [z] "+v"(z), [sv] "=&s"(sv)
+                                     : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
+                                     : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+                    } else {
+                        asm volatile(SDRG_LPF_CHUNK_ASM
+                                     : [z] "+v"(z)
+                                     : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
+                                     : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+                    }
                     z1 = z.x;
                     z2 = z.y;
                 } else if (lim == CH) {
@@ -685,7 +698,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         chunk_loop([&](int it) {
             // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
             const int c = it - 4;
-            if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 4) || lane < PG)) {
+            if (SDRG_AGC_ASM && !(SDRG_SERIAL_FULL_EXEC & 4) && c >= 0 && c < nch && lane < PG) {
+                // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
+                f2v g = {gain, gain};
+                const uint32_t src = lds_addr(&L.d[c & 1][my_s * ROW]), dst = lds_addr(&L.g[c & 1][my_s * ROW]);
+                asm volatile(SDRG_AGC_CHUNK_ASM
+                             : [g] "+v"(g)
+                             : [src] "v"(src), [dst] "v"(dst), [keep] "s"(keep), [rates] "s"(rates)
+                             : SDRG_CHUNK_CLOBBERS, "vcc", "memory");
+                gain = g.x;
+            } else if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 4) || lane < PG)) {
                 row_pipeline(&L.d[c & 1][my_s * ROW], &L.g[c & 1][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                     for (int q = 0; q < SB; q++) {

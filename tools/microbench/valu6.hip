@@ -31,13 +31,13 @@ __global__ void k(unsigned long long *out, const float *xs) {
             if constexpr (MODE == 9) {  // VALU on all 64 lanes, LDS on the caller's 16 (SPLIT), + barrier
                 unsigned long long sv;
                 asm volatile(SDRG_LPF_CHUNK_SPLIT_ASM : [z] "+v"(z), [sv] "=&s"(sv) : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
-                             : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+                             : SDRG_CHUNK_CLOBBERS, "memory");
             } else if constexpr (MODE >= 7)  // register data only: 7 = 64 lanes, 8 = 16 lanes (+ barrier, 12 waves)
                 asm volatile(SDRG_LPF_CHUNK_NOLDS_ASM : [z] "+v"(z) : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
-                             : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+                             : SDRG_CHUNK_CLOBBERS, "memory");
             else
                 asm volatile(SDRG_LPF_CHUNK_ASM : [z] "+v"(z) : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
-                             : SDRG_LPF_CHUNK_CLOBBERS, "memory");
+                             : SDRG_CHUNK_CLOBBERS, "memory");
             z1 = z.x;
             z2 = z.y;
         } else if (MODE < 4 && w == 0 && (MODE < 3 || lane < 16)) {
