@@ -320,6 +320,10 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 #ifndef SDRG_LPF_ASM
 #define SDRG_LPF_ASM 1
 #endif
+// the DC wave's chunks as one hand-scheduled asm block (1) or through row_pipeline (0)
+#ifndef SDRG_DC_ASM
+#define SDRG_DC_ASM 1
+#endif
 // the AGC gain wave's chunks as one hand-scheduled asm block (1) or through row_pipeline (0)
 #ifndef SDRG_AGC_ASM
 #define SDRG_AGC_ASM 1
@@ -600,10 +604,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         chunk_loop([&](int it) {
             // ---- removeDC (:49-55) and the a0*x term of iir2Process, chunk it-1 ----
             const int c = it - 1;
-            if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 1) || lane < PG)) {
-                // the frame's last chunk runs whole too: dc restarts every frame and the samples past the
-                // frame end (zeros from the loader) only feed outputs nothing reads
-                const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
+            // the frame's last chunk runs whole too: dc restarts every frame and the samples past the frame end
+            // (zeros from the loader) only feed outputs nothing reads
+            const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
+            if (SDRG_DC_ASM && !(SDRG_SERIAL_FULL_EXEC & 1) && c >= 0 && c < nch && lane < PG) {
+                // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
+                const f2v om2 = {one_minus, one_minus}, a02 = {a0, a0};
+                const uint32_t src = lds_addr(&L.re[c & 1][my_s * ROW]), dst = lds_addr(&L.a[c & 1][my_s * ROW]);
+                asm volatile(SDRG_DC_CHUNK_ASM
+                             : [dc] "+v"(dc)
+                             : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
+                             : SDRG_CHUNK_CLOBBERS, "memory");
+            } else if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 1) || lane < PG)) {
                 row_pipeline(&L.re[c & 1][my_s * ROW], &L.a[c & 1][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                     for (int q = 0; q < SB; q++) {

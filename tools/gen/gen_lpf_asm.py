@@ -1,5 +1,8 @@
-"""Generate csrc/ssb_lpf_asm.h: the SSB pipeline's two heaviest serial roles, one 64-sample chunk each, as
-hand-scheduled asm blocks.
+"""Generate csrc/ssb_lpf_asm.h: the SSB pipeline's three serial roles (DC tracker, low-pass, AGC gain), one 64-sample
+chunk each, as hand-scheduled asm blocks.
+
+DC wave (removeDC, ssb_demod_opt.cpp:49-55, and iir2Process's a0 x product): see dc_pair(); two samples per group
+of seven instructions (the order-free products and the v - dc / a0 steps packed over sample pairs).
 
 Low-pass wave (iir2Process, ssb_demod_opt.cpp:75-84), per sample in the reference's float order without
 contraction (products rounded, adds left to right):
@@ -58,6 +61,22 @@ def agc_sample(x, g):
     ]
 
 
+def dc_pair(x, prev):
+    """removeDC (ssb_demod_opt.cpp:49-55) for samples x, x + 1 (x even) and the a0 product of iir2Process:
+    dc = alpha dc + (1 - alpha) v, v' = a0 (v - dc).  The (1 - alpha) v products of both samples are one packed
+    multiply, the two dc steps run on v48 / v49 (so the pair {dc_x, dc_x+1} is v[48:49]), then v - dc and the a0
+    product are one packed op each over the sample pair.  prev: the VGPR holding the dc before sample x."""
+    return [
+        f"v_pk_mul_f32 v[50:51], %[om2], v[{x}:{x + 1}]",
+        f"v_mul_f32 v52, %[alpha], v{prev}",
+        f"v_add_f32 v48, v52, v50",
+        f"v_mul_f32 v52, %[alpha], v48",
+        f"v_add_f32 v49, v52, v51",
+        f"v_pk_add_f32 v[{x}:{x + 1}], v[{x}:{x + 1}], v[48:49] neg_lo:[0,1] neg_hi:[0,1]",
+        f"v_pk_mul_f32 v[{x}:{x + 1}], %[a02], v[{x}:{x + 1}]",
+    ]
+
+
 def reads(sb, buf):
     return [f"ds_read_b128 v[{buf + 4 * i}:{buf + 4 * i + 3}], %[src] offset:{(16 * sb + 4 * i) * 4}" for i in range(4)]
 
@@ -67,7 +86,7 @@ def writes(sb, buf):
 
 
 def chunk(role, lds=True, split=False):
-    """role 'lpf' or 'agc'.  split: VALU with all 64 lanes on (lanes past the 16 streams compute on whatever their
+    """role 'dc', 'lpf' or 'agc'.  split (low-pass, lab): VALU with all 64 lanes on (lanes past the 16 streams compute on whatever their
     registers hold and store nothing), LDS operations with the caller's EXEC (saved in %[sv])"""
     out = []
 
@@ -84,6 +103,8 @@ def chunk(role, lds=True, split=False):
     waits = {0: 4, 1: 8, 2: 8, 3: 4}
     if role == "lpf":
         prev1, prev2 = ("%[z]", 0), ("%[z]", 1)  # z.x = z1, z.y = z2 of the chunk's first sample
+    elif role == "dc":
+        out.append("v_mov_b32 v49, %[dc]")  # the incoming dc
     else:
         out.append(f"v_pk_mov_b32 v[{T0}:{T0 + 1}], %[g], %[g] op_sel:[0,0]")  # the incoming gain as a VGPR
         g = T0
@@ -92,6 +113,10 @@ def chunk(role, lds=True, split=False):
             out.append(f"s_waitcnt lgkmcnt({waits[sb]})")
         b = buf[sb]
         for q in range(16):
+            if role == "dc":
+                if q % 2 == 0:
+                    out += dc_pair(b + q, 49)
+                continue
             if role == "lpf":
                 out += lpf_sample(b + q, prev1, prev2)
                 prev2, prev1 = prev1, pair(b + q)
@@ -103,7 +128,9 @@ def chunk(role, lds=True, split=False):
     last = buf[3] + 15
     if split:  # the carried state is written on the caller's lanes only
         out.append("s_mov_b64 exec, %[sv]")
-    if role == "lpf":  # carry (z1, z2) = (y63, y62): one v_pk_mov_b32 from the aligned pair holding both
+    if role == "dc":
+        out.append("v_mov_b32 %[dc], v49")
+    elif role == "lpf":  # carry (z1, z2) = (y63, y62): one v_pk_mov_b32 from the aligned pair holding both
         out.append(f"v_pk_mov_b32 %[z], v[{last - 1}:{last}], v[{last - 1}:{last}] op_sel:[1,0]")
     else:
         out.append(f"v_pk_mov_b32 %[g], v[{last - 1}:{last}], v[{last - 1}:{last}] op_sel:[1,1]")
@@ -118,14 +145,16 @@ def emit(name, lines):
 
 
 def main():
-    print("// Generated by tools/gen/gen_lpf_asm.py -- do not edit.  The SSB pipeline's low-pass and AGC waves, one 64-sample")
-    print("// chunk each; see the generator for the schedule.  Operands: %[src] / %[dst] (v, LDS byte addresses of the")
+    print("// Generated by tools/gen/gen_lpf_asm.py -- do not edit.  The SSB pipeline's DC, low-pass and AGC waves, one")
+    print("// 64-sample chunk each; see the generator for the schedule.  Operands: %[src] / %[dst] (v, LDS byte addresses of the")
     print("// stream's input / output rows); low-pass: %[z] (+v, {z1, z2}), %[c1] = {a1, -b1}, %[c2] = {a2, -b2} (s);")
-    print("// AGC: %[g] (+v, {gain, -}), %[keep] = {1 - fast, 1 - slow}, %[rates] = {fast, slow} (s).  Clobbers v0-v53")
-    print("// (SDRG_CHUNK_CLOBBERS) and, for the AGC, vcc.")
+    print("// AGC: %[g] (+v, {gain, -}), %[keep] = {1 - fast, 1 - slow}, %[rates] = {fast, slow} (s); DC: %[dc] (+v), %[alpha],")
+    print("// %[om2] = {1 - alpha, 1 - alpha}, %[a02] = {a0, a0} (s).  Clobbers v0-v53 (SDRG_CHUNK_CLOBBERS) and, for the")
+    print("// AGC, vcc.")
     print("#pragma once")
     emit("SDRG_LPF_CHUNK_ASM", chunk("lpf"))
     emit("SDRG_AGC_CHUNK_ASM", chunk("agc"))
+    emit("SDRG_DC_CHUNK_ASM", chunk("dc"))
     print("// the low-pass chunk with its VALU on all 64 lanes and the LDS operations on the caller's lanes; extra operand")
     print("// %[sv] (=&s, 64-bit): the caller's EXEC (lab option SDRG_LPF_ASM=2)")
     emit("SDRG_LPF_CHUNK_SPLIT_ASM", chunk("lpf", split=True))
