@@ -74,20 +74,6 @@ __device__ __forceinline__ f2 convert_raw(uint32_t v) {
     return r;
 }
 
-// The sample in the upper 16 bits of a word holding two 8-bit-format samples (CS8/CU8)
-template <int FMT>
-__device__ __forceinline__ f2 convert_raw_hi(uint32_t v) {
-    f2 r;
-    if constexpr (FMT == SDRG_IQ_CS8) {
-        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(r.x) : "v"(v));
-        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3" : "=v"(r.y) : "v"(v));
-    } else {
-        static_assert(FMT == SDRG_IQ_CU8, "8-bit formats only");
-        r = f2{(float)((v >> 16) & 0xffu), (float)(v >> 24)} - f2{127.4f, 127.4f};
-    }
-    return r;
-}
-
 // buffer resource over one frame: per-lane offset in a VGPR, per-element offset as a scalar
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const void *base, int bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
@@ -328,10 +314,6 @@ namespace k16 {
 #define SDRG_K16_ABLATE 0
 #endif
 constexpr int ABL = SDRG_K16_ABLATE;
-// next frame's raw samples issued right after this frame's convert (1) instead of before its stores (0)
-#ifndef SDRG_K16_EARLY
-#define SDRG_K16_EARLY 0
-#endif
 
 constexpr int LOG2N = 14, N = 1 << LOG2N, T = N / E, HALF = N / 2;
 constexpr int XCH_F2 = HALF;              // half-frame exchange buffer, f2 slots (XOR-swizzled, no padding)
@@ -413,21 +395,6 @@ __device__ __forceinline__ void issue_raw(const void *iq, int f, int t, uint32_t
     for (int r = 0; r < E; ++r) raw[r] = load_raw_word<FMT>(rs, t * BPS, r * (N / 32) * BPS);
 }
 
-// 8-bit formats: samples x[t + 512 r] of frame f two per register (r = 2q in the low half, 2q + 1 in the high
-// half, loaded with d16 / d16_hi), so the next frame's samples take 16 VGPRs and can be in flight for a whole frame
-typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-template <int FMT>
-__device__ __forceinline__ void issue_raw_packed(const void *iq, int f, int t, uint32_t (&raw)[E / 2]) {
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(reinterpret_cast<const char *>(iq) + (size_t)f * N * 2, N * 2);
-#pragma unroll
-    for (int q = 0; q < E / 2; ++q) {
-        us2 w;
-        w.x = __builtin_amdgcn_raw_buffer_load_b16(rs, t * 2, (2 * q) * (N / 32) * 2, 0);
-        w.y = __builtin_amdgcn_raw_buffer_load_b16(rs, t * 2, (2 * q + 1) * (N / 32) * 2, 0);
-        raw[q] = __builtin_bit_cast(uint32_t, w);
-    }
-}
-
 // __launch_bounds__(512, 4): four waves per SIMD = two workgroups per CU, so at most 128 VGPRs
 template <int FMT>
 __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restrict__ iq, float *__restrict__ spectra,
@@ -444,26 +411,15 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
     constexpr float S = power_scale<FMT>();
     const f2 *p1_row = p1 + (t & 31);  // pass 1: P1[r][k], k = t mod 32
 
-    constexpr bool EARLY = SDRG_K16_EARLY == 1 && BPS == 2;
-    constexpr bool EARLY32 = SDRG_K16_EARLY == 2 && BPS == 2;  // lab: unpacked raw issued early (spills)  // 8-bit formats: next frame issued a whole frame ahead
-    constexpr bool STAGE = FMT != SDRG_IQ_CF32 && !EARLY;  // CF32 (8 B/sample) loads at the top of the iteration
+    constexpr bool STAGE = FMT != SDRG_IQ_CF32;  // CF32 (8 B/sample) loads at the top of the iteration
     uint32_t raw[E];
-    uint32_t rawp[E / 2];
     if constexpr (STAGE)
         if ((int)blockIdx.x < n_frames) issue_raw<FMT>(iq, blockIdx.x, t, raw);
-    if constexpr (EARLY)
-        if ((int)blockIdx.x < n_frames) issue_raw_packed<FMT>(iq, blockIdx.x, t, rawp);
 
     for (int frame = blockIdx.x; frame < n_frames; frame += gridDim.x) {
         f2 v[E];
         // ---- pass 0: radix 32 over x[t + 512 r] (no twiddles) ----
-        if constexpr (EARLY) {
-#pragma unroll
-            for (int q = 0; q < E / 2; ++q) {
-                v[2 * q] = convert_raw<FMT>(rawp[q]);
-                v[2 * q + 1] = convert_raw_hi<FMT>(rawp[q]);
-            }
-        } else if constexpr (STAGE) {
+        if constexpr (STAGE) {
 #pragma unroll
             for (int r = 0; r < E; ++r) v[r] = convert_raw<FMT>(raw[r]);
         } else {
@@ -472,12 +428,6 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
             for (int r = 0; r < E; ++r) v[r] = load_unscaled<FMT>(rs, t * BPS, r * (N / 32) * BPS);
         }
         const int next = frame + gridDim.x;
-        if constexpr (EARLY) {
-            if (next < n_frames) issue_raw_packed<FMT>(iq, next, t, rawp);
-        }
-        if constexpr (EARLY32) {
-            if (next < n_frames) issue_raw<FMT>(iq, next, t, raw);
-        }
         if constexpr (!(ABL & 8)) dft<32>(v);
         if constexpr (!(ABL & 4)) exch1(xch, v);
         // ---- pass 1: radix 32, NS = 32 ----
@@ -519,7 +469,7 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
 #pragma unroll
         for (int r = 0; r < 16; ++r)
             pw[r] = f2s{(x0[r].x * x0[r].x + x0[r].y * x0[r].y) * S, (x1[r].x * x1[r].x + x1[r].y * x1[r].y) * S};
-        if constexpr (STAGE && !EARLY32) {
+        if constexpr (STAGE) {
             if (next < n_frames) {
                 issue_raw<FMT>(iq, next, t, raw);
             } else {  // last frame: define raw on this path too, so it is dead between the convert and here
