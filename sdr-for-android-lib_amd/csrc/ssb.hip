@@ -350,8 +350,16 @@ constexpr int MAX_DONE = 8;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
 
 constexpr int TAPS_ROW = CH + 256 + CH + 4;
+// The low-pass wave one chunk behind the DC wave's output (1): its input ring gets a third slot and the wave runs
+// its whole loop as one asm block that reads the next chunk's first sub-blocks before each barrier (csrc/ssb_lpf_asm.h);
+// every later role moves one iteration later.  The raw-IQ batches shrink to 256 B x 3 to keep the LDS budget.
+#ifndef SDRG_LPF_LOOKAHEAD
+#define SDRG_LPF_LOOKAHEAD 1
+#endif
+constexpr int LA = SDRG_LPF_LOOKAHEAD ? 1 : 0;
+constexpr int NA = 2 + LA;  // slots of the DC -> low-pass ring
 #ifndef SDRG_PIPE_RAWB  // bytes of raw IQ per stream per prefetch batch
-#define SDRG_PIPE_RAWB 512
+#define SDRG_PIPE_RAWB (SDRG_LPF_LOOKAHEAD ? 256 : 512)
 #endif
 constexpr int RAWB = SDRG_PIPE_RAWB;
 constexpr int RAW_PIECES = RAWB / 64;     // 16-B LDS-DMA pieces per loader lane (lane = 4 x stream + quarter)
@@ -362,8 +370,8 @@ constexpr int batch_chunks() {  // chunks per RAWB-per-stream prefetch batch (DM
     constexpr int b = RAWB / (CH * (FMT == SDRG_IQ_CF32 ? 8 : FMT == SDRG_IQ_CS16 ? 4 : 2));
     return b > 0 ? b : 1;
 }
-#ifndef SDRG_PIPE_NRAW  // 2: one batch unpacked, one in flight (3 needs 8 KiB more LDS than co-residency allows)
-#define SDRG_PIPE_NRAW 2
+#ifndef SDRG_PIPE_NRAW  // 512 B: 2 (one batch unpacked, one in flight; 3 needs 8 KiB more LDS than co-residency allows)
+#define SDRG_PIPE_NRAW (SDRG_LPF_LOOKAHEAD ? 3 : 2)
 #endif
 // Co-residency with the spectrum kernel (measured +4-5 % per step, tools/gpu_cores.sh): the pipeline keeps to
 // 80 VGPRs (6 waves per SIMD's worth; 3 x 80 + 2 x 128 <= 512) and 84.5 KiB of LDS (+ 74.3 KiB <= 160 KiB), so
@@ -381,7 +389,7 @@ constexpr int NRAW = SDRG_PIPE_NRAW;  // raw-IQ batches in LDS: one being unpack
 struct PipeLds {
     uint4 raw[NRAW][RAW_U4];  // raw IQ bytes of the prefetch batches (LDS-DMA), [piece][loader lane]
     float re[2][BUFF];
-    float a[2][BUFF];
+    float a[NA][BUFF];
     float y[4][BUFF];
     float d[2][BUFF];
     float g[2][BUFF];
@@ -587,7 +595,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     // the register allocator sees one role per loop and the kernel's VGPR count is the largest role's,
     // not the sum of every role's loop-invariant values.
     auto chunk_loop = [&](auto &&body) {
-        for (int it = 0; it < nch + 8; ++it) {
+        for (int it = 0; it < nch + 8 + LA; ++it) {
             if (stamps) st_a = __builtin_amdgcn_s_memtime();
             body(it);
             if (stamps) {
@@ -610,13 +618,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             if (SDRG_DC_ASM && !(SDRG_SERIAL_FULL_EXEC & 1) && c >= 0 && c < nch && lane < PG) {
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 const f2v om2 = {one_minus, one_minus}, a02 = {a0, a0};
-                const uint32_t src = lds_addr(&L.re[c & 1][my_s * ROW]), dst = lds_addr(&L.a[c & 1][my_s * ROW]);
+                const uint32_t src = lds_addr(&L.re[c & 1][my_s * ROW]), dst = lds_addr(&L.a[c % NA][my_s * ROW]);
                 asm volatile(SDRG_DC_CHUNK_ASM
                              : [dc] "+v"(dc)
                              : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
                              : SDRG_CHUNK_CLOBBERS, "memory");
             } else if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 1) || lane < PG)) {
-                row_pipeline(&L.re[c & 1][my_s * ROW], &L.a[c & 1][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
+                row_pipeline(&L.re[c & 1][my_s * ROW], &L.a[c % NA][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                     for (int q = 0; q < SB; q++) {
                         dc = alpha * dc + one_minus * v[q];
@@ -635,9 +643,24 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         // lane of v_pk_mul_f32 rounds like v_mul_f32), the adds in order; the subtractions are additions of
         // (-b) z (a - b == a + (-b) exactly, and (-b) z == -(b z))
         const f2v c1 = {p.lpf[1], -p.lpf[3]}, c2 = {p.lpf[2], -p.lpf[4]};
-        chunk_loop([&](int it) {
+        static_assert(BUFF * 4 == SDRG_LPF_LOOP_SLOT_BYTES, "ring slot stride of the generated loop");
+        if (LA && SDRG_LPF_ASM == 1 && !(SDRG_SERIAL_FULL_EXEC & 2) && S % CH == 0) {
+            // the whole loop as one block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py): nch + 8 + LA iterations
+            // with one s_barrier each, the same count as every other role's chunk_loop
+            f2v z = {z1, z2};
+            const uint32_t abase = lds_addr(&L.a[0][my_s * ROW]), ybase = lds_addr(&L.y[0][my_s * ROW]);
+            const int nit = nch + 8 + LA;
+            unsigned long long sv;
+            int t_it, t_cc, t_r, t_yo;
+            asm volatile(SDRG_LPF_LOOP_ASM
+                         : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                         : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
+                         : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+            z1 = z.x;
+            z2 = z.y;
+        } else chunk_loop([&](int it) {
             // ---- iir2Process recurrence (:75-84), chunk it-2 ----
-            const int c = it - 2;
+            const int c = it - 2 - LA;
             if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 2) || lane < PG)) {
                 const int lim = min(CH, S - c * CH);
 #ifdef SDRG_DIAG_LPF_NOLDS  // diagnostic build only: the recurrence on register data, no LDS traffic
@@ -657,8 +680,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 if (lim == CH && SDRG_LPF_ASM && !(SDRG_SERIAL_FULL_EXEC & 2)) {
                     // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                     f2v z = {z1, z2};
-                    const uint32_t src = lds_addr(&L.a[c & 1][my_s * ROW]), dst = lds_addr(&L.y[c & 3][my_s * ROW]);
-                    if (SDRG_LPF_ASM == 2) {  // VALU on all 64 lanes, LDS on the 16 stream lanes
+                    const uint32_t src = lds_addr(&L.a[c % NA][my_s * ROW]), dst = lds_addr(&L.y[c & 3][my_s * ROW]);
+                    if (SDRG_LPF_ASM == 3) {  // lab: the chain on register data, no LDS (wrong results)
+                        asm volatile(SDRG_LPF_CHUNK_NOLDS_ASM
+                                     : [z] "+v"(z)
+                                     : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
+                                     : SDRG_CHUNK_CLOBBERS, "memory");
+                    } else if (SDRG_LPF_ASM == 4) {  // lab: as 3 on all 64 lanes
+                        unsigned long long sv;
+                        asm volatile(SDRG_LPF_CHUNK_NOLDS_SPLIT_ASM
+                                     : [z] "+v"(z), [sv] "=&s"(sv)
+                                     : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
+                                     : SDRG_CHUNK_CLOBBERS, "memory");
+                    } else if (SDRG_LPF_ASM == 2) {  // VALU on all 64 lanes, LDS on the 16 stream lanes
                         unsigned long long sv;
                         asm volatile(SDRG_LPF_CHUNK_SPLIT_ASM
                                      : [z] "+v"(z), [sv] "=&s"(sv)
@@ -673,7 +707,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                     z1 = z.x;
                     z2 = z.y;
                 } else if (lim == CH) {
-                    row_pipeline(&L.a[c & 1][my_s * ROW], &L.y[c & 3][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
+                    row_pipeline(&L.a[c % NA][my_s * ROW], &L.y[c & 3][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                         for (int q = 0; q < SB; q++) {
                             const f2v p1 = c1 * z1, p2 = c2 * z2;
@@ -688,7 +722,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                     // so the carried state is the one after exactly S samples
                     for (int q = 0; q < lim; q++) {
                         const f2v p1 = c1 * z1, p2 = c2 * z2;
-                        const float y = (((L.a[c & 1][my_s * ROW + q] + p1.x) + p2.x) + p1.y) + p2.y;
+                        const float y = (((L.a[c % NA][my_s * ROW + q] + p1.x) + p2.x) + p1.y) + p2.y;
                         z2 = z1;
                         z1 = y;
                         if (lane < PG) L.y[c & 3][my_s * ROW + q] = y;
@@ -709,7 +743,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         const f2v keep = {1.0f - p.agc_fast, 1.0f - 0.00035f};
         chunk_loop([&](int it) {
             // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
-            const int c = it - 4;
+            const int c = it - 4 - LA;
             if (SDRG_AGC_ASM && !(SDRG_SERIAL_FULL_EXEC & 4) && c >= 0 && c < nch && lane < PG) {
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 f2v g = {gain, gain};
@@ -811,7 +845,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         chunk_loop([&](int it) {
             // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot mod 4, stream); slot groups
             //      4j..4j+3 split between the two FIR waves ----
-            const int c = it - 6;
+            const int c = it - 6 - LA;
             if (c >= 0 && c < nch && PL > 0) {
                 const int4 r = chunk_out[c];  // outputs overlapping chunk c: [r.x, r.y] (host table, no division)
                 const int sl = lane % PG, sub = lane / PG;
@@ -833,7 +867,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             // lane = 4 x stream + part of 8 samples.  x = demodSSB(y, y) = y + y (upper) or y - y (lower)
             // is y * 2 or y * 0: equal values (the lower sideband's zero may carry y's sign, which the
             // clamp keeps and the FIR's sums absorb: acc + (+-0) == acc).  clamp == med3 for non-NaN input.
-            const int c = it - 5;
+            const int c = it - 5 - LA;
             if (c >= 0 && c < nch) {
 #pragma unroll
                 for (int g8 = 0; g8 < CH / 32; ++g8) {
@@ -878,7 +912,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         int np = 0;
         chunk_loop([&](int it) {
             // ---- HP -> BP -> transientBoost -> floatToPCM on the outputs the FIR completed, chunk it-7 ----
-            const int ce = it - 7;
+            const int ce = it - 7 - LA;
             if (ce >= 0 && ce < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
                 const int c = ce;
                 const int4 r = chunk_out[c];  // outputs completed in chunk c: [r.z, r.w]
@@ -917,7 +951,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             const int hl = (wave == W_DES0 ? 0 : wave == W_DES1 ? 1 : wave == W_DES2 ? 2 : 3) * 64 + lane;
             const int sl = hl / (CH / SPL), i0 = (hl % (CH / SPL)) * SPL;
             // ---- AGC "desired" level (:104-107), chunk it-3 ----
-            const int c = it - 3;
+            const int c = it - 3 - LA;
             if (c >= 0 && c < nch) {
 #pragma unroll
                 for (int h = 0; h < SPL; h += 2) {

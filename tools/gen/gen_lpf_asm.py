@@ -94,7 +94,7 @@ def chunk(role, lds=True, split=False):
         return ([f"s_mov_b64 exec, %[sv]"] + ops + ["s_mov_b64 exec, -1"]) if (split and ops) else ops
 
     if split:
-        out += ["s_mov_b64 %[sv], exec"]
+        out += ["s_mov_b64 %[sv], exec"] + ([] if lds else ["s_mov_b64 exec, -1"])
     buf = [BUFS[sb % 3] for sb in range(4)]
     if lds:
         out += exec_lds(reads(0, buf[0]) + reads(1, buf[1]))
@@ -137,6 +137,103 @@ def chunk(role, lds=True, split=False):
     return out
 
 
+SLOT = 16 * 68 * 4  # bytes per [stream][sample] chunk buffer (PG x ROW floats)
+
+
+def lpf_loop():
+    """The low-pass wave's whole chunk loop (SDRG_LPF_LOOKAHEAD): one s_barrier per iteration, like every other
+    role's loop, and chunk c = it - 3 (one iteration behind the DC wave's output, through a 3-slot ring), so the
+    next chunk's input is complete while this chunk runs: its first two sub-blocks are read before the barrier
+    and stay in flight across it (the barrier waits only for this chunk's output writes).  Sub-block j of chunk
+    c lives in buffer (c + j) mod 3; three copies of the chunk body, one per c mod 3.
+    Operands: %[z] (+v {z1, z2}), %[abase] / %[ybase] (v: LDS byte address of slot 0 of the input / output ring
+    at this stream's row), %[c1], %[c2] (s), %[nit] (s: iterations), %[nch] (s: chunks, all full), temps %[sv]
+    (=&s 64-bit), %[it], %[cc], %[r], %[yo] (=&s); clobbers v0-v54, vcc-free."""
+    out = []
+    u = "%="
+    out += [
+        "s_mov_b64 %[sv], exec",
+        "s_mov_b64 exec, 0xffff",          # the 16 stream lanes
+        "s_nop 4",
+        f"v_pk_mov_b32 v[46:47], %[z], %[z] op_sel:[1,0]",   # chunk -1's sb3 buffer (2): v47 = z1, v46 = z2
+        f"v_pk_mov_b32 v[52:53], %[z], %[z] op_sel:[0,1]",   # the carried {z1, z2} if no chunk runs
+        "s_mov_b32 %[it], 0",
+        "s_mov_b32 %[cc], -3",
+        "s_mov_b32 %[r], 0",               # c mod 3 once c >= 0
+        f"L_top_{u}:",
+        "s_cmp_lt_i32 %[cc], 0",
+        f"s_cbranch_scc1 L_pre_{u}",
+        "s_cmp_ge_i32 %[cc], %[nch]",
+        f"s_cbranch_scc1 L_drain_{u}",
+        # output slot c mod 4
+        "s_and_b32 %[yo], %[cc], 3",
+        f"s_mul_i32 %[yo], %[yo], {SLOT}",
+        "v_add_u32 v54, %[yo], %[ybase]",
+        "s_cmp_eq_u32 %[r], 0",
+        f"s_cbranch_scc1 L_r0_{u}",
+        "s_cmp_eq_u32 %[r], 1",
+        f"s_cbranch_scc1 L_r1_{u}",
+        f"s_branch L_r2_{u}",
+    ]
+    for r in range(3):
+        out.append(f"L_r{r}_{u}:")
+        bufs = [BUFS[(r + j) % 3] for j in range(4)]
+        zb = BUFS[(r + 2) % 3]
+        prev1, prev2 = pair(zb + 15), pair(zb + 14)
+        rd = lambda sb, buf, slot: [f"ds_read_b128 v[{buf + 4 * i}:{buf + 4 * i + 3}], %[abase] offset:{slot * SLOT + (16 * sb + 4 * i) * 4}" for i in range(4)]
+        wr = lambda sb, buf: [f"ds_write_b128 v54, v[{buf + 4 * i}:{buf + 4 * i + 3}] offset:{(16 * sb + 4 * i) * 4}" for i in range(4)]
+        waits = {0: 4, 1: 8, 2: 8, 3: 4}
+        for sb in range(4):
+            out.append(f"s_waitcnt lgkmcnt({waits[sb]})")
+            b = bufs[sb]
+            for q in range(16):
+                out += lpf_sample(b + q, prev1, prev2)
+                prev2, prev1 = prev1, pair(b + q)
+            out += wr(sb, b)
+            if sb + 2 < 4:
+                out += rd(sb + 2, bufs[sb + 2], r)
+        last = bufs[3] + 15
+        out.append(f"v_pk_mov_b32 v[52:53], v[{last - 1}:{last}], v[{last - 1}:{last}] op_sel:[1,0]")
+        # prefetch the next chunk's sub-blocks 0 and 1 (slot (r + 1) mod 3, buffers (r + 1), (r + 2) mod 3)
+        out += ["s_add_u32 %[yo], %[cc], 1", "s_cmp_ge_i32 %[yo], %[nch]", f"s_cbranch_scc1 L_drain_{u}"]
+        nr = (r + 1) % 3
+        out += rd(0, BUFS[nr], nr) + rd(1, BUFS[(nr + 1) % 3], nr)
+        out.append(f"s_branch L_bar8_{u}")
+    out += [
+        f"L_pre_{u}:",                      # c < 0: chunk 0's sub-blocks 0, 1 once c == -1 (chunk 0 is complete)
+        "s_cmp_lg_i32 %[cc], -1",
+        f"s_cbranch_scc1 L_drain_{u}",
+        "s_cmp_le_i32 %[nch], 0",
+        f"s_cbranch_scc1 L_drain_{u}",
+    ]
+    out += [f"ds_read_b128 v[{BUFS[0] + 4 * i}:{BUFS[0] + 4 * i + 3}], %[abase] offset:{(4 * i) * 4}" for i in range(4)]
+    out += [f"ds_read_b128 v[{BUFS[1] + 4 * i}:{BUFS[1] + 4 * i + 3}], %[abase] offset:{(16 + 4 * i) * 4}" for i in range(4)]
+    out += [
+        f"L_bar8_{u}:",
+        "s_waitcnt lgkmcnt(8)",            # this chunk's output writes done; the 8 prefetch reads may fly on
+        f"s_branch L_bar_{u}",
+        f"L_drain_{u}:",
+        "s_waitcnt lgkmcnt(0)",
+        f"L_bar_{u}:",
+        "s_barrier",
+        # next iteration: it + 1, c + 1, r = c mod 3 (for c >= 0)
+        "s_add_u32 %[it], %[it], 1",
+        "s_add_i32 %[cc], %[cc], 1",
+        "s_cmp_le_i32 %[cc], 0",
+        f"s_cbranch_scc1 L_next_{u}",      # c <= 0 after the increment: r stays 0
+        "s_add_u32 %[r], %[r], 1",
+        "s_cmp_eq_u32 %[r], 3",
+        "s_cselect_b32 %[r], 0, %[r]",
+        f"L_next_{u}:",
+        "s_cmp_lt_u32 %[it], %[nit]",
+        f"s_cbranch_scc1 L_top_{u}",
+        "s_mov_b64 exec, %[sv]",
+        "s_nop 4",
+        "v_pk_mov_b32 %[z], v[52:53], v[52:53] op_sel:[0,1]",
+    ]
+    return out
+
+
 def emit(name, lines):
     print(f"#define {name} \\")
     for l in lines:
@@ -155,16 +252,21 @@ def main():
     emit("SDRG_LPF_CHUNK_ASM", chunk("lpf"))
     emit("SDRG_AGC_CHUNK_ASM", chunk("agc"))
     emit("SDRG_DC_CHUNK_ASM", chunk("dc"))
+    print("// the low-pass wave's whole loop with a one-chunk lookahead (SDRG_LPF_LOOKAHEAD; see lpf_loop() in the generator)")
+    emit("SDRG_LPF_LOOP_ASM", lpf_loop())
     print("// the low-pass chunk with its VALU on all 64 lanes and the LDS operations on the caller's lanes; extra operand")
     print("// %[sv] (=&s, 64-bit): the caller's EXEC (lab option SDRG_LPF_ASM=2)")
     emit("SDRG_LPF_CHUNK_SPLIT_ASM", chunk("lpf", split=True))
-    print("// lab only (tools/microbench/valu6.hip): the low-pass chunk on register data, no LDS operations")
+    print("// lab only (tools/microbench/valu6.hip, SDRG_LPF_ASM=3 / 4): the low-pass chunk on register data, no LDS")
+    print("// operations (wrong results), on the caller's lanes / on all 64 lanes (extra operand %[sv] as above)")
     emit("SDRG_LPF_CHUNK_NOLDS_ASM", chunk("lpf", lds=False))
+    emit("SDRG_LPF_CHUNK_NOLDS_SPLIT_ASM", chunk("lpf", lds=False, split=True))
     print("#define SDRG_CHUNK_CLOBBERS \\")
     regs = [f'"v{i}"' for i in range(T0 + 2)]
     for i in range(0, len(regs), 16):
         print("    " + ", ".join(regs[i:i + 16]) + (", \\" if i + 16 < len(regs) else ""))
     print("#define SDRG_LPF_CHUNK_CLOBBERS SDRG_CHUNK_CLOBBERS")
+    print(f"#define SDRG_LPF_LOOP_SLOT_BYTES {SLOT}")
 
 
 if __name__ == "__main__":
