@@ -455,6 +455,18 @@ def main() -> int:
             "ssb_ms_alone": round(ssb_iso_ms, 4), "frac_alone": round(floor_ms / ssb_iso_ms, 4),
             "ssb_ms_coresident": round(ts["ssb_ms"], 4),
             "frac_coresident": round(floor_ms / ts["ssb_ms"], 4) if ts["ssb_ms"] > 0 else None}
+        # the same kernel against HBM: the step's longest kernel by GPU time, and latency-bound (the floor above)
+        ssb_bytes = streams * n * in_bps + streams * 2 * plen
+        ssb_traffic = pmc_traffic("ssb_pipe_kernel", streams)
+        if ts["ssb_ms"] > 0:
+            ssb_gbs = ssb_bytes / (ts["ssb_ms"] * 1e-3) / 1e9
+            out["roofline_ssb"] = {
+                "kernel": "ssb_pipe_kernel", "bound": "hbm", "achieved": round(ssb_gbs, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ssb_gbs / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": ssb_bytes,
+                "traffic": ssb_traffic[0] if ssb_traffic else None,
+                "traffic_source": ssb_traffic[1] if ssb_traffic else None,
+                "note": "the longest kernel by GPU time, measured co-resident in the timed region; it is bound by the "
+                        "sample-serial recurrences (ssb_latency_floor), not by HBM: IQ in (I used) + PCM out"}
     if labelled:
         out["labelled"] = labelled
     if rehearse:
