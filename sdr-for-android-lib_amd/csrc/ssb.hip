@@ -304,7 +304,7 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 // go to the EQ role (HP, BP, boost, PCM).  All arithmetic is the reference's, in its order, without
 // contraction: bit-identical PCM.
 //
-// Workgroup = 16 streams x 12 waves, one workgroup per CU (84.5 KiB of LDS: two never fit), beside one spectrum workgroup.  A wave issues
+// Workgroup = 16 streams x 12 waves, one workgroup per CU (84.8 KiB of LDS: two never fit), beside one spectrum workgroup.  A wave issues
 // at most about one VALU instruction per ~10 cycles however idle its SIMD is, while a SIMD serves several
 // waves at that rate (tools/microbench/valu2.hip), so the order-free work is spread over as many waves as
 // keep the heaviest helper's instruction count below the low-pass wave's.  The roles are dealt to the
@@ -374,7 +374,7 @@ constexpr int batch_chunks() {  // chunks per RAWB-per-stream prefetch batch (DM
 #define SDRG_PIPE_NRAW (SDRG_LPF_LOOKAHEAD ? 3 : 2)
 #endif
 // Co-residency with the spectrum kernel (measured +4-5 % per step, tools/gpu_cores.sh): the pipeline keeps to
-// 80 VGPRs (6 waves per SIMD's worth; 3 x 80 + 2 x 128 <= 512) and 84.5 KiB of LDS (+ 74.3 KiB <= 160 KiB), so
+// 80 VGPRs (6 waves per SIMD's worth; 3 x 80 + 2 x 128 <= 512) and 84.8 KiB of LDS (+ 72.3 KiB <= 160 KiB), so
 // one 512-thread spectrum workgroup fits beside it on every CU and the next call's spectrum runs while this
 // call's latency-bound SSB pipeline holds the CUs.  The LDS is dynamic so that the compiler's occupancy model
 // (which otherwise clamps waves-per-EU to what the static LDS allows) honours the 80-VGPR budget.
