@@ -357,6 +357,11 @@ constexpr int TAPS_ROW = CH + 256 + CH + 4;
 #define SDRG_LPF_LOOKAHEAD 1
 #endif
 constexpr int LA = SDRG_LPF_LOOKAHEAD ? 1 : 0;
+// with the lookahead: the loop's LDS reads and writes interleaved quad by quad with the chain (1) or grouped per
+// sub-block (0)
+#ifndef SDRG_LPF_INTERLEAVE
+#define SDRG_LPF_INTERLEAVE 1
+#endif
 constexpr int NA = 2 + LA;  // slots of the DC -> low-pass ring
 #ifndef SDRG_PIPE_RAWB  // bytes of raw IQ per stream per prefetch batch
 #define SDRG_PIPE_RAWB (SDRG_LPF_LOOKAHEAD ? 256 : 512)
@@ -652,10 +657,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             const int nit = nch + 8 + LA;
             unsigned long long sv;
             int t_it, t_cc, t_r, t_yo;
-            asm volatile(SDRG_LPF_LOOP_ASM
-                         : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
-                         : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
-                         : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+            if (SDRG_LPF_INTERLEAVE)
+                asm volatile(SDRG_LPF_LOOP_IL_ASM
+                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
+                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+            else
+                asm volatile(SDRG_LPF_LOOP_ASM
+                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
+                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
             z1 = z.x;
             z2 = z.y;
         } else chunk_loop([&](int it) {

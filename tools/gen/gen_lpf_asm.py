@@ -234,6 +234,93 @@ def lpf_loop():
     return out
 
 
+def lpf_loop_interleaved():
+    """lpf_loop() with the LDS traffic spread through the VALU stream: sub-blocks are numbered g = 4c + sb across
+    chunks and live in buffer g mod 3; while sub-block g runs, after each 4-sample quad t its output quad is written
+    and quad t of sub-block g + 2 is read (for sb = 2, 3 that is the next chunk's sub-block 0, 1, complete in its
+    ring slot).  So at the barrier only the chunk's last write is outstanding (lgkmcnt(1)), and the first two
+    sub-blocks of the next chunk are already in registers.  The last chunk's reads of a next chunk fetch a stale
+    ring slot and are never used; the block drains them (lgkmcnt(0)) before it ends."""
+    out = []
+    u = "%="
+    out += [
+        "s_mov_b64 %[sv], exec",
+        "s_mov_b64 exec, 0xffff",
+        "s_nop 4",
+        "v_pk_mov_b32 v[46:47], %[z], %[z] op_sel:[1,0]",
+        "v_pk_mov_b32 v[52:53], %[z], %[z] op_sel:[0,1]",
+        "s_mov_b32 %[it], 0",
+        "s_mov_b32 %[cc], -3",
+        "s_mov_b32 %[r], 0",
+        f"L_top_{u}:",
+        "s_cmp_lt_i32 %[cc], 0",
+        f"s_cbranch_scc1 L_pre_{u}",
+        "s_cmp_ge_i32 %[cc], %[nch]",
+        f"s_cbranch_scc1 L_drain_{u}",
+        "s_and_b32 %[yo], %[cc], 3",
+        f"s_mul_i32 %[yo], %[yo], {SLOT}",
+        "v_add_u32 v54, %[yo], %[ybase]",
+        "s_cmp_eq_u32 %[r], 0",
+        f"s_cbranch_scc1 L_r0_{u}",
+        "s_cmp_eq_u32 %[r], 1",
+        f"s_cbranch_scc1 L_r1_{u}",
+        f"s_branch L_r2_{u}",
+    ]
+    for r in range(3):
+        out.append(f"L_r{r}_{u}:")
+        zb = BUFS[(r + 2) % 3]
+        prev1, prev2 = pair(zb + 15), pair(zb + 14)
+        for sb in range(4):
+            out.append(f"s_waitcnt lgkmcnt({4 if sb == 0 else 8})")
+            b = BUFS[(r + sb) % 3]
+            rb = BUFS[(r + sb + 2) % 3]                      # buffer of sub-block g + 2
+            rslot, rsb = (r, sb + 2) if sb < 2 else ((r + 1) % 3, sb - 2)
+            for q in range(16):
+                out += lpf_sample(b + q, prev1, prev2)
+                prev2, prev1 = prev1, pair(b + q)
+                if q % 4 == 3:
+                    t = q // 4
+                    out.append(f"ds_write_b128 v54, v[{b + 4 * t}:{b + 4 * t + 3}] offset:{(16 * sb + 4 * t) * 4}")
+                    out.append(f"ds_read_b128 v[{rb + 4 * t}:{rb + 4 * t + 3}], %[abase] offset:{rslot * SLOT + (16 * rsb + 4 * t) * 4}")
+        last = BUFS[(r + 3) % 3] + 15
+        out.append(f"v_pk_mov_b32 v[52:53], v[{last - 1}:{last}], v[{last - 1}:{last}] op_sel:[1,0]")
+        out.append(f"s_branch L_bar1_{u}")
+    out += [
+        f"L_pre_{u}:",                      # c < 0: chunk 0's sub-blocks 0, 1 once c == -1 (chunk 0 is complete)
+        "s_cmp_lg_i32 %[cc], -1",
+        f"s_cbranch_scc1 L_drain_{u}",
+        "s_cmp_le_i32 %[nch], 0",
+        f"s_cbranch_scc1 L_drain_{u}",
+    ]
+    out += [f"ds_read_b128 v[{BUFS[0] + 4 * i}:{BUFS[0] + 4 * i + 3}], %[abase] offset:{(4 * i) * 4}" for i in range(4)]
+    out += [f"ds_read_b128 v[{BUFS[1] + 4 * i}:{BUFS[1] + 4 * i + 3}], %[abase] offset:{(16 + 4 * i) * 4}" for i in range(4)]
+    out += [
+        f"s_branch L_bar_{u}",
+        f"L_bar1_{u}:",
+        "s_waitcnt lgkmcnt(1)",            # this chunk's writes done; the last read of the next chunk may fly on
+        f"s_branch L_bar_{u}",
+        f"L_drain_{u}:",
+        "s_waitcnt lgkmcnt(0)",
+        f"L_bar_{u}:",
+        "s_barrier",
+        "s_add_u32 %[it], %[it], 1",
+        "s_add_i32 %[cc], %[cc], 1",
+        "s_cmp_le_i32 %[cc], 0",
+        f"s_cbranch_scc1 L_next_{u}",
+        "s_add_u32 %[r], %[r], 1",
+        "s_cmp_eq_u32 %[r], 3",
+        "s_cselect_b32 %[r], 0, %[r]",
+        f"L_next_{u}:",
+        "s_cmp_lt_u32 %[it], %[nit]",
+        f"s_cbranch_scc1 L_top_{u}",
+        "s_waitcnt lgkmcnt(0)",            # the last chunk's reads of a next chunk that does not exist
+        "s_mov_b64 exec, %[sv]",
+        "s_nop 4",
+        "v_pk_mov_b32 %[z], v[52:53], v[52:53] op_sel:[0,1]",
+    ]
+    return out
+
+
 def emit(name, lines):
     print(f"#define {name} \\")
     for l in lines:
@@ -254,6 +341,8 @@ def main():
     emit("SDRG_DC_CHUNK_ASM", chunk("dc"))
     print("// the low-pass wave's whole loop with a one-chunk lookahead (SDRG_LPF_LOOKAHEAD; see lpf_loop() in the generator)")
     emit("SDRG_LPF_LOOP_ASM", lpf_loop())
+    print("// the same loop with the chunk's LDS reads and writes interleaved quad by quad (SDRG_LPF_INTERLEAVE)")
+    emit("SDRG_LPF_LOOP_IL_ASM", lpf_loop_interleaved())
     print("// the low-pass chunk with its VALU on all 64 lanes and the LDS operations on the caller's lanes; extra operand")
     print("// %[sv] (=&s, 64-bit): the caller's EXEC (lab option SDRG_LPF_ASM=2)")
     emit("SDRG_LPF_CHUNK_SPLIT_ASM", chunk("lpf", split=True))
