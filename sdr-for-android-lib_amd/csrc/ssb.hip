@@ -624,10 +624,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 const f2v om2 = {one_minus, one_minus}, a02 = {a0, a0};
                 const uint32_t src = lds_addr(&L.re[c & 1][my_s * ROW]), dst = lds_addr(&L.a[c % NA][my_s * ROW]);
-                asm volatile(SDRG_DC_CHUNK_ASM
-                             : [dc] "+v"(dc)
-                             : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
-                             : SDRG_CHUNK_CLOBBERS, "memory");
+                if (SDRG_DC_ASM == 2)
+                    asm volatile(SDRG_DC_CHUNK_IL_ASM
+                                 : [dc] "+v"(dc)
+                                 : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
+                                 : SDRG_CHUNK_CLOBBERS, "memory");
+                else
+                    asm volatile(SDRG_DC_CHUNK_ASM
+                                 : [dc] "+v"(dc)
+                                 : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
+                                 : SDRG_CHUNK_CLOBBERS, "memory");
             } else if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 1) || lane < PG)) {
                 row_pipeline(&L.re[c & 1][my_s * ROW], &L.a[c % NA][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
@@ -759,10 +765,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 f2v g = {gain, gain};
                 const uint32_t src = lds_addr(&L.d[c & 1][my_s * ROW]), dst = lds_addr(&L.g[c & 1][my_s * ROW]);
-                asm volatile(SDRG_AGC_CHUNK_ASM
-                             : [g] "+v"(g)
-                             : [src] "v"(src), [dst] "v"(dst), [keep] "s"(keep), [rates] "s"(rates)
-                             : SDRG_CHUNK_CLOBBERS, "vcc", "memory");
+                if (SDRG_AGC_ASM == 2)
+                    asm volatile(SDRG_AGC_CHUNK_IL_ASM
+                                 : [g] "+v"(g)
+                                 : [src] "v"(src), [dst] "v"(dst), [keep] "s"(keep), [rates] "s"(rates)
+                                 : SDRG_CHUNK_CLOBBERS, "vcc", "memory");
+                else
+                    asm volatile(SDRG_AGC_CHUNK_ASM
+                                 : [g] "+v"(g)
+                                 : [src] "v"(src), [dst] "v"(dst), [keep] "s"(keep), [rates] "s"(rates)
+                                 : SDRG_CHUNK_CLOBBERS, "vcc", "memory");
                 gain = g.x;
             } else if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 4) || lane < PG)) {
                 row_pipeline(&L.d[c & 1][my_s * ROW], &L.g[c & 1][my_s * ROW], lane < PG, [&](float (&v)[SB]) {

@@ -85,7 +85,7 @@ def writes(sb, buf):
     return [f"ds_write_b128 %[dst], v[{buf + 4 * i}:{buf + 4 * i + 3}] offset:{(16 * sb + 4 * i) * 4}" for i in range(4)]
 
 
-def chunk(role, lds=True, split=False):
+def chunk(role, lds=True, split=False, il=False):
     """role 'dc', 'lpf' or 'agc'.  split (low-pass, lab): VALU with all 64 lanes on (lanes past the 16 streams compute on whatever their
     registers hold and store nothing), LDS operations with the caller's EXEC (saved in %[sv])"""
     out = []
@@ -116,14 +116,16 @@ def chunk(role, lds=True, split=False):
             if role == "dc":
                 if q % 2 == 0:
                     out += dc_pair(b + q, 49)
-                continue
-            if role == "lpf":
+            elif role == "lpf":
                 out += lpf_sample(b + q, prev1, prev2)
                 prev2, prev1 = prev1, pair(b + q)
             else:
                 out += agc_sample(b + q, g)
                 g = b + q
-        if lds:
+            if il and lds and q % 4 == 3:  # interleaved: this quad's write and sub-block sb + 2's same quad
+                t = q // 4
+                out += writes(sb, b)[t:t + 1] + (reads(sb + 2, buf[sb + 2])[t:t + 1] if sb + 2 < 4 else [])
+        if lds and not il:
             out += exec_lds(writes(sb, b) + (reads(sb + 2, buf[sb + 2]) if sb + 2 < 4 else []))
     last = buf[3] + 15
     if split:  # the carried state is written on the caller's lanes only
@@ -339,6 +341,10 @@ def main():
     emit("SDRG_LPF_CHUNK_ASM", chunk("lpf"))
     emit("SDRG_AGC_CHUNK_ASM", chunk("agc"))
     emit("SDRG_DC_CHUNK_ASM", chunk("dc"))
+    print("// the DC and AGC chunks with each quad's LDS write and read issued right after it (lab: SDRG_DC_ASM=2,")
+    print("// SDRG_AGC_ASM=2)")
+    emit("SDRG_DC_CHUNK_IL_ASM", chunk("dc", il=True))
+    emit("SDRG_AGC_CHUNK_IL_ASM", chunk("agc", il=True))
     print("// the low-pass wave's whole loop with a one-chunk lookahead (SDRG_LPF_LOOKAHEAD; see lpf_loop() in the generator)")
     emit("SDRG_LPF_LOOP_ASM", lpf_loop())
     print("// the same loop with the chunk's LDS reads and writes interleaved quad by quad (SDRG_LPF_INTERLEAVE)")
