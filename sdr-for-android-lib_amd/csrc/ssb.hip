@@ -320,13 +320,14 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 #ifndef SDRG_LPF_ASM
 #define SDRG_LPF_ASM 1
 #endif
-// the DC wave's chunks as one hand-scheduled asm block (1) or through row_pipeline (0)
+// the DC wave's chunks as one hand-scheduled asm block, its LDS reads and writes interleaved quad by quad with the
+// arithmetic (2) or grouped per sub-block (1), or through row_pipeline (0)
 #ifndef SDRG_DC_ASM
-#define SDRG_DC_ASM 1
+#define SDRG_DC_ASM 2
 #endif
-// the AGC gain wave's chunks as one hand-scheduled asm block (1) or through row_pipeline (0)
+// the AGC gain wave's chunks, the same three forms
 #ifndef SDRG_AGC_ASM
-#define SDRG_AGC_ASM 1
+#define SDRG_AGC_ASM 2
 #endif
 constexpr int PG = 16;          // streams per workgroup
 // serial roles (bit 0 DC, 1 LPF, 2 AGC) that run on all 64 lanes (16 copies of the 16 streams) instead of the

@@ -341,8 +341,8 @@ def main():
     emit("SDRG_LPF_CHUNK_ASM", chunk("lpf"))
     emit("SDRG_AGC_CHUNK_ASM", chunk("agc"))
     emit("SDRG_DC_CHUNK_ASM", chunk("dc"))
-    print("// the DC and AGC chunks with each quad's LDS write and read issued right after it (lab: SDRG_DC_ASM=2,")
-    print("// SDRG_AGC_ASM=2)")
+    print("// the DC and AGC chunks with each quad's LDS write and read issued right after it (the product:")
+    print("// SDRG_DC_ASM=2, SDRG_AGC_ASM=2; the grouped forms above are options 1)")
     emit("SDRG_DC_CHUNK_IL_ASM", chunk("dc", il=True))
     emit("SDRG_AGC_CHUNK_IL_ASM", chunk("agc", il=True))
     print("// the low-pass wave's whole loop with a one-chunk lookahead (SDRG_LPF_LOOKAHEAD; see lpf_loop() in the generator)")
