@@ -12,7 +12,7 @@ iqs = [bench.synth_device_frames(torch, dev, bench.B, seed=7 + k, n=bench.N, cs1
 spec = torch.empty((bench.B, bench.N), dtype=torch.float32, device=dev)
 rec = torch.zeros((bench.B, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
 pcm = torch.empty((bench.B, eng.pcm_len), dtype=torch.int16, device=dev)
-eng.set_pipelining(True)
+eng.set_pipelining(sdrg.PIPELINE_INPUTS_READY if os.environ.get("INPUTS_READY") else True)
 now = [1000]
 def run(k, prof):
     eng.set_profiling(prof)
@@ -23,9 +23,9 @@ def run(k, prof):
         now[0] += 8
     eng.synchronize(); torch.cuda.synchronize()
     return (time.perf_counter() - t0) / k * 1e3
-run(10, False)
+run(100, False)
 for rep in range(3):
-    a = run(50, False); b = run(50, True)
+    a = run(200, False); b = run(200, True)
     print(f"no events {a:.4f} ms/step   events {b:.4f} ms/step")
 # host-side enqueue cost: calls issued back to back without waiting (the GPU queue absorbs them)
 eng.set_profiling(False)
