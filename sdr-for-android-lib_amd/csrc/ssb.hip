@@ -297,7 +297,9 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 // The stages are pipelined over chunks of CH samples through LDS rings with one workgroup barrier per
 // chunk, so while the low-pass wave works on chunk c the DC wave is on c+1 and the helpers on c-1 ... c-4:
 //
-//   it:  load c=it | DC c=it-1 | LPF c=it-2 | DESIRED c=it-3 | AGC c=it-4 | OUT c=it-5 | FIR c=it-6 | EQ c=it-7
+//   it:  load c=it | DC c=it-1 | LPF c=it-3 | DESIRED c=it-4 | AGC c=it-5 | OUT c=it-6 | FIR c=it-7 | EQ c=it-8
+//   (SDRG_LPF_LOOKAHEAD, below: the low-pass wave one chunk behind the DC wave's output; without it every role
+//   from the low-pass on is one chunk closer)
 //
 // The FIR accumulates each output's 255 products as its samples arrive (k ascending, exactly the
 // reference's order) in per-(stream, slot) accumulators, so no sample window is kept; completed outputs
