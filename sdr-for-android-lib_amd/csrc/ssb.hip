@@ -295,7 +295,7 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 // recurrence its own wave (lane = stream), keeps ONLY the recurrence arithmetic in it, and moves every
 // order-free operation (unpack, the AGC's sqrt/div "desired" level, the clamp, the FIR) to helper waves.
 // The stages are pipelined over chunks of CH samples through LDS rings with one workgroup barrier per
-// chunk, so while the low-pass wave works on chunk c the DC wave is on c+1 and the helpers on c-1 ... c-4:
+// chunk, so while the low-pass wave works on chunk c the DC wave is on c+2 and the helpers on c-1 ... c-5:
 //
 //   it:  load c=it | DC c=it-1 | LPF c=it-3 | DESIRED c=it-4 | AGC c=it-5 | OUT c=it-6 | FIR c=it-7 | EQ c=it-8
 //   (SDRG_LPF_LOOKAHEAD, below: the low-pass wave one chunk behind the DC wave's output; without it every role
