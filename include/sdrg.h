@@ -396,6 +396,15 @@ int32_t sdrg_engine_process_device(sdrg_engine *eng, const void *iq, int32_t for
                                    float *spectra, sdrg_frame_record *records, int16_t *pcm,
                                    int64_t now_ms);
 int32_t sdrg_engine_synchronize(sdrg_engine *eng);
+/* evaluateSignalStrength alone (fft_process.cpp:122-379) on caller spectra: [n_streams][samples_per_reading]
+ * fftshifted linear power (the FFTProcessor's power_shifted member after process()), records out, each stream's
+ * statistics state (tracking latch, detection ring, stale outputs) advanced exactly as by a process() call with
+ * STATS.  _device: both buffers in device memory, ordered on the main stream (complete after
+ * sdrg_engine_synchronize).  _host: host buffers, synchronous. */
+int32_t sdrg_engine_signal_strength_device(sdrg_engine *eng, const float *spectra, sdrg_frame_record *records,
+                                           int64_t now_ms);
+int32_t sdrg_engine_signal_strength_host(sdrg_engine *eng, const float *spectra, sdrg_frame_record *records,
+                                         int64_t now_ms);
 /* Enqueue the engine's work on the caller's HIP stream (a hipStream_t; NULL = the engine's own stream): the
  * SSB fork/join happens relative to it, so consumers on that stream (e.g. an RCCL gather of the records)
  * are ordered after each call without a host synchronisation.  Synchronises the previous stream first.

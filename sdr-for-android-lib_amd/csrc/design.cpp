@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include "design.h"
+#include "glibc_logf.h"
 
 #ifndef M_PI
 #define M_PI 3.14159265358979323846
@@ -118,6 +119,9 @@ StatsGeometry stats_geometry(uint32_t sample_rate, uint32_t center_frequency, in
     g.focus_lo = lo > 0 ? lo : 0;
     g.focus_hi = hi < n - 1 ? hi : n - 1;
     g.focus_len = g.focus_hi - g.focus_lo + 1;
+    // the Gumbel term's logN (:282): geometry only, so computed here with the reference's libm (glibc's logf,
+    // restated in glibc_logf.h so the value does not depend on the host's C library)
+    g.log_focus_len = g.focus_len > 0 ? glibc::logf(static_cast<float>(g.focus_len)) : 0.0f;
     const int w = (int)ceilf(1000.0f / freq_per_bin);
     g.win_bins_1k = w > 1 ? w : 1;
     int nr = 0;

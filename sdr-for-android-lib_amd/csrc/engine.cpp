@@ -997,6 +997,50 @@ int32_t sdrg_engine_process_device(sdrg_engine *e, const void *iq, int32_t forma
     return enqueue(e, iq, format, stages, spectra, records, pcm, now_ms, false);
 }
 
+// evaluateSignalStrength (fft_process.cpp:122-379) on spectra the caller supplies: the FFTProcessor's
+// power_shifted member in, the getters' values out, the stream state (tracking latch, detection ring, stale
+// outputs) carried exactly as a process() call carries it.  Ordered on the main stream.
+static int32_t signal_strength(sdrg_engine *e, const float *spectra, sdrg_frame_record *records, int64_t now_ms) {
+    const int n = e->cfg.samples_per_reading, B = e->n_streams;
+    if (e->fft_fs == 0) return fail(SDRG_E_INVALID, "the statistics' sample rate is 0");
+    StatsGeometry geo = stats_geometry(e->fft_fs, e->fft_fc, n, e->fft_focus);
+    geo.cf_changed = e->cf_changed_pending ? 1 : 0;
+    int32_t rc = ensure_device(&e->d_pool, &e->pool_elems, stats_global_pool_floats(geo, B));
+    if (rc) return rc;
+    HIP_TRY(launch_stats(spectra, B, geo, now_ms, e->d_stats, records, e->d_pool, e->s_main));
+    e->cf_changed_pending = false;
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_signal_strength_device(sdrg_engine *e, const float *spectra, sdrg_frame_record *records,
+                                           int64_t now_ms) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if (!spectra || !records) return fail(SDRG_E_INVALID, "null spectra or records");
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
+    return signal_strength(e, spectra, records, now_ms);
+}
+
+int32_t sdrg_engine_signal_strength_host(sdrg_engine *e, const float *spectra, sdrg_frame_record *records,
+                                         int64_t now_ms) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    if (!spectra || !records) return fail(SDRG_E_INVALID, "null spectra or records");
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
+    const int n = e->cfg.samples_per_reading, B = e->n_streams;
+    int32_t rc = ensure_device(&e->d_spec_stage, &e->spec_stage_elems, (size_t)B * n, true);
+    if (rc) return rc;
+    if (!e->d_rec_stage)
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_rec_stage), sizeof(sdrg_frame_record) * (size_t)B));
+    HIP_TRY(hipMemcpyAsync(e->d_spec_stage, spectra, sizeof(float) * (size_t)B * n, hipMemcpyHostToDevice, e->s_main));
+    rc = signal_strength(e, e->d_spec_stage, e->d_rec_stage, now_ms);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(records, e->d_rec_stage, sizeof(sdrg_frame_record) * (size_t)B, hipMemcpyDeviceToHost,
+                           e->s_main));
+    HIP_TRY(hipStreamSynchronize(e->s_main));
+    return SDRG_OK;
+}
+
 int32_t sdrg_engine_synchronize(sdrg_engine *e) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     HIP_TRY(hipStreamSynchronize(e->s_main));

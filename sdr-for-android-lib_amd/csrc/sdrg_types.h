@@ -44,6 +44,7 @@ struct StatsGeometry {
     float cf_u32_minus_nyq;    // (centerFrequency - nyquist), uint32 promoted to float (:350)
     float cf_float;            // static_cast<float>(centerFrequency)
     int32_t cf_changed;        // setFrequency happened since the last frame (isCenterFrequencyChanged)
+    float log_focus_len;       // std::log(static_cast<float>(focusLen)) (:282) with glibc's logf, on the host
 };
 
 // ------------------------------------------------------------------------------------------------

@@ -18,6 +18,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "glibc_logf.h"
 #include "sdrg_internal.h"
 
 #pragma clang fp contract(off)
@@ -42,7 +43,16 @@ __device__ unsigned long long g_stats_stamps[STAMP_PHASES * 8192];
             g_stats_stamps[blockIdx.x * STAMP_PHASES + (k)] = __builtin_amdgcn_s_memtime();                   \
     } while (0)
 
-__device__ __forceinline__ float db_of(float p) { return 10.0f * log10f(p / 1.0f + 1e-20f); }  // refPower = 1
+// glibc's logf table, copied into LDS by every kernel of this file before its first barrier (load_logf_tab): the
+// dB values are the reference's `10.0f * log10f(p / refPower + 1e-20f)` with glibc's log10f (glibc_logf.h), so
+// every dB, the peak index, the window order and the pooled gaps equal the reference's x86-64 build bit for bit
+__shared__ glibc::LogfEntry s_logf_tab[16];
+__device__ __forceinline__ void load_logf_tab() {
+    if (threadIdx.x < 16) s_logf_tab[threadIdx.x] = glibc::logf_table()[threadIdx.x];
+}
+__device__ __forceinline__ float db_of(float p) {  // refPower = 1
+    return 10.0f * glibc::log10f_with(p / 1.0f + 1e-20f, s_logf_tab);
+}
 
 struct WinScan {
     float sum;       // sequential sum over [lo, hi]
@@ -368,7 +378,7 @@ __device__ __forceinline__ void snr_6_4cd(const StatsGeometry &g, StatsState &st
                                           float focus_best1k_linear, int best_start) {
     const int w1k = g.win_bins_1k;
     st.peak_above_noise_mean_db = abs_peak_db - pbm;  // :274
-    const float logN = logf((float)g.focus_len);
+    const float logN = g.log_focus_len;  // std::log(float(focusLen)) (:282), glibc logf on the host
     const float sqrt2logN = sqrtf(2.0f * logN);
     const float gumbel_loc = pbm + sigma_bin * sqrt2logN;
     const float gumbel_sig = fmax_ref(sigma_bin * 3.14159f / (sqrtf(6.0f) * sqrt2logN), 0.5f);
@@ -384,14 +394,13 @@ __device__ __forceinline__ void snr_6_4cd(const StatsGeometry &g, StatsState &st
     float sigma1k = 1.4816f * kth_of4(g1k, n_bottom / 2);
     if (sigma1k < sigma_floor_1k) sigma1k = sigma_floor_1k;
     if (sigma1k < 0.5f) sigma1k = 0.5f;
-    if (focus_best1k_linear > 0.0f) {
-        const float focus_best1k_db = db_of(focus_best1k_linear);
-        st.best1khz_snr_db = focus_best1k_db - mean1k;
-        st.best1khz_snr_sigma = st.best1khz_snr_db / sigma1k;
-        st.best1khz_center_freq_hz = (best_start + w1k / 2) * g.freq_per_bin + g.cf_minus_nyq;
-    } else {
-        st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
-    }
+    // (:303-327; selects rather than a branch around the dB, which kept the state struct in scratch)
+    const bool pos = focus_best1k_linear > 0.0f;
+    const float focus_best1k_db = db_of(pos ? focus_best1k_linear : 1.0f);
+    const float snr1k_db = focus_best1k_db - mean1k;
+    st.best1khz_snr_db = pos ? snr1k_db : 0.0f;
+    st.best1khz_snr_sigma = pos ? snr1k_db / sigma1k : 0.0f;
+    if (pos) st.best1khz_center_freq_hz = (best_start + w1k / 2) * g.freq_per_bin + g.cf_minus_nyq;
 }
 
 // 6.5 frequency tracking (:333-361), clock injected; 6.6 detection (:365-378)
@@ -639,6 +648,7 @@ __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restr
     const int lane = threadIdx.x;
     const size_t frame = blockIdx.x;
     const int n_ref = g.n_ref;
+    load_logf_tab();
 #pragma unroll
     for (int i = 0; i < 10; i++) {  // constant kernarg indices (a lane-indexed kernarg array would go to scratch)
         if (lane == i) {
@@ -891,6 +901,7 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
     const int lane = threadIdx.x;
     const size_t frame = blockIdx.x;
     const int n_ref = g.n_ref;
+    load_logf_tab();
     // the window bounds are indexed by thread below: copy them out of the kernel arguments with constant
     // indices (a thread-indexed kernarg array would be copied to scratch)
 #pragma unroll

@@ -83,7 +83,7 @@ EXPORTS = [
     "sdrg_engine_input_released", "sdrg_engine_wait_input_released", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
     "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_set_stream",
     "sdrg_engine_set_pipelining", "sdrg_engine_set_ssb_variant", "sdrg_engine_get_ssb_variant",
-    "sdrg_engine_process_host",
+    "sdrg_engine_process_host", "sdrg_engine_signal_strength_device", "sdrg_engine_signal_strength_host",
     "sdrg_engine_set_callbacks", "sdrg_engine_set_profiling", "sdrg_engine_get_timings",
     "sdrg_engine_get_timing_stats", "sdrg_engine_reset_timing_stats",
     "sdrg_engine_set_spectral_pulse_config", "sdrg_engine_set_audio_pulse_config", "sdrg_engine_pulse_outputs",
@@ -226,6 +226,8 @@ def load() -> ctypes.CDLL:
         "sdrg_host_free": (_I32, [P]),
         "sdrg_engine_get_ssb_variant": (_I32, [P, P, P, P, P]),
         "sdrg_engine_process_host": (_I32, [P, P, _I32, _I32, P, P, P, _I64]),
+        "sdrg_engine_signal_strength_device": (_I32, [P, P, P, _I64]),
+        "sdrg_engine_signal_strength_host": (_I32, [P, P, P, _I64]),
         "sdrg_engine_set_callbacks": (_I32, [P, ctypes.POINTER(_Callbacks)]),
         "sdrg_engine_set_profiling": (_I32, [P, _I32]),
         "sdrg_engine_get_timings": (_I32, [P, ctypes.POINTER(_Timings)]),
@@ -495,6 +497,19 @@ class Engine:
                                                ptr(pcm) if (pcm is not None and plen > 0) else None, now_ms),
                "process_host")
         return spec, recs, pcm
+
+    def signal_strength(self, spectra: np.ndarray, now_ms: int = 0) -> np.ndarray:
+        """evaluateSignalStrength alone on caller spectra ([n_streams][samplesPerReading] fftshifted linear power,
+        fft_process.cpp:122-379): returns the records; each stream's statistics state advances as in process()."""
+        n = self.cfg.samplesPerReading
+        spectra = np.ascontiguousarray(spectra, dtype=np.float32)
+        if spectra.shape != (self.n_streams, n):
+            raise SdrgError(f"spectra {spectra.shape}: expected ({self.n_streams}, {n})")
+        recs = np.zeros(self.n_streams, RECORD_DTYPE)
+        _check(load().sdrg_engine_signal_strength_host(self._h, spectra.ctypes.data_as(ctypes.c_void_p),
+                                                       recs.ctypes.data_as(ctypes.c_void_p), now_ms),
+               "signal_strength_host")
+        return recs
 
     def process_device(self, iq_ptr: int, fmt: int, stages: int, spectra_ptr: int | None, records_ptr: int | None,
                        pcm_ptr: int | None, now_ms: int = 0) -> None:

@@ -8,7 +8,7 @@
 import numpy as np
 import pytest
 
-from test_gpu_parity import assert_records_close, engine, spectrum_ok
+from test_gpu_parity import assert_records_equal, engine, spectrum_ok
 
 pytestmark = pytest.mark.gpu
 
@@ -43,7 +43,7 @@ def _check_calls(S, O, raw, fmt, n, fs):
             assert ok.all(), (b, f, np.argwhere(~ok)[:5].ravel())
             want[b] = fst[b].signal_strength(spec[b], now)
             np.testing.assert_array_equal(pcm[b], sst[b].process(iq, fs, 1), err_msg=f"pcm stream {b} call {f}")
-        assert_records_close(rec, want, 2e-5, 2e-4, msg=f"call {f}")
+        assert_records_equal(rec, want, msg=f"call {f}")
     eng.close()
 
 
