@@ -11,8 +11,11 @@ work (the per-stream filter state advances from step to step like a live receive
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one process per GPU)
 
-With N > 1 every rank runs its own 4096 streams (weak scaling) and the per-frame records of each step are
-gathered to rank 0 over RCCL; value = all ranks' samples / max-over-ranks time.
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts the N rank processes itself
+(torch.distributed.run as a child process, before anything touches a GPU) and exits with their status.
+With N > 1 every rank runs its own 4096 streams (weak scaling) and the per-frame records (+ focus-window
+spectra) of each step are gathered to rank 0 over RCCL; value = all ranks' samples / max-over-ranks time.  The
+full-spectra gather (the fftCallback payload) is timed after the timed region and reported separately.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -178,6 +181,43 @@ def rehearsal_verify(torch, dist, world, rank, streams, rec, f_stage, pcm, gathe
     return result
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_command(gpus: int, argv: list[str], port: int) -> list[str]:
+    """The one-process-per-GPU launch of this script (the driver's own form of the command)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + argv
+
+
+def maybe_launch(args, argv: list[str]) -> int | None:
+    """--gpus N > 1 without WORLD_SIZE: start the N ranks as a child torch.distributed.run (nothing in this
+    process has touched a GPU: counting devices does not initialise one on this image) and return its exit
+    status; None when this process is a rank (or N == 1)."""
+    if args.gpus < 1:
+        log(f"bench: --gpus must be >= 1 (got {args.gpus})")
+        return 2
+    if args.gpus == 1 or "WORLD_SIZE" in os.environ:
+        return None
+    if not args.rehearse_gloo:
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            log(f"bench: --gpus {args.gpus} but only {have} GPU(s) visible")
+            return 3
+    cmd = launch_command(args.gpus, argv, free_port())
+    if args.launch_dry_run:
+        print(json.dumps({"launch": cmd}), flush=True)
+        return 0
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -212,7 +252,19 @@ def main() -> int:
     ap.add_argument("--rehearse-gloo", action="store_true",
                     help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, gloo backend, the gathers "
                          "staged through host memory (not a measurement)")
-    args = ap.parse_args()
+    ap.add_argument("--spectra-gather-steps", type=int, default=10,
+                    help="N > 1: after the timed region, time this many gathers of every rank's full spectra (the "
+                         "fftCallback payload, 4 B x N bins per frame) to rank 0, reported as spectra_gather_ms (0: skip)")
+    ap.add_argument("--prewarm-ms", type=float, default=100.0,
+                    help="untimed pre-roll before --warmup: the same step, in blocks of 25, until this much wall time has "
+                         "passed, so the timed steps run at the chip's steady clock whatever --warmup is (reported as "
+                         "prewarm_ms)")
+    ap.add_argument("--launch-dry-run", action="store_true", help=argparse.SUPPRESS)
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+    rc = maybe_launch(args, argv)
+    if rc is not None:
+        return rc
 
     import torch
     import torch.distributed as dist
@@ -223,6 +275,12 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     rehearse = args.rehearse_gloo and world > 1
+    if world > 1 and args.gpus not in (1, world):
+        log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return 3
+    if world > 1 and not rehearse and torch.cuda.device_count() < world:
+        log(f"bench: WORLD_SIZE={world} but only {torch.cuda.device_count()} GPU(s) visible")
+        return 3
     if rehearse:
         local = 0
         dist.init_process_group("gloo")
@@ -231,6 +289,22 @@ def main() -> int:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    ranks_info = None
+    if world > 1:
+        if dist.get_world_size() != world:
+            log(f"bench: process group has {dist.get_world_size()} ranks, expected {world}")
+            return 3
+        props = torch.cuda.get_device_properties(dev)
+        mine = {"rank": rank, "local_rank": local, "device": dev.index, "name": props.name,
+                "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", ""))}
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        distinct = len({e["uuid"] or (e["pci_bus_id"], e["device"]) for e in every}) == world
+        ranks_info = {"ranks_seen": dist.get_world_size(), "backend": dist.get_backend(),
+                      "distinct_devices": distinct,
+                      "devices": [{k: v for k, v in e.items() if v not in (None, "")} for e in every]}
+        if not rehearse and not distinct:
+            log(f"bench: warning: ranks may share a GPU: {every}")
 
     c5 = args.config == "c5"
     n = 65536 if c5 else N
@@ -303,6 +377,16 @@ def main() -> int:
     if pipelined:
         eng.set_pipelining(pipelined)
     eng.set_profiling(True)
+    # pre-roll: from idle the chip needs ~50 steps (~20 ms) of this load to reach its steady clock
+    # (tools/lab/warm_trace.py), more than a short --warmup covers; blocks of 25 steps until prewarm_ms has passed
+    t_pre = time.perf_counter()
+    prewarm_steps = 0
+    while (time.perf_counter() - t_pre) * 1e3 < args.prewarm_ms:
+        for _ in range(25):
+            step()
+        prewarm_steps += 25
+        eng.synchronize()
+    prewarm_ms = (time.perf_counter() - t_pre) * 1e3
     for _ in range(args.warmup):
         step()
     eng.synchronize()
@@ -319,6 +403,30 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    spectra_gather = None
+    if world > 1 and args.spectra_gather_steps > 0:
+        # the full spectra of every frame (fftCallback payload) to rank 0, timed on its own: outside the metric
+        eng.synchronize()
+        s_out = torch.empty((world * streams, n), dtype=torch.float32, device=gdev) if rank == 0 else None
+        s_src = host(spec)
+        shard.gather_spectra(s_src, world, rank, dst=0, out=s_out)  # untimed first gather
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = time.perf_counter()
+        for _ in range(args.spectra_gather_steps):
+            shard.gather_spectra(s_src, world, rank, dst=0, out=s_out)
+        torch.cuda.synchronize()
+        dist.barrier()
+        tgt = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=gdev)
+        dist.all_reduce(tgt, op=dist.ReduceOp.MAX)
+        g_ms = float(tgt.item()) / args.spectra_gather_steps * 1e3
+        into0 = (world - 1) * streams * n * 4
+        spectra_gather = {"spectra_gather_ms": round(g_ms, 4), "bytes_per_rank": streams * n * 4,
+                          "bytes_into_rank0": into0, "GBs_into_rank0": round(into0 / (g_ms * 1e-3) / 1e9, 1),
+                          "steps": args.spectra_gather_steps,
+                          "note": "every rank's full [streams, N] float32 spectra gathered to rank 0 (the fftCallback "
+                                  "payload, SURVEY 8e), after the timed region; not part of value"}
+        del s_out
     rehearsal_check = rehearsal_verify(torch, dist, world, rank, streams, rec, f_stage, pcm, gather_pcm, gathered, f_out,
                                        p_out) if rehearse else None
     ts = eng.timing_stats()
@@ -358,6 +466,47 @@ def main() -> int:
             eng.set_ssb_variant(0.0, 0)
         return {"value": round(k_steps * streams * n / dt / 1e6, 2), "ms_per_step": round(dt / k_steps * 1e3, 4)}
 
+    def c5_line(focus_c5: int, k_steps: int) -> dict:
+        """BASELINE configs[4] in this same run: 1024 streams x 65536-pt CS16 frames, FFT + |X|^2 + fftshift + stats
+        over a focus_c5 kHz focus, its own engine and rotated inputs."""
+        n5, s5 = 65536, 1024
+        e5 = sdrg.Engine(sdrg.SDRConfig(centerFrequency=CF, samplesPerReading=n5, sampleRate=FS,
+                                        freqFocusRangeKhz=focus_c5, soundMode=1), s5, device=local)
+        iq5 = [synth_device_frames(torch, dev, s5, seed=0xC5 + k, n=n5, cs16=True) for k in range(N_INPUTS)]
+        sp5 = torch.empty((s5, n5), dtype=torch.float32, device=dev)
+        rc5 = torch.zeros((s5, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        st5 = sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS
+        torch.cuda.synchronize()
+        e5.set_profiling(True)
+        t5 = [1000]
+
+        def run(k):
+            for i in range(k):
+                e5.process_device(iq5[i % N_INPUTS].data_ptr(), sdrg.CS16, st5, sp5.data_ptr(), rc5.data_ptr(), None,
+                                  t5[0])
+                t5[0] += n5 // 2000
+        run(20)
+        e5.synchronize()
+        e5.reset_timing_stats()
+        t1 = time.perf_counter()
+        run(k_steps)
+        e5.synchronize()
+        dt = time.perf_counter() - t1
+        tm = e5.timing_stats()
+        e5.close()
+        ms = dt / k_steps * 1e3
+        fft_bytes = 8.0 * s5 * n5  # CS16: 4 B in + 4 B float32 power out per sample
+        step_b = fft_bytes + s5 * sdrg.RECORD_DTYPE.itemsize
+        del iq5, sp5, rc5
+        return {"value": round(k_steps * s5 * n5 / dt / 1e6, 2), "ms_per_step": round(ms, 4),
+                "spectrum_ms": round(tm["spectrum_ms"], 4), "stats_ms": round(tm["stats_ms"], 4),
+                "roofline_fft": {"kernel": "four_step_a + four_step_b", "achieved": round(fft_bytes / tm["spectrum_ms"]
+                                                                                          / 1e6, 1),
+                                 "frac": round(fft_bytes / tm["spectrum_ms"] / 1e6 / HBM_PEAK_GBS, 4)},
+                "roofline_step_frac": round(step_b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "workload": f"BASELINE configs[4]: {s5} streams x {n5}-pt CS16 frames @2 Msps, four-step FFT + |X|^2 "
+                            f"+ fftshift + signal-strength stats over a {focus_c5} kHz focus; no SSB"}
+
     labelled = {}
     if world == 1 and args.config == "c3" and args.stages == "all" and not variant and not args.no_labelled:
         eng.set_profiling(False)
@@ -368,6 +517,8 @@ def main() -> int:
                                            workload="BASELINE configs[2] as written (a build extension, not the "
                                                     f"reference chain): SSB with an NCO mixer at +{NCO_HZ / 1e3:g} kHz "
                                                     "+ 127-tap FIR decim 41, every other stage as the headline")
+        labelled["configs4_c5_5khz"] = c5_line(5, args.steps)
+        labelled["configs4_c5_200khz"] = c5_line(200, args.steps)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -445,6 +596,25 @@ def main() -> int:
         "inputs": f"{N_INPUTS} distinct {streams}x{n} {fmt_name} batches ({N_INPUTS * streams * n * in_bps / 2**20:.0f} "
                   "MiB) rotated per step in every leg, so inputs are not served from the 256 MiB Infinity Cache",
     }
+    if args.stages == "all":
+        # the step cannot beat its slowest bound: the SSB chain's serial floor (one frame's recurrences) or the HBM
+        # time of its algorithmic bytes; as a fraction of HBM peak that ceiling is what ">= 60 % of HBM" can reach
+        floor_ms = n * SSB_CHAIN_CYCLES / (MAX_CLOCK_GHZ * 1e9) * 1e3
+        hbm_ms = step_bytes / (HBM_PEAK_GBS * 1e9) * 1e3
+        ceil_ms = max(floor_ms, hbm_ms)
+        out["roofline_step"]["ceiling"] = {
+            "step_ceiling_frac": round(hbm_ms / ceil_ms, 4), "ceiling_ms": round(ceil_ms, 4),
+            "bound_by": "ssb serial floor" if floor_ms >= hbm_ms else "hbm",
+            "hbm_ms_at_peak": round(hbm_ms, 4), "ssb_floor_ms": round(floor_ms, 4),
+            "frac_of_ceiling": round(ceil_ms / ms_per_step, 4),
+            "note": "step algorithmic bytes / max(SSB serial floor, HBM time at peak) / peak: the highest "
+                    "roofline_step.frac any bit-exact schedule of this step can reach"}
+    out["prewarm_ms"] = round(prewarm_ms, 1)
+    out["prewarm_steps"] = prewarm_steps
+    if ranks_info:
+        out.update(ranks_info)
+    if spectra_gather:
+        out["spectra_gather"] = spectra_gather
     if ssb_iso_ms:
         floor_ms = n * SSB_CHAIN_CYCLES / (MAX_CLOCK_GHZ * 1e9) * 1e3
         out["ssb_latency_floor"] = {

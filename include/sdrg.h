@@ -139,7 +139,8 @@ typedef struct sdrg_callbacks {
  * timing statistics average the measured ones). */
 typedef struct sdrg_timings {
     float spectrum_ms;   /* unpack + FFT + |X|^2 + fftshift kernel */
-    float stats_ms;      /* signal-strength kernel (+ spectral pulse detector when requested) */
+    float stats_ms;      /* end of the spectrum -> end of the signal-strength kernel (+ spectral pulse detector when
+                            requested), on the statistics' stream; never includes the SSB stream's work */
     float ssb_ms;        /* whole SSB chain (all its kernels, + audio pulse detector when requested) */
     float total_ms;      /* call start -> end of the main stream's work; joined calls include the SSB stream */
 } sdrg_timings;
@@ -386,7 +387,10 @@ int32_t sdrg_engine_reset_state(sdrg_engine *eng);
 /* Process one frame of every stream, all buffers in device memory (HBM).
  *   iq       : [n_streams][samples_per_reading] samples in `format`
  *   spectra  : [n_streams][samples_per_reading] float, fftshifted linear power (fftCallback payload);
- *              may be NULL when STATS is not requested (then an internal buffer is used)
+ *              may be NULL when STATS is not requested (then an internal buffer is used).  Odd N: element
+ *              N-1 of each row is never written, as in the reference's fftshift loop (fft_process.cpp:92-97),
+ *              whose member vector keeps its old value there (0 when fresh); a caller buffer should be zeroed
+ *              once before its first use, since the statistics may read that bin
  *   records  : [n_streams] sdrg_frame_record (may be NULL if STATS not requested)
  *   pcm      : [n_streams][pcm_len] int16 (may be NULL if SSB not requested)
  *   now_ms   : monotonic clock in ms for the 300 ms frequency-tracking latch

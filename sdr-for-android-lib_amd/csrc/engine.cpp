@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
 #include <mutex>
 #include <set>
 #include <string>
@@ -45,17 +46,21 @@ int32_t sdrg::fail(int32_t code, const char *fmt, ...) {
     return code;
 }
 
+// The attribute is one limit per (kernel, device) that each set overwrites, and launches asking for more than it
+// fail; requests vary with the geometry (statistics) and N (any-N FFT), so the limit only ever rises: the largest
+// value set so far is cached per (kernel, device), and a smaller request leaves it as it is.
 hipError_t sdrg::ensure_dynamic_lds(const void *kernel, int bytes) {
     static std::mutex mu;
-    static std::set<std::tuple<const void *, int, int>> done;  // (kernel, device, bytes)
+    static std::map<std::pair<const void *, int>, int> limit;  // (kernel, device) -> largest limit set
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> lk(mu);
-    const auto key = std::make_tuple(kernel, dev, bytes);
-    if (done.count(key)) return hipSuccess;
+    const auto key = std::make_pair(kernel, dev);
+    auto it = limit.find(key);
+    if (it != limit.end() && it->second >= bytes) return hipSuccess;
     e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    if (e == hipSuccess) done.insert(key);
+    if (e == hipSuccess) limit[key] = bytes;
     return e;
 }
 
@@ -119,6 +124,7 @@ struct EvSet {
     hipEvent_t t0 = nullptr, spec = nullptr, stats = nullptr, ssb0 = nullptr, ssb1 = nullptr, end = nullptr;
     bool has_spec = false, has_stats = false, has_ssb = false, pending = false;
     bool ssb_timed = false;  // ssb0 recorded: this call's SSB duration is measured
+    bool stats_marked = false;  // `stats` recorded after the statistics (joined calls, whose `end` follows the join)
 };
 
 }  // namespace
@@ -274,7 +280,7 @@ int32_t fold_slot(sdrg_engine *e, int slot) {
         t.spectrum_ms = ms;
     }
     if (ev.has_stats) {
-        HIP_TRY(hipEventElapsedTime(&ms, ev.has_spec ? ev.spec : ev.t0, ev.end));
+        HIP_TRY(hipEventElapsedTime(&ms, ev.has_spec ? ev.spec : ev.t0, ev.stats_marked ? ev.stats : ev.end));
         t.stats_ms = ms;
     }
     if (ev.has_ssb && ev.ssb_timed) {
@@ -333,6 +339,9 @@ int32_t prepare_ssb(sdrg_engine *e, SsbControl &c, uint32_t &nco_phase, SsbParam
     if (c.taps_samp != c.samp_count || c.taps_decim != decim || c.taps_req != e->fir_taps || !e->d_taps) {
         // an earlier call's SSB kernels may still read the taps and the chunk table (non-blocking streams)
         HIP_TRY(hipStreamSynchronize(e->s_ssb));
+        // the device tables change now, before this call commits its SSB state: the committed key no longer
+        // describes them, so a call that fails after this point leaves the next one to upload again
+        e->ssb.taps_samp = -1;
         float h[256];
         c.n_taps = design_fir(c.samp_count, decim, 0.45f, h, e->fir_taps);
         c.taps_req = e->fir_taps;
@@ -511,6 +520,8 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         // the SSB start marker sits on the SSB stream between the fork and the pipeline; pipelined, that
         // stream is the step's critical path, so only every 8th call carries one (its mean is the sample's)
         ev->ssb_timed = do_ssb && (!(e->pipelined && !join) || e->calls_profiled % 8 == 0);
+        // a joined call's end marker follows the wait for the SSB stream: the statistics get a marker of their own
+        ev->stats_marked = do_stats && !(e->pipelined && !join);
         e->calls_profiled++;
     }
     // Markers: every event recorded between two kernels of a stream costs that stream a gap (several us
@@ -575,6 +586,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
                                              (int)sizeof(sdrg_frame_record), e->spec_bank.d_out, sm);
             if (rc) return rc;
         }
+        if (prof && ev->stats_marked) HIP_TRY(hipEventRecord(ev->stats, sm));
     }
     // the main stream's end marker: input release (the spectrum reads iq), timing; joined calls place it after
     // the join, so total_ms spans both streams
@@ -715,7 +727,7 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
     // stream priorities (lab: SDRG_STREAM_PRIO = "main,ssb" in hipDeviceGetStreamPriorityRange units; default
     // both normal)
     int prio_main = 0, prio_ssb = 0;
-    if (const char *v = getenv("SDRG_STREAM_PRIO")) {
+    if (const char *v = lab_getenv("SDRG_STREAM_PRIO")) {
         if (sscanf(v, "%d,%d", &prio_main, &prio_ssb) != 2) prio_main = prio_ssb = 0;
     }
     if (hipStreamCreateWithPriority(&e->s_own, hipStreamNonBlocking, prio_main) != hipSuccess ||
@@ -723,7 +735,7 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
     e->s_main = e->s_own;
     // lab: SDRG_CU_SPLIT = 1 (SSB on even CU-mask bits, spectrum/statistics on odd) or 2 (low / high half)
-    if (const char *v = getenv("SDRG_CU_SPLIT")) {
+    if (const char *v = lab_getenv("SDRG_CU_SPLIT")) {
         const int mode = atoi(v);
         const int ncu = prop.multiProcessorCount;
         if ((mode == 1 || mode == 2) && ncu >= 2) {
@@ -746,7 +758,7 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
     // stream-to-stream ordering events on one device: no system-scope fence needed (lab: SDRG_EVENT_FENCE=1
     // restores the default system-scope release/acquire)
     static const unsigned ev_flags = [] {
-        const char *v = getenv("SDRG_EVENT_FENCE");
+        const char *v = lab_getenv("SDRG_EVENT_FENCE");
         return (v && atoi(v) == 1) ? (unsigned)hipEventDisableTiming
                                    : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
     }();
@@ -1046,7 +1058,7 @@ int32_t sdrg_engine_synchronize(sdrg_engine *e) {
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));  // not joined into s_main when pipelined
     static const bool stamps = [] {
-        const char *v = getenv("SDRG_PIPE_STAMPS");
+        const char *v = lab_getenv("SDRG_PIPE_STAMPS");
         return v && v[0] == '1';
     }();
     if (stamps) ssb_report_stamps();

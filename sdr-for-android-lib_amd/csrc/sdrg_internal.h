@@ -7,6 +7,16 @@
 
 #include "sdrg_types.h"
 
+#include <stdlib.h>
+
+// Lab knobs (tools/: role maps, priorities, CU splits, stamps ...) are read from the environment only in lab
+// builds (-DSDRG_LAB=1, tools/build_variant.sh); the product library (make) ignores them, so a stray variable in
+// a deployed process cannot change its results or its schedule.
+#ifndef SDRG_LAB
+#define SDRG_LAB 0
+#endif
+static inline const char *lab_getenv(const char *name) { return SDRG_LAB ? getenv(name) : nullptr; }
+
 namespace sdrg {
 
 // Raise a kernel's dynamic-LDS limit to `bytes` on the CURRENT device, once per (kernel, device): the

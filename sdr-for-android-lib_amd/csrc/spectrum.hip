@@ -526,7 +526,7 @@ hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectr
     hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(k), LDS_BYTES);
     if (e != hipSuccess) return e;
     static const int max_grid = [] {  // lab override (SDRG_SPECTRUM_GRID): persistent workgroups
-        const char *v = getenv("SDRG_SPECTRUM_GRID");
+        const char *v = lab_getenv("SDRG_SPECTRUM_GRID");
         const int g = v ? atoi(v) : 0;
         return g > 0 ? g : 0;
     }();

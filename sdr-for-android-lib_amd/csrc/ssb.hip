@@ -1033,7 +1033,7 @@ hipError_t launch_ssb_reference(const void *iq, int fmt, int n_frames, const Ssb
 
 bool ssb_force_reference_kernels() {
     static const bool force = [] {
-        const char *v = getenv("SDRG_SSB_REFERENCE_KERNELS");
+        const char *v = lab_getenv("SDRG_SSB_REFERENCE_KERNELS");
         return v && v[0] == '1';
     }();
     return force;
@@ -1048,7 +1048,7 @@ static unsigned long long *g_stamps = nullptr;
 static int g_stamps_groups = 0, g_stamp_call = 0;
 unsigned long long *ssb_stamps_buffer(int n_frames) {
     static const bool on = [] {
-        const char *v = getenv("SDRG_PIPE_STAMPS");
+        const char *v = lab_getenv("SDRG_PIPE_STAMPS");
         return v && v[0] == '1';
     }();
     if (!on) return nullptr;
@@ -1169,16 +1169,16 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         AudioFront af{};
         if (audio) af = *audio;
         static const int prio_mask = [] {  // diagnostic override: SDRG_PIPE_PRIO = bit mask of high-priority waves
-            const char *e = getenv("SDRG_PIPE_PRIO");
+            const char *e = lab_getenv("SDRG_PIPE_PRIO");
             return e ? (int)strtol(e, nullptr, 0) : 0x7;
         }();
         // role of hardware wave w = nibble w (wave w runs on SIMD w % 4); SDRG_PIPE_MAP overrides (diagnostic)
         static const unsigned long long role_map = [] {
-            const char *e = getenv("SDRG_PIPE_MAP");
+            const char *e = lab_getenv("SDRG_PIPE_MAP");
             return e ? strtoull(e, nullptr, 16) : DEFAULT_ROLE_MAP;
         }();
         static const int skip_mask = [] {  // diagnostic only (wrong results): roles whose work is skipped
-            const char *e = getenv("SDRG_PIPE_SKIP");
+            const char *e = lab_getenv("SDRG_PIPE_SKIP");
             return e ? (int)strtol(e, nullptr, 0) : 0;
         }();
 #define SDRG_PIPE_LAUNCH(F)                                                                                      \

@@ -54,6 +54,7 @@ struct sdrg_ssb_processor {
     std::deque<Item> q;
     bool busy = false;  // the worker holds a popped frame
     std::thread worker;
+    std::mutex join_mu;  // stop() may race with another stop (stopReading vs close from different threads)
     std::atomic<bool> running{false};
     sdrg_ssb_callbacks cbs{};
     std::atomic<int32_t> sound_mode{1};
@@ -156,12 +157,14 @@ int32_t sdrg_ssb_processor_create(int32_t device, int32_t queue_max, sdrg_ssb_pr
 
 int32_t sdrg_ssb_processor_stop(sdrg_ssb_processor *p) {
     if (!p) return fail(SDRG_E_INVALID, "null processor");
-    if (!p->running.load()) return SDRG_OK;  // stopProcessing (:40-49)
     {
         std::lock_guard<std::mutex> lk(p->mu);
-        p->running.store(false);
+        p->running.store(false);  // stopProcessing (:40-49)
     }
     p->cv.notify_one();
+    // a callback on the worker thread that stops its own processor cannot join itself: the loop ends after it
+    if (p->worker.joinable() && p->worker.get_id() == std::this_thread::get_id()) return SDRG_OK;
+    std::lock_guard<std::mutex> jl(p->join_mu);  // one joiner at a time
     if (p->worker.joinable()) p->worker.join();
     return SDRG_OK;
 }
@@ -177,6 +180,12 @@ int32_t sdrg_ssb_processor_destroy(sdrg_ssb_processor *p) {
 int32_t sdrg_ssb_processor_start(sdrg_ssb_processor *p, const sdrg_ssb_callbacks *cbs) {
     if (!p) return fail(SDRG_E_INVALID, "null processor");
     if (p->running.load()) return SDRG_OK;  // "SSB processing already running" (:28-31)
+    if (p->worker.joinable()) {  // a loop stopped from its own callback has ended or is ending: reap it
+        if (p->worker.get_id() == std::this_thread::get_id())
+            return fail(SDRG_E_INVALID, "start from the worker's own callback");
+        std::lock_guard<std::mutex> jl(p->join_mu);
+        if (p->worker.joinable()) p->worker.join();
+    }
     p->cbs = cbs ? *cbs : sdrg_ssb_callbacks{};
     p->running.store(true);
     p->worker = std::thread([p] { p->loop(); });

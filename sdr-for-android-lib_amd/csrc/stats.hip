@@ -1100,8 +1100,8 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
     const int pool_stride = (geo.max_pool + 3) & ~3;
     if (wide_for(geo)) {
         size_t lds = sizeof(float) * (size_t)RING_FLOATS;
-        if (SDRG_STATS_STAMPS && getenv("SDRG_STATS_LDS_KB")) {  // diagnostic: fewer frames per CU
-            lds = (size_t)atoi(getenv("SDRG_STATS_LDS_KB")) * 1024;
+        if (SDRG_STATS_STAMPS && lab_getenv("SDRG_STATS_LDS_KB")) {  // diagnostic: fewer frames per CU
+            lds = (size_t)atoi(lab_getenv("SDRG_STATS_LDS_KB")) * 1024;
             hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(stats_wide_kernel), (int)lds);
             if (e != hipSuccess) return e;
         }

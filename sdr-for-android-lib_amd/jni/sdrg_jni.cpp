@@ -7,7 +7,6 @@
 #include <jni.h>
 
 #include <chrono>
-#include <mutex>
 
 #include "sdrg_jni_bridge.hpp"
 
@@ -69,8 +68,9 @@ struct RealJni {
     }
 };
 
-std::mutex g_mu;  // the JVM thread (setters) and the rx thread (frames) share the bridge
-sdrg::jni::Bridge<RealJni> g_bridge;
+// the JVM thread (setters), the rx thread (frames) and the SSB worker's callbacks share the bridge; LockedBridge
+// serialises them and joins the worker outside its lock
+sdrg::jni::LockedBridge<RealJni> g_bridge;
 
 int64_t now_ms() {
     return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -81,14 +81,12 @@ int64_t now_ms() {
 
 // Called by the bridge's rx_process_thread for each exact-N chunk (replaces soapyCallback).
 extern "C" void sdrg_jni_on_frame(JNIEnv *env, const std::complex<float> *buf, uint32_t len) {
-    std::lock_guard<std::mutex> lk(g_mu);
     g_bridge.onFrame(env, buf, len, now_ms());
 }
 
 extern "C" JNIEXPORT jboolean JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_applyConfig(
     JNIEnv *env, jobject, jlong cf, jlong fs, jint n, jint focus, jint gain, jlong rfft, jlong rpeak, jlong rss,
     jint mode) {
-    std::lock_guard<std::mutex> lk(g_mu);
     return g_bridge.applyConfig(env, cf, fs, n, focus, gain, rfft, rpeak, rss, mode) ? JNI_TRUE : JNI_FALSE;
 }
 
@@ -96,25 +94,21 @@ extern "C" JNIEXPORT void JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_read(
     JNIEnv *env, jobject, jobject fft, jobject detectionFlag, jobject meanSnr, jobject meanSnrSigma,
     jobject peakFrequency, jobject pcm, jobject audioPulse, jobject peakAboveNoiseMean, jobject maxBin,
     jobject best1kHz, jobject spectralPulse, jobject noiseLevel) {
-    std::lock_guard<std::mutex> lk(g_mu);
     const jobject cbs[] = {fft, detectionFlag, meanSnr, meanSnrSigma, peakFrequency, pcm, audioPulse,
                            peakAboveNoiseMean, maxBin, best1kHz, spectralPulse, noiseLevel};
     g_bridge.read(env, cbs);
 }
 
 extern "C" JNIEXPORT void JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_stopReading(JNIEnv *env, jobject) {
-    std::lock_guard<std::mutex> lk(g_mu);
     g_bridge.stopReading(env);
 }
 
 extern "C" JNIEXPORT void JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_close(JNIEnv *env, jobject) {
-    std::lock_guard<std::mutex> lk(g_mu);
     g_bridge.close(env);
 }
 
 #define SDRG_JNI_SETTER(NAME, JT, CALL)                                                                    \
     extern "C" JNIEXPORT void JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_##NAME(JNIEnv *env, jobject, JT v) { \
-        std::lock_guard<std::mutex> lk(g_mu);                                                              \
         g_bridge.CALL(env, v);                                                                             \
     }
 SDRG_JNI_SETTER(setFrequency, jlong, setFrequency)
@@ -129,17 +123,14 @@ SDRG_JNI_SETTER(setRefreshSignalStrengthMs, jlong, setRefreshSignalStrengthMs)
 
 extern "C" JNIEXPORT void JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_setPulseConfig(
     JNIEnv *env, jobject, jfloat, jfloat, jfloat, jfloat, jfloat, jfloat, jfloat, jfloat, jfloat) {
-    std::lock_guard<std::mutex> lk(g_mu);
     g_bridge.setPulseConfig(env);
 }
 
 extern "C" JNIEXPORT jfloat JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_getAmbientAudioEnergy(JNIEnv *env, jobject) {
-    std::lock_guard<std::mutex> lk(g_mu);
     return g_bridge.getAmbientAudioEnergy(env);
 }
 
 // getCurrentAudioRatio (sdr-bridge-java-soapy.cpp:1168-1171): ssbProcessor.getCurrentRatio(), always 0
 extern "C" JNIEXPORT jfloat JNICALL Java_fr_intuite_sdr_bridge_SDRBridge_getCurrentAudioRatio(JNIEnv *env, jobject) {
-    std::lock_guard<std::mutex> lk(g_mu);
     return g_bridge.getCurrentAudioRatio(env);
 }

@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <complex>
 #include <cstdint>
+#include <mutex>
 #include <vector>
 
 #include "../../include/sdrg.h"
@@ -145,6 +146,22 @@ public:
         if (ssb_) sdrg_ssb_processor_stop(ssb_);
     }
 
+    // two-phase stop for callers that serialise the bridge behind a lock (LockedBridge below): under the lock,
+    // stop reading and hand out the SSB processor; the caller stops (joins) it after releasing the lock, so
+    // callbacks running on the worker can still enter the bridge
+    sdrg_ssb_processor *beginStopReading() {
+        reading_ = false;
+        return ssb_;
+    }
+    sdrg_ssb_processor *ssbHandle() const { return ssb_; }
+    // close(), first phase: the processor leaves the bridge (the caller destroys it outside the lock)
+    sdrg_ssb_processor *detachSsb() {
+        reading_ = false;
+        sdrg_ssb_processor *p = ssb_;
+        ssb_ = nullptr;
+        return p;
+    }
+
     void close(Env *env) {
         reading_ = false;
         if (ssb_) sdrg_ssb_processor_destroy(ssb_);
@@ -246,6 +263,81 @@ private:
     std::vector<int16_t> pcm_;
     sdrg_frame_record rec_{};
     sdrg_pulse_output spectral_{}, audio_{};
+};
+
+// The bridge behind one mutex, as the JNI exports use it: the JVM thread (setters, read, stopReading, close), the
+// rx thread (frames) and the SSB worker's callbacks (which may call back into the bridge, e.g.
+// getAmbientAudioEnergy or setSoundMode from a pcm listener) share it.  Joining the SSB worker never happens
+// under the mutex -- a worker blocked in a re-entrant call would never return and the join would deadlock (the
+// reference takes no lock around ssbProcessor.stopProcessing, sdr-bridge-java-soapy.cpp:766-793).
+template <class J>
+class LockedBridge {
+public:
+    using Br = Bridge<J>;
+    using Env = typename J::Env;
+    using Obj = typename J::Obj;
+
+    bool applyConfig(Env *env, int64_t cf, int64_t fs, int32_t n, int32_t focus, int32_t gain, int64_t rfft,
+                     int64_t rpeak, int64_t rss, int32_t mode) {
+        std::lock_guard<std::mutex> lk(mu_);
+        return b_.applyConfig(env, cf, fs, n, focus, gain, rfft, rpeak, rss, mode);
+    }
+    void read(Env *env, const Obj (&cbs)[Br::N_CALLBACKS]) {
+        stopWorker();  // read() replaces the callback table the worker reads
+        std::lock_guard<std::mutex> lk(mu_);
+        b_.read(env, cbs);
+    }
+    void onFrame(Env *env, const std::complex<float> *buf, uint32_t len, int64_t now_ms) {
+        std::lock_guard<std::mutex> lk(mu_);
+        b_.onFrame(env, buf, len, now_ms);
+    }
+    void stopReading(Env *) {
+        sdrg_ssb_processor *p;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            p = b_.beginStopReading();
+        }
+        if (p) sdrg_ssb_processor_stop(p);
+    }
+    void close(Env *env) {
+        sdrg_ssb_processor *p;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            p = b_.detachSsb();
+        }
+        if (p) sdrg_ssb_processor_destroy(p);  // joins the worker; its callbacks still see valid global refs
+        std::lock_guard<std::mutex> lk(mu_);
+        b_.close(env);
+    }
+    // setters and getters: short, under the lock
+    template <class F>
+    auto with(F f) -> decltype(f(std::declval<Br &>())) {
+        std::lock_guard<std::mutex> lk(mu_);
+        return f(b_);
+    }
+    void setFrequency(Env *e, int64_t v) { with([&](Br &b) { b.setFrequency(e, v); }); }
+    void setSampleRate(Env *e, int64_t v) { with([&](Br &b) { b.setSampleRate(e, v); }); }
+    void setSamplesPerReading(Env *e, int32_t v) { with([&](Br &b) { b.setSamplesPerReading(e, v); }); }
+    void setFrequencyFocusRange(Env *e, int32_t v) { with([&](Br &b) { b.setFrequencyFocusRange(e, v); }); }
+    void setSoundMode(Env *e, int32_t v) { with([&](Br &b) { b.setSoundMode(e, v); }); }
+    void setRefreshFFTMs(Env *e, int64_t v) { with([&](Br &b) { b.setRefreshFFTMs(e, v); }); }
+    void setRefreshPeakMs(Env *e, int64_t v) { with([&](Br &b) { b.setRefreshPeakMs(e, v); }); }
+    void setRefreshSignalStrengthMs(Env *e, int64_t v) { with([&](Br &b) { b.setRefreshSignalStrengthMs(e, v); }); }
+    void setPulseConfig(Env *e) { with([&](Br &b) { b.setPulseConfig(e); }); }
+    float getAmbientAudioEnergy(Env *e) { return with([&](Br &b) { return b.getAmbientAudioEnergy(e); }); }
+    float getCurrentAudioRatio(Env *e) { return with([&](Br &b) { return b.getCurrentAudioRatio(e); }); }
+
+private:
+    void stopWorker() {
+        sdrg_ssb_processor *p;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            p = b_.ssbHandle();
+        }
+        if (p) sdrg_ssb_processor_stop(p);
+    }
+    std::mutex mu_;
+    Br b_;
 };
 
 }  // namespace jni

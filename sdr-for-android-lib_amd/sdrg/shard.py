@@ -5,7 +5,8 @@ so the path shards by stream with no data-path collective: rank r owns streams [
 own engine on its own GPU (weak scaling).  The one collective is the per-step gather of the 72-byte frame
 records to rank 0; spectra and PCM stay on the GPU that produced them.  A consumer that
 wants spectra on rank 0 gathers the focus-window slice of each frame (gather_focus: 82 bins of 16384 at
-2 MHz / 5 kHz, 0.5 % of the bytes) rather than the 268 MB of full spectra per GPU per step.
+2 MHz / 5 kHz, 0.5 % of the bytes) rather than the 268 MB of full spectra per GPU per step; gather_spectra moves
+the full spectra (the fftCallback payload, sdr-bridge-java-soapy.cpp:456-465) when a consumer needs them all.
 """
 from __future__ import annotations
 
@@ -55,3 +56,12 @@ def gather_focus(spectra, first_bin: int, n_bins: int, world: int, rank: int, ds
         staging = torch.empty((spectra.shape[0], n_bins), dtype=spectra.dtype, device=spectra.device)
     staging.copy_(sl)
     return gather_records(staging, world, rank, dst=dst, group=group, out=out)
+
+
+def gather_spectra(spectra, world: int, rank: int, dst: int = 0, group=None, out=None):
+    """Gather each rank's full [B, N] fftshifted spectra (the fftCallback payload of every frame,
+    sdr-bridge-java-soapy.cpp:456-465) to `dst` as [world*B, N] float32 in global stream order: 4*N bytes per
+    frame (268 MB per rank at 4096 x 16384).  Returns the result on dst, None elsewhere."""
+    if not spectra.is_contiguous():
+        raise ValueError("gather_spectra needs contiguous [B, N] spectra")
+    return gather_records(spectra, world, rank, dst=dst, group=group, out=out)

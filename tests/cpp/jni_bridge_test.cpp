@@ -4,11 +4,17 @@
 // callback's arguments against a second engine driven directly through the C ABI on the same frames:
 // the order is soapyCallback's (sdr-bridge-java-soapy.cpp:458-488) then the SSB worker's
 // (ssb_processor.cpp:105-113), and every value is bit-identical.  Prints "OK ..." and exits 0 on success.
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <complex>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sdrg_jni_bridge.hpp"
@@ -35,6 +41,7 @@ struct FakeVm {
     int attaches = 0, detaches = 0;
 };
 FakeVm g_vm;
+std::function<void()> g_worker_hook;  // runs inside the SSB worker's pcm callback (re-entrancy test)
 
 struct FakeJni {
     using Env = FakeEnv;
@@ -63,6 +70,7 @@ struct FakeJni {
         e->log.push_back({o->id, m, {}, std::vector<float>(p, p + n), {}});
     }
     static void CallShorts(Env *e, Obj o, Mid m, const int16_t *p, int32_t n) {
+        if (e == &g_vm.worker_env && g_worker_hook) g_worker_hook();
         e->log.push_back({o->id, m, {}, {}, std::vector<int16_t>(p, p + n)});
     }
 };
@@ -158,6 +166,69 @@ int queued_phase() {
     return 0;
 }
 
+// The JNI exports' lock discipline (sdrg::jni::LockedBridge): a pcm listener on the SSB worker thread that calls
+// back into the bridge (getAmbientAudioEnergy, setSoundMode) while the JVM thread runs stopReading or close must
+// not deadlock -- the worker is joined outside the bridge's lock.  A watchdog fails the test after 10 s instead of
+// hanging.
+bool wait_for(const std::atomic<int> &flag, int ms) {
+    for (int i = 0; i < ms && !flag.load(); i++) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    return flag.load() != 0;
+}
+
+int reentrant_phase() {
+    const int n = 4096;
+    const int64_t fs = 2000000, cf = 100000000;
+    FakeEnv env, env2;
+    g_vm = FakeVm{};
+    sdrg::jni::LockedBridge<FakeJni> lb;
+    if (!lb.applyConfig(&env, cf, fs, n, 5, 10, 50, 200, 30, 1)) return 22;
+    FakeObj objs[B::N_CALLBACKS];
+    B::Obj cbs[B::N_CALLBACKS];
+    for (int i = 0; i < B::N_CALLBACKS; i++) {
+        objs[i].id = i;
+        cbs[i] = &objs[i];
+    }
+    std::vector<std::complex<float>> buf(n);
+    uint64_t x = 4242;
+    std::atomic<int> in_cb{0}, reentered{0};
+    g_worker_hook = [&] {
+        in_cb.store(1);
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));  // the JVM thread's stop starts meanwhile
+        (void)lb.getAmbientAudioEnergy(&env2);
+        lb.setSoundMode(&env2, 1);
+        reentered.fetch_add(1);
+    };
+    for (int round = 0; round < 2; round++) {  // 0: stopReading, 1: close
+        in_cb.store(0);
+        lb.read(&env, cbs);
+        synth(buf, round, n, fs, x);
+        lb.onFrame(&env, buf.data(), n, 1000 + round);
+        if (!wait_for(in_cb, 10000)) {
+            std::fprintf(stderr, "FAIL reentrant round %d: the worker never called pcm\n", round);
+            return 23;
+        }
+        std::atomic<int> done{0};
+        std::thread t([&] {
+            if (round == 0)
+                lb.stopReading(&env);
+            else
+                lb.close(&env);
+            done.store(1);
+        });
+        if (!wait_for(done, 10000)) {
+            std::fprintf(stderr, "FAIL reentrant round %d: %s deadlocked with a re-entrant pcm callback\n", round,
+                         round == 0 ? "stopReading" : "close");
+            std::fflush(stderr);
+            _exit(9);
+        }
+        t.join();
+        CHECK(reentered.load() == round + 1, "reentrant round %d: %d re-entries", round, reentered.load());
+    }
+    g_worker_hook = nullptr;
+    CHECK(env.global_refs == 0, "reentrant global refs after close %d", env.global_refs);
+    return 0;
+}
+
 int main() {
     const int n = 4096, frames = 180;
     const int64_t fs = 2000000, cf = 100000000;
@@ -242,8 +313,10 @@ int main() {
     if (fails) return 1;
     const int q = queued_phase();
     if (q) return q;
+    const int r = reentrant_phase();
+    if (r) return r;
     if (fails) return 1;
-    std::printf("OK %d frames, %d callbacks each, spectral live %d, audio live %d; queued SSB worker OK\n", frames, 12,
+    std::printf("OK %d frames, %d callbacks each, spectral live %d, audio live %d; queued SSB worker OK; re-entrant stop/close OK\n", frames, 12,
                 sp.live_etat, ap.live_etat);
     return 0;
 }

@@ -100,3 +100,16 @@ def test_jni_bridge_and_dropins_compile(tmp_path):
     for src in ("jni_bridge_test.cpp", "compat_main.cpp", "compat_pulse.cpp"):
         subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", f"-I{inc}", f"-I{jni}",
                         os.path.join(ROOT, "tests", "cpp", src)], check=True)
+
+
+def test_product_library_reads_no_lab_knobs():
+    """The lab environment knobs exist only in -DSDRG_LAB=1 builds: the product library neither imports getenv nor
+    carries a knob's name (tests/test_gpu_lab_knobs.py checks the behaviour on the GPU)."""
+    import sdrg
+    dyn = subprocess.run(["nm", "-D", "--undefined-only", sdrg.lib_path()], capture_output=True, text=True,
+                         check=True).stdout
+    assert "getenv" not in dyn
+    blob = open(sdrg.lib_path(), "rb").read()
+    for knob in (b"SDRG_PIPE_SKIP", b"SDRG_PIPE_MAP", b"SDRG_CU_SPLIT", b"SDRG_PIPE_PRIO", b"SDRG_SPECTRUM_GRID",
+                 b"SDRG_SSB_REFERENCE_KERNELS", b"SDRG_STREAM_PRIO", b"SDRG_EVENT_FENCE", b"SDRG_PIPE_STAMPS"):
+        assert knob not in blob, knob

@@ -221,3 +221,25 @@ def test_engines_in_concurrent_threads(S, O):
         for f in range(2):
             for a, b in zip(results[k][f], want[f]):
                 assert a.tobytes() == b.tobytes()  # records included: their tail padding is written as zeros
+
+
+def test_dynamic_lds_limit_survives_large_small_large(S, O):
+    """The max-dynamic-LDS attribute is one limit per (kernel, device): the engine only ever raises it
+    (csrc/engine.cpp ensure_dynamic_lds), so a large, small, large sequence of frame sizes on ONE engine (the any-N
+    FFT kernels size their LDS from N; 12288 points need more than the 64 KiB default) keeps every launch valid and
+    every call's spectrum and records equal to a fresh engine's."""
+    fs = 2_000_000
+    eng = engine(S, 12288, fs, 2)
+    for k, n in enumerate((12288, 1536, 12288, 6144, 12288)):
+        cfg = S.SDRConfig(centerFrequency=100_000_000, samplesPerReading=n, sampleRate=fs, freqFocusRangeKhz=5,
+                          soundMode=1)
+        assert eng.applyConfig(cfg)
+        raw = np.stack([O.synth_frames(1, n, O.CS8, tone_hz=900.0 + 300 * b, fs=fs, seed=10 * k + b)[0]
+                        for b in range(2)])
+        spec, rec, _ = eng.process(raw, fmt=S.CS8, stages=S.STAGE_SPECTRUM | S.STAGE_STATS, now_ms=1000 + k)
+        fresh = engine(S, n, fs, 2)
+        spec1, rec1, _ = fresh.process(raw, fmt=S.CS8, stages=S.STAGE_SPECTRUM | S.STAGE_STATS, now_ms=1000 + k)
+        fresh.close()
+        assert spec.tobytes() == spec1.tobytes(), n
+        np.testing.assert_array_equal(rec["peak_bin"], rec1["peak_bin"])
+    eng.close()
