@@ -26,9 +26,12 @@ def O():
                                            ("CS8", 1000, 2_000_000), ("CU8", 1500, 2_400_000),
                                            ("CS16", 4096, 2_000_000), ("CF32", 1000, 2_500_000),
                                            ("CF32", 4096, 2_000_000)])
-def test_ssb_schedule_edges_vs_oracle(S, O, fmt_name, n, fs):
+@pytest.mark.parametrize("B", [21, 45])
+def test_ssb_schedule_edges_vs_oracle(S, O, fmt_name, n, fs, B):
     fmt = getattr(O, fmt_name)
-    B, F = 21, 4  # 21 streams: one full and one partial workgroup of 16
+    # 21 streams: one workgroup of 32 with its second 16-stream group partly live (16 + 5); 45: a full workgroup and
+    # one of 13 streams whose second group is empty (lab builds of 16-stream workgroups: 1 full + 1 partial, 2 + 1)
+    F = 4
     raw = np.stack([O.synth_frames(F, n, fmt, tone_hz=300.0 * (b + 1) - 3000.0, fs=fs, seed=77 + b) for b in range(B)])
     cfg = S.SDRConfig(centerFrequency=100_000_000, samplesPerReading=n, sampleRate=fs, freqFocusRangeKhz=5,
                       soundMode=1)

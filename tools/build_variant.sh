@@ -11,7 +11,7 @@ CXX="g++ -O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -D__HIP_PLATFORM_
 $HIP -I$D/csrc -Iinclude -c ${SPECTRUM_SRC:-$D/csrc/spectrum.hip} -o $B/spectrum.o
 $HIP -c $D/csrc/fftany.hip -o $B/fftany.o
 $HIP -I$D/csrc -Iinclude -ffp-contract=off -fno-slp-vectorize -c ${STATS_SRC:-$D/csrc/stats.hip} -o $B/stats.o
-$HIP -ffp-contract=off -fno-slp-vectorize -c $D/csrc/ssb.hip -o $B/ssb.o
+$HIP -I$D/csrc -Iinclude -ffp-contract=off -fno-slp-vectorize -c ${SSB_SRC:-$D/csrc/ssb.hip} -o $B/ssb.o
 $HIP -ffp-contract=off -c $D/csrc/pulse.hip -o $B/pulse.o
 for f in design engine pulse_bank ingest compat ssb_processor; do $CXX -c $D/csrc/$f.cpp -o $B/$f.o; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/lib/libsdrg_$NAME.so $B/spectrum.o $B/fftany.o $B/stats.o \

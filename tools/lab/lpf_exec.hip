@@ -1,5 +1,5 @@
 // Lab: the low-pass step (2 v_pk_mul_f32 + 4 dependent v_add_f32 per sample) on registers only, one wave alone:
-// operand order of the dependent adds (running value as src0 or src1) x EXEC (64 lanes or 16), s_memtime cycles
+// operand order of the dependent adds (running value as src0 or src1) x EXEC pattern, s_memtime cycles
 // per sample.  Build: hipcc --offload-arch=gfx950 -O3 -o tools/lab/lpf_exec tools/lab/lpf_exec.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -21,11 +21,11 @@ constexpr int REP = 512;
     "v_add_f32 v" #Y ", v7, v8\n"
 #define BODY(S) S(0, 2, 2) S(2, 0, 0) S(0, 2, 2) S(2, 0, 0) S(0, 2, 2) S(2, 0, 0) S(0, 2, 2) S(2, 0, 0)
 
-template <int V, int LANES>
+template <int V, unsigned long long MASK>
 __global__ void k(unsigned long long *out) {
     const int lane = threadIdx.x & 63;
     unsigned long long t0 = 0, t1 = 0;
-    if (lane < LANES) {
+    if ((MASK >> lane) & 1) {
         asm volatile("v_mov_b32 v0, 0.5\n v_mov_b32 v2, 0.25\n v_mov_b32 v10, 0.125\n v_mov_b32 v20, 0.5\n v_mov_b32 v21, -0.25\n"
                      "v_mov_b32 v22, 0.125\n v_mov_b32 v23, -0.0625\n" ::: "v0", "v2", "v10", "v20", "v21", "v22", "v23");
         t0 = __builtin_amdgcn_s_memtime();
@@ -35,22 +35,29 @@ __global__ void k(unsigned long long *out) {
         }
         t1 = __builtin_amdgcn_s_memtime();
     }
-    if (threadIdx.x == 0) out[0] = t1 - t0;
+    if (lane == __builtin_ctzll(MASK)) out[0] = t1 - t0;
 }
-template <int V, int LANES>
+template <int V, unsigned long long MASK>
 void run(const char *name, unsigned long long *d) {
     unsigned long long h = 0;
-    for (int r = 0; r < 3; r++) k<V, LANES><<<1, 64>>>(d);
+    for (int r = 0; r < 3; r++) k<V, MASK><<<1, 64>>>(d);
     if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    printf("%-28s lanes %2d: %6.2f cyc/sample\n", name, LANES, h / (double)(REP * 8));
+    printf("%-28s exec %016llx: %6.2f cyc/sample\n", name, MASK, h / (double)(REP * 8));
 }
 int main() {
     unsigned long long *d;
     if (hipMalloc(&d, 64) != hipSuccess) return 2;
-    run<0, 64>("running value as src0", d);
-    run<1, 64>("running value as src1", d);
-    run<0, 16>("running value as src0", d);
-    run<1, 16>("running value as src1", d);
-    run<0, 1>("running value as src0", d);
+    run<0, ~0ull>("running value as src0", d);
+    run<1, ~0ull>("running value as src1", d);
+    run<0, 0xffffull>("running value as src0", d);
+    run<1, 0xffffull>("running value as src1", d);
+    run<0, 1ull>("running value as src0", d);
+    // 16 lanes spread over the four 16-lane quarters (4 each / 1 in 4), 32 lanes (two quarters / spread)
+    run<0, 0x000f000f000f000full>("running value as src0", d);
+    run<0, 0x1111111111111111ull>("running value as src0", d);
+    run<0, 0x0001000100010001ull>("running value as src0", d);
+    run<0, 0xffffffffull>("running value as src0", d);
+    run<0, 0x00ff00ff00ff00ffull>("running value as src0", d);
+    run<0, 0x5555555555555555ull>("running value as src0", d);
     return 0;
 }
