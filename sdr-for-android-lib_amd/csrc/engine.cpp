@@ -734,14 +734,11 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         hipStreamCreateWithPriority(&e->s_ssb, hipStreamNonBlocking, prio_ssb) != hipSuccess)
         return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
     e->s_main = e->s_own;
-    // CU split: with 32-stream SSB workgroups (one per CU, 135 KiB of LDS: nothing else fits beside one) the SSB
-    // stream runs on one half of the CUs and the spectrum / statistics stream on the other, so the latency-bound
-    // SSB pipeline and the issue/HBM-bound spectrum never share a SIMD.  Mode 2: CU-mask bits [0, ncu/2) for the
-    // SSB, the rest for the spectrum; mode 1: even / odd bits; 0: no split (lab: SDRG_CU_SPLIT).
-    int split_mode = ssb_pipe_streams_per_workgroup() == 32 ? 2 : 0;
-    if (const char *v = lab_getenv("SDRG_CU_SPLIT")) split_mode = atoi(v);
-    {
-        const int mode = split_mode;
+    // lab: SDRG_CU_SPLIT = 1 (SSB on even CU-mask bits, spectrum/statistics on odd) or 2 (low / high half): the
+    // SSB stream and the spectrum / statistics stream on disjoint CUs.  (32-stream SSB workgroups on half the CUs
+    // with the spectrum on the other half measured slower than co-residency: DESIGN.md 3.3.)
+    if (const char *v = lab_getenv("SDRG_CU_SPLIT")) {
+        const int mode = atoi(v);
         const int ncu = prop.multiProcessorCount;
         if ((mode == 1 || mode == 2) && ncu >= 2) {
             std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);

@@ -80,7 +80,6 @@ void ssb_report_stamps();  // diagnostic (SDRG_PIPE_STAMPS=1)
 // chunk_table: per chunk of ssb_pipe_chunk() samples {first, last output overlapping it, first, last output
 // completed in it} (host-computed, see engine.cpp); may be null (reference kernels).
 int ssb_pipe_chunk(void);
-int ssb_pipe_streams_per_workgroup(void);  // streams per SSB pipeline workgroup (16 or 32)
 // audio (nullable): run the audio pulse detector's front end on the PCM as it is produced
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,

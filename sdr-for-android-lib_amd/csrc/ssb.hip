@@ -331,16 +331,7 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 #ifndef SDRG_AGC_ASM
 #define SDRG_AGC_ASM 2
 #endif
-// streams per workgroup: 16 (the product: one workgroup per CU on every CU, co-resident with one spectrum
-// workgroup) or 32 (lab, -DSDRG_PIPE_PG=32: one workgroup per CU on the SSB stream's half of the CUs, the spectrum
-// and statistics on the other half, the serial waves on 32 lanes; measured 44 % more cycles per frame than 16,
-// its helper waves doing twice the work each: DESIGN.md 3.3)
-#ifndef SDRG_PIPE_PG
-#define SDRG_PIPE_PG 16
-#endif
-constexpr int PG = SDRG_PIPE_PG;
-static_assert(PG == 16 || PG == 32, "16 or 32 streams per workgroup");
-constexpr int NG = PG / 16;     // 16-stream groups: the loader, clamp and FIR waves each serve one group
+constexpr int PG = 16;          // streams per workgroup
 // serial roles (bit 0 DC, 1 LPF, 2 AGC) that run on all 64 lanes (16 copies of the 16 streams) instead of the
 // first 16: a dependent VALU chain issues faster with the full EXEC mask, while the LDS reads of 16 copies cost
 // more LDS cycles (tools/microbench/valu5.hip, valu6.hip; tools/build_variant.sh for the trade per role)
@@ -350,19 +341,16 @@ constexpr int NG = PG / 16;     // 16-stream groups: the loader, clamp and FIR w
 constexpr int CH = 64;          // samples per chunk
 constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_read_b128 by stream lanes
 constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
-constexpr int PIPE_WAVES = 12 + 4 * (NG - 1);  // 16 at PG = 32: a second loader and clamp wave, two more FIR waves
+constexpr int PIPE_WAVES = 12;
 constexpr int PIPE_T = PIPE_WAVES * 64;
 enum PipeWave : int { W_DC = 0, W_LPF = 1, W_AGC = 2, W_LOAD = 3, W_FIR0 = 4, W_OUT = 5, W_EQ = 6, W_FIR1 = 7,
-                      W_DES0 = 8, W_DES1 = 9, W_DES2 = 10, W_DES3 = 11,
-                      W_LOAD1 = 12, W_OUT1 = 13, W_FIR2 = 14, W_FIR3 = 15 };
-// role of hardware wave w = nibble w (hardware wave w runs on SIMD w % 4)
-//   PG 16: w0 DC, w1 LPF, w2 AGC, w3 load, w4 OUT, w5 EQ, w6 DES2, w7 FIR0, w8 DES0, w9 DES1, w10 DES3, w11 FIR1
-//   PG 32: SIMD0 DC, FIR0, DES0, OUT1 | SIMD1 LPF, OUT, DES1, EQ | SIMD2 AGC, FIR1, DES2, DES3 |
-//          SIMD3 load, load1, FIR2, FIR3
-constexpr unsigned long long DEFAULT_ROLE_MAP = PG == 16 ? 0x7B984A653210ull : 0xFB6DEA98C7543210ull;
+                      W_DES0 = 8, W_DES1 = 9, W_DES2 = 10, W_DES3 = 11 };
+// role of hardware wave w = nibble w: w0 DC, w1 LPF, w2 AGC, w3 load, w4 OUT, w5 EQ, w6 DES2, w7 FIR0,
+// w8 DES0, w9 DES1, w10 DES3, w11 FIR1
+constexpr unsigned long long DEFAULT_ROLE_MAP = 0x7B984A653210ull;
 constexpr int MAX_SLOTS = 32;   // concurrent FIR outputs per stream (up to 4 per FIR lane)
 constexpr int MAX_DONE = 8;     // FIR outputs completed per stream per chunk
-constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU (PG 16, static LDS)
+constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
 
 constexpr int TAPS_ROW = CH + 256 + CH + 4;
 // The low-pass wave one chunk behind the DC wave's output (1): its input ring gets a third slot and the wave runs
@@ -378,12 +366,12 @@ constexpr int LA = SDRG_LPF_LOOKAHEAD ? 1 : 0;
 #define SDRG_LPF_INTERLEAVE 1
 #endif
 constexpr int NA = 2 + LA;  // slots of the DC -> low-pass ring
-#ifndef SDRG_PIPE_RAWB  // bytes of raw IQ per stream per prefetch batch (PG 32: 128, the NCO variant's tables fit)
-#define SDRG_PIPE_RAWB (SDRG_PIPE_PG == 32 ? 128 : SDRG_LPF_LOOKAHEAD ? 256 : 512)
+#ifndef SDRG_PIPE_RAWB  // bytes of raw IQ per stream per prefetch batch
+#define SDRG_PIPE_RAWB (SDRG_LPF_LOOKAHEAD ? 256 : 512)
 #endif
 constexpr int RAWB = SDRG_PIPE_RAWB;
 constexpr int RAW_PIECES = RAWB / 64;     // 16-B LDS-DMA pieces per loader lane (lane = 4 x stream + quarter)
-constexpr int RAW_U4 = 16 * RAWB / 16;    // one 16-stream group's prefetch batch as [piece][lane 64] uint4
+constexpr int RAW_U4 = PG * RAWB / 16;    // one prefetch batch as [piece][lane 64] uint4
 
 template <int FMT>
 constexpr int batch_chunks() {  // chunks per RAWB-per-stream prefetch batch (DMA needs CH * bps <= RAWB)
@@ -401,37 +389,26 @@ constexpr int batch_chunks() {  // chunks per RAWB-per-stream prefetch batch (DM
 #ifndef SDRG_PIPE_DYN_LDS
 #define SDRG_PIPE_DYN_LDS 1
 #endif
-#ifndef SDRG_PIPE_MINW  // waves per SIMD the VGPR budget must allow: 6 -> at most 80 VGPRs (PG 32: 4, 128)
-#define SDRG_PIPE_MINW (PG == 16 ? 6 : 4)
+#ifndef SDRG_PIPE_MINW  // waves per SIMD the VGPR budget must allow: 6 -> at most 80 VGPRs
+#define SDRG_PIPE_MINW 6
 #endif
 constexpr int NRAW = SDRG_PIPE_NRAW;  // raw-IQ batches in LDS: one being unpacked, NRAW - 1 in flight
 
-// The y ring carries the low-pass output: slot c % YR is written by the low-pass wave (iteration c + 2 + LA), read by
-// the desired waves (c + 3 + LA) and the clamp waves (c + 5 + LA).  16-stream workgroups: 4 slots, and the clamped
-// AGC output goes to a 2-slot out ring the FIR reads (c + 6 + LA).  32-stream workgroups (LDS for the NCO tables):
-// 5 slots, and the clamp writes its output in place over the y values it read, for the FIR (c + 6 + LA), before
-// the slot is reused for chunk c + 5 (c + 7 + LA).
-constexpr int YR = PG == 16 ? 4 : 5;
-__device__ __forceinline__ int yslot(int c) { return YR == 4 ? (c & 3) : c % YR; }  // c >= 0
 struct PipeLds {
-    uint4 raw[NRAW][NG][RAW_U4];  // raw IQ bytes of the prefetch batches (LDS-DMA), [group][piece][loader lane]
+    uint4 raw[NRAW][RAW_U4];  // raw IQ bytes of the prefetch batches (LDS-DMA), [piece][loader lane]
     float re[2][BUFF];
     float a[NA][BUFF];
-    float y[YR][BUFF];
+    float y[4][BUFF];
     float d[2][BUFF];
     float g[2][BUFF];
-#if SDRG_PIPE_PG == 16
     float out[2][BUFF];
-#endif
     float fq[2][PG * MAX_DONE];
     // taps with CH zeros on both sides (out-of-window FIR steps multiply by 0), in 4 copies shifted by
     // 0..3 floats so that any 32-tap window is read with aligned ds_read_b128
     float taps_sh[4][TAPS_ROW];
 };
 // NCO variant only, in dynamic LDS: the phasor tables, then the current chunk's CH phasors {re, im}
-constexpr int NCO_LDS_BYTES = (2 * 1024 * 2 + 2 * CH * NG) * 4;  // + each loader wave's chunk phasors
-
-static_assert(sizeof(PipeLds) + NCO_LDS_BYTES <= 160 * 1024, "the pipeline's LDS (with the NCO tables) fits a CU");
+constexpr int NCO_LDS_BYTES = (2 * 1024 * 2 + 2 * CH) * 4;
 
 // LDS byte address of a pointer into the workgroup's LDS (for asm operands)
 __device__ __forceinline__ uint32_t lds_addr(const float *p) {
@@ -522,11 +499,7 @@ __device__ __forceinline__ void fir_chunk(PipeLds &L, int c, int t0, int o_lo, i
         if (active[j] && base >= t0) acc[J0 + j] = 0.0f;
         k0[j] = active[j] ? (t0 - base + CH) : 0;  // taps_pad index of step 0 (inactive: the zero padding)
     }
-#if SDRG_PIPE_PG == 16
     const float4 *in = reinterpret_cast<const float4 *>(&L.out[c & 1][sl * ROW]);  // 0 beyond frame end
-#else
-    const float4 *in = reinterpret_cast<const float4 *>(&L.y[yslot(c)][sl * ROW]);  // clamped; 0 beyond frame end
-#endif
 #pragma unroll 4
     for (int i = 0; i < CH / 4; i++) {
         const float4 x = in[i];
@@ -593,14 +566,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     const size_t bps = bytes_per_sample<FMT>();
     const int n_live = min(p.n_in, S);
 
-    // raw-IQ prefetch of the loader waves (one per 16-stream group): batch kb = chunks [kb*BC, kb*BC+BC) = RAWB
-    // bytes per stream, moved by LDS-DMA (global_load_lds, no registers) ahead of its first chunk's unpack.
-    // Lane = 4 x stream + quarter of the stream's RAWB bytes; RAW_PIECES DMA pieces of 16 B per lane.
+    // raw-IQ prefetch of the loader wave (wave 3): batch kb = chunks [kb*BC, kb*BC+BC) = 512 B per stream,
+    // moved by LDS-DMA (global_load_lds, no registers) BC iterations before its first chunk is unpacked.
+    // Lane = 4 x stream + quarter of the stream's 512 B; 8 DMA pieces of 16 B per lane.
     constexpr int BC = batch_chunks<FMT>();
     constexpr int SPU = 16 / (int)bytes_per_sample<FMT>();  // samples per 16 B
-    const bool loader = wave == W_LOAD || wave == W_LOAD1;
-    const int lg = wave == W_LOAD1 ? 1 : 0;  // the loader's 16-stream group
-    const int ld_s = 16 * lg + (lane >> 2), ld_q = lane & 3;
+    const int ld_s = lane >> 2, ld_q = lane & 3;
     const bool ld_live = (s0 + ld_s < n_frames);
     const char *ld_frame = iq + (size_t)(ld_live ? s0 + ld_s : s0) * p.n_in * bps;
     const int n_batches = (n_live + BC * CH - 1) / (BC * CH);
@@ -609,7 +580,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
 #pragma unroll
         for (int q = 0; q < RAW_PIECES; q++)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + 16 * q),
-                                             (__attribute__((address_space(3))) void *)&L.raw[kb % NRAW][lg][q * 64], 16, 0, 0);
+                                             (__attribute__((address_space(3))) void *)&L.raw[kb % NRAW][q * 64], 16, 0, 0);
     };
     // wait until at most `k` batches (the youngest) of this wave's LDS-DMA are still in flight
     auto wait_raw = [](int k) {
@@ -620,7 +591,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     };
     if constexpr (DMA) {
         const int first = min(NRAW - 1, n_batches);  // batches 0 .. NRAW-2 in flight before the loop
-        if (loader)
+        if (wave == W_LOAD)
             for (int kb = 0; kb < first; kb++) issue_batch(kb);
         wait_raw(first - 1);  // batch 0 landed
     }
@@ -686,9 +657,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         // lane of v_pk_mul_f32 rounds like v_mul_f32), the adds in order; the subtractions are additions of
         // (-b) z (a - b == a + (-b) exactly, and (-b) z == -(b z))
         const f2v c1 = {p.lpf[1], -p.lpf[3]}, c2 = {p.lpf[2], -p.lpf[4]};
-        static_assert(BUFF * 4 == (PG == 16 ? SDRG_LPF_LOOP_SLOT_BYTES : SDRG_LPF_LOOP_SLOT_BYTES_PG32),
-                      "ring slot stride of the generated loop");
-        static_assert(PG == 16 || SDRG_LPF_INTERLEAVE, "32-stream workgroups: the interleaved loop only");
+        static_assert(BUFF * 4 == SDRG_LPF_LOOP_SLOT_BYTES, "ring slot stride of the generated loop");
         if (LA && SDRG_LPF_ASM == 1 && !(SDRG_SERIAL_FULL_EXEC & 2) && S % CH == 0) {
             // the whole loop as one block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py): nch + 8 + LA iterations
             // with one s_barrier each, the same count as every other role's chunk_loop
@@ -696,23 +665,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             const uint32_t abase = lds_addr(&L.a[0][my_s * ROW]), ybase = lds_addr(&L.y[0][my_s * ROW]);
             const int nit = nch + 8 + LA;
             unsigned long long sv;
-            int t_it, t_cc, t_r, t_q, t_yo;
-            if (PG == 32)
-                asm volatile(SDRG_LPF_LOOP_IL_ASM_PG32
-                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [q] "=&s"(t_q),
-                               [yo] "=&s"(t_yo)
-                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
-                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
-            else if (SDRG_LPF_INTERLEAVE)
+            int t_it, t_cc, t_r, t_yo;
+            if (SDRG_LPF_INTERLEAVE)
                 asm volatile(SDRG_LPF_LOOP_IL_ASM
-                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [q] "=&s"(t_q),
-                               [yo] "=&s"(t_yo)
+                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                              : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
                              : SDRG_CHUNK_CLOBBERS, "v54", "memory");
             else
                 asm volatile(SDRG_LPF_LOOP_ASM
-                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [q] "=&s"(t_q),
-                               [yo] "=&s"(t_yo)
+                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                              : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
                              : SDRG_CHUNK_CLOBBERS, "v54", "memory");
             z1 = z.x;
@@ -739,7 +700,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 if (lim == CH && SDRG_LPF_ASM && !(SDRG_SERIAL_FULL_EXEC & 2)) {
                     // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                     f2v z = {z1, z2};
-                    const uint32_t src = lds_addr(&L.a[c % NA][my_s * ROW]), dst = lds_addr(&L.y[yslot(c)][my_s * ROW]);
+                    const uint32_t src = lds_addr(&L.a[c % NA][my_s * ROW]), dst = lds_addr(&L.y[c & 3][my_s * ROW]);
                     if (SDRG_LPF_ASM == 3) {  // lab: the chain on register data, no LDS (wrong results)
                         asm volatile(SDRG_LPF_CHUNK_NOLDS_ASM
                                      : [z] "+v"(z)
@@ -766,7 +727,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                     z1 = z.x;
                     z2 = z.y;
                 } else if (lim == CH) {
-                    row_pipeline(&L.a[c % NA][my_s * ROW], &L.y[yslot(c)][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
+                    row_pipeline(&L.a[c % NA][my_s * ROW], &L.y[c & 3][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                         for (int q = 0; q < SB; q++) {
                             const f2v p1 = c1 * z1, p2 = c2 * z2;
@@ -784,7 +745,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                         const float y = (((L.a[c % NA][my_s * ROW + q] + p1.x) + p2.x) + p1.y) + p2.y;
                         z2 = z1;
                         z1 = y;
-                        if (lane < PG) L.y[yslot(c)][my_s * ROW + q] = y;
+                        if (lane < PG) L.y[c & 3][my_s * ROW + q] = y;
                     }
                 }
             }
@@ -830,7 +791,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 });
             }
         });
-    } else if (loader) {
+    } else if (wave == W_LOAD) {
         chunk_loop([&](int it) {
             if constexpr (DMA) {
                 // batch kb + 2 starts moving when batch kb's first chunk is unpacked (its buffer held batch
@@ -848,8 +809,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             {
                 const int c = it;
                 if (c < nch) {
-                    const int sl = 16 * lg + (lane >> 2), part = lane & 3;
-                    float *chunk_w = nco_lds + 2 * 1024 * 2 + 2 * CH * lg;
+                    const int sl = lane >> 2, part = lane & 3;
+                    float *chunk_w = nco_lds + 2 * 1024 * 2;
                     if (p.nco_on) {
                         // every stream of the engine is at the same phase, so the chunk needs CH phasors, not
                         // PG x CH: lane j forms sample c*CH + j's (the table product of nco_mix with x = 1, 0:
@@ -873,8 +834,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                             const int quarter = off / (RAWB / 4), piece = (off % (RAWB / 4)) >> 4;
                             uint4 u[U4];
 #pragma unroll
-                            for (int q = 0; q < U4; q++)
-                                u[q] = L.raw[(c / BC) % NRAW][lg][(piece + q) * 64 + (sl - 16 * lg) * 4 + quarter];
+                            for (int q = 0; q < U4; q++) u[q] = L.raw[(c / BC) % NRAW][(piece + q) * 64 + sl * 4 + quarter];
                             unpack_i8<FMT>(u, x);
                             if (p.nco_on) unpack_q8<FMT>(u, xq);
                         } else {
@@ -906,20 +866,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 }
             }
         });
-    } else if (wave == W_FIR0 || wave == W_FIR1 || wave == W_FIR2 || wave == W_FIR3) {
+    } else if (wave == W_FIR0 || wave == W_FIR1) {
         float facc[MAX_SLOTS / 4] = {};  // FIR accumulators (slots j*4 + lane/16)
-        // FIR0 / FIR1: the first / second half of the slot groups of streams 0-15; FIR2 / FIR3 the same for 16-31
-        const int fg = (wave == W_FIR2 || wave == W_FIR3) ? 1 : 0;
-        const bool first_half = wave == W_FIR0 || wave == W_FIR2;
         chunk_loop([&](int it) {
             // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot mod 4, stream); slot groups
-            //      4j..4j+3 split between the two FIR waves of a 16-stream group ----
+            //      4j..4j+3 split between the two FIR waves ----
             const int c = it - 6 - LA;
             if (c >= 0 && c < nch && PL > 0) {
                 const int4 r = chunk_out[c];  // outputs overlapping chunk c: [r.x, r.y] (host table, no division)
-                const int sl = 16 * fg + (lane & 15), sub = lane >> 4;
+                const int sl = lane % PG, sub = lane / PG;
                 const int t0 = c * CH;
-                if (first_half) {
+                if (wave == W_FIR0) {
                     if (nsl_mask == 31) fir_chunk<4, 0>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
                     else if (nsl_mask == 15) fir_chunk<2, 0>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
                     else fir_chunk<1, 0>(L, c, t0, r.x, r.y, sub, nsl_mask, sl, D, NT, facc);
@@ -930,8 +887,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 }
             }
         });
-    } else if (wave == W_OUT || wave == W_OUT1) {
-        const int og = wave == W_OUT1 ? 1 : 0;  // the clamp wave's 16-stream group
+    } else if (wave == W_OUT) {
         chunk_loop([&](int it) {
             // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5; zero beyond the frame end ----
             // lane = 4 x stream + part of 8 samples.  x = demodSSB(y, y) = y + y (upper) or y - y (lower)
@@ -941,8 +897,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             if (c >= 0 && c < nch) {
 #pragma unroll
                 for (int g8 = 0; g8 < CH / 32; ++g8) {
-                    const int sl = 16 * og + (lane >> 2), part = lane & 3, within = part * (CH / 4) + g8 * 8;
-                    const float *yr = &L.y[yslot(c)][sl * ROW + within];
+                    const int sl = lane >> 2, part = lane & 3, within = part * (CH / 4) + g8 * 8;
+                    const float *yr = &L.y[c & 3][sl * ROW + within];
                     const float *gr = &L.g[c & 1][sl * ROW + within];
                     const float4 ya = *reinterpret_cast<const float4 *>(yr), yb = *reinterpret_cast<const float4 *>(yr + 4);
                     const float4 ga = *reinterpret_cast<const float4 *>(gr), gb = *reinterpret_cast<const float4 *>(gr + 4);
@@ -962,11 +918,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                             if (t + 2 * q + 1 >= S) o[q].y = 0.0f;
                         }
                     }
-#if SDRG_PIPE_PG == 16
                     float *dst = &L.out[c & 1][sl * ROW + within];
-#else
-                    float *dst = &L.y[yslot(c)][sl * ROW + within];  // in place: the FIR reads the clamped values here
-#endif
                     *reinterpret_cast<float4 *>(dst) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
                     *reinterpret_cast<float4 *>(dst + 4) = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
                 }
@@ -1020,8 +972,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         }
     } else {
         chunk_loop([&](int it) {
-            // waves 8-11: per 16-stream group, lane = CH/16 consecutive samples of one stream (256 lanes = the
-            // 16 x CH chunk); NG groups, their pairs interleaved
+            // waves 8-11: lane = CH/16 consecutive samples of one stream (256 lanes = the 16 x CH chunk)
             constexpr int SPL = CH / 16;
             const int hl = (wave == W_DES0 ? 0 : wave == W_DES1 ? 1 : wave == W_DES2 ? 2 : 3) * 64 + lane;
             const int sl = hl / (CH / SPL), i0 = (hl % (CH / SPL)) * SPL;
@@ -1030,16 +981,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             if (c >= 0 && c < nch) {
 #pragma unroll
                 for (int h = 0; h < SPL; h += 2) {
-#pragma unroll
-                    for (int g = 0; g < NG; g++) {
-                        const int row = (16 * g + sl) * ROW + i0 + h;
-                        const float2 y2 = *reinterpret_cast<const float2 *>(&L.y[yslot(c)][row]);
-                        // fabsf(demodSSB(y, y)) == |y| * k exactly (k = 2 or 0)
-                        const f2v a = f2v{fabsf(y2.x), fabsf(y2.y)} * f2v{demod_k, demod_k};
-                        // target / (sqrtf(fabsf(a) + 1e-8f) + 1e-6f), correctly rounded, two lanes per op (ssb_math.h)
-                        const f2v d = agc_desired_abs2(a, p.agc_target);
-                        *reinterpret_cast<float2 *>(&L.d[c & 1][row]) = make_float2(d.x, d.y);
-                    }
+                    const float2 y2 = *reinterpret_cast<const float2 *>(&L.y[c & 3][sl * ROW + i0 + h]);
+                    // fabsf(demodSSB(y, y)) == |y| * k exactly (k = 2 or 0)
+                    const f2v a = f2v{fabsf(y2.x), fabsf(y2.y)} * f2v{demod_k, demod_k};
+                    // target / (sqrtf(fabsf(a) + 1e-8f) + 1e-6f), correctly rounded, two lanes per op (ssb_math.h)
+                    const f2v d = agc_desired_abs2(a, p.agc_target);
+                    *reinterpret_cast<float2 *>(&L.d[c & 1][sl * ROW + i0 + h]) = make_float2(d.x, d.y);
                 }
             }
         });
@@ -1127,8 +1074,8 @@ void ssb_report_stamps() {
     const int ncalls = g_stamp_call < STAMP_CALLS ? g_stamp_call : STAMP_CALLS;
     std::vector<unsigned long long> h(per_call * STAMP_CALLS);
     if (hipMemcpy(h.data(), g_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const char *names[16] = {"DC", "LPF", "AGC", "LOAD", "FIR-0", "OUT", "EQ", "FIR-1", "DES-0", "DES-1",
-                             "DES-2", "DES-3", "LOAD-1", "OUT-1", "FIR-2", "FIR-3"};
+    const char *names[PIPE_WAVES] = {"DC", "LPF", "AGC", "LOAD", "FIR-0", "OUT", "EQ", "FIR-1", "DES-0", "DES-1",
+                                     "DES-2", "DES-3"};
     const int last = (g_stamp_call - 1) % STAMP_CALLS;
     for (int w = 0; w < PIPE_WAVES; w++) {
         double work = 0, loop = 0, real = 0, swork = 0, sloop = 0, sreal = 0;
@@ -1180,7 +1127,6 @@ bool ssb_pipe_supported(const SsbParams &p, int *nsl_mask) {
 }
 
 int ssb_pipe_chunk(void) { return CH; }
-int ssb_pipe_streams_per_workgroup(void) { return PG; }
 
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,

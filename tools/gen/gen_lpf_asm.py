@@ -34,11 +34,6 @@ def pair(reg):
     return f"v[{base}:{base + 1}]", reg & 1
 
 
-# The running value of each dependent chain is the SECOND source operand of the instruction that consumes it.
-# With a partial EXEC (the pipeline's 16 stream lanes) a dependent v_add_f32 whose fresh operand is src0 issues
-# about 6 cycles later per sample than one whose fresh operand is src1 (tools/lab/lpf_exec.hip: the low-pass step
-# 30.6 vs 25.3 cycles per sample on lanes 0-15, 24.7 either way on all 64); a + b == b + a exactly in IEEE
-# arithmetic, so the order of the operands changes no result.
 def lpf_sample(x, z1, z2):
     """x: input/output VGPR; z1, z2: (pair text, half) of the previous two outputs"""
     p1, h1 = z1
@@ -46,10 +41,10 @@ def lpf_sample(x, z1, z2):
     return [
         f"v_pk_mul_f32 v[{P1}:{P1 + 1}], %[c1], {p1} op_sel:[0,{h1}] op_sel_hi:[1,{h1}]",
         f"v_pk_mul_f32 v[{P2}:{P2 + 1}], %[c2], {p2} op_sel:[0,{h2}] op_sel_hi:[1,{h2}]",
-        f"v_add_f32 v{x}, v{P1}, v{x}",
-        f"v_add_f32 v{x}, v{P2}, v{x}",
-        f"v_add_f32 v{x}, v{P1 + 1}, v{x}",
-        f"v_add_f32 v{x}, v{P2 + 1}, v{x}",
+        f"v_add_f32 v{x}, v{x}, v{P1}",
+        f"v_add_f32 v{x}, v{x}, v{P2}",
+        f"v_add_f32 v{x}, v{x}, v{P1 + 1}",
+        f"v_add_f32 v{x}, v{x}, v{P2 + 1}",
     ]
 
 
@@ -61,7 +56,7 @@ def agc_sample(x, g):
         f"v_pk_mul_f32 v[{P2}:{P2 + 1}], %[rates], {px} op_sel:[0,{hx}] op_sel_hi:[1,{hx}]",
         f"v_pk_mul_f32 v[{P1}:{P1 + 1}], %[keep], {pg} op_sel:[0,{hg}] op_sel_hi:[1,{hg}]",
         f"v_cmp_lt_f32 vcc, v{x}, v{g}",
-        f"v_pk_add_f32 v[{P1}:{P1 + 1}], v[{P2}:{P2 + 1}], v[{P1}:{P1 + 1}]",
+        f"v_pk_add_f32 v[{P1}:{P1 + 1}], v[{P1}:{P1 + 1}], v[{P2}:{P2 + 1}]",
         f"v_cndmask_b32 v{x}, v{P1 + 1}, v{P1}, vcc",
     ]
 
@@ -74,9 +69,9 @@ def dc_pair(x, prev):
     return [
         f"v_pk_mul_f32 v[50:51], %[om2], v[{x}:{x + 1}]",
         f"v_mul_f32 v52, %[alpha], v{prev}",
-        f"v_add_f32 v48, v50, v52",
+        f"v_add_f32 v48, v52, v50",
         f"v_mul_f32 v52, %[alpha], v48",
-        f"v_add_f32 v49, v51, v52",
+        f"v_add_f32 v49, v52, v51",
         f"v_pk_add_f32 v[{x}:{x + 1}], v[{x}:{x + 1}], v[48:49] neg_lo:[0,1] neg_hi:[0,1]",
         f"v_pk_mul_f32 v[{x}:{x + 1}], %[a02], v[{x}:{x + 1}]",
     ]
@@ -144,61 +139,37 @@ def chunk(role, lds=True, split=False, il=False):
     return out
 
 
-def slot_bytes(pg):  # bytes per [stream][sample] chunk buffer (PG x ROW floats)
-    return pg * 68 * 4
+SLOT = 16 * 68 * 4  # bytes per [stream][sample] chunk buffer (PG x ROW floats)
 
 
-def exec_streams(pg):  # EXEC = the pg stream lanes
-    return ["s_mov_b64 exec, 0xffff"] if pg == 16 else ["s_mov_b32 exec_lo, -1", "s_mov_b32 exec_hi, 0"]
-
-
-SLOT = slot_bytes(16)
-
-
-def y_slot(pg):  # the y ring: 4 slots (16-stream workgroups), 5 (32-stream: the clamp writes its output in place)
-    return 4 if pg == 16 else 5
-
-
-def yo_lines(pg, SLOT):  # %[yo] = (c mod ring) * SLOT
-    if y_slot(pg) == 4:
-        return ["s_and_b32 %[yo], %[cc], 3", f"s_mul_i32 %[yo], %[yo], {SLOT}"]
-    return [f"s_mul_i32 %[yo], %[q], {SLOT}"]
-
-
-def q_step(pg):  # advance the mod-5 counter with c (32-stream ring only)
-    if y_slot(pg) == 4:
-        return []
-    return ["s_add_u32 %[q], %[q], 1", "s_cmp_eq_u32 %[q], 5", "s_cselect_b32 %[q], 0, %[q]"]
-
-
-def lpf_loop(pg=16):
+def lpf_loop():
     """The low-pass wave's whole chunk loop (SDRG_LPF_LOOKAHEAD): one s_barrier per iteration, like every other
     role's loop, and chunk c = it - 3 (one iteration behind the DC wave's output, through a 3-slot ring), so the
     next chunk's input is complete while this chunk runs: its first two sub-blocks are read before the barrier
     and stay in flight across it (the barrier waits only for this chunk's output writes).  Sub-block j of chunk
     c lives in buffer (c + j) mod 3; three copies of the chunk body, one per c mod 3.
     Operands: %[z] (+v {z1, z2}), %[abase] / %[ybase] (v: LDS byte address of slot 0 of the input / output ring
-    at this stream's row; the output ring has 4 slots, 5 at pg 32), %[c1], %[c2] (s), %[nit] (s: iterations), %[nch]
-    (s: chunks, all full), temps %[sv] (=&s 64-bit), %[it], %[cc], %[r], %[q] (pg 32), %[yo] (=&s); clobbers v0-v54,
-    vcc-free."""
-    SLOT = slot_bytes(pg)
+    at this stream's row), %[c1], %[c2] (s), %[nit] (s: iterations), %[nch] (s: chunks, all full), temps %[sv]
+    (=&s 64-bit), %[it], %[cc], %[r], %[yo] (=&s); clobbers v0-v54, vcc-free."""
     out = []
     u = "%="
-    out += ["s_mov_b64 %[sv], exec"] + exec_streams(pg) + [   # the stream lanes
+    out += [
+        "s_mov_b64 %[sv], exec",
+        "s_mov_b64 exec, 0xffff",          # the 16 stream lanes
         "s_nop 4",
         f"v_pk_mov_b32 v[46:47], %[z], %[z] op_sel:[1,0]",   # chunk -1's sb3 buffer (2): v47 = z1, v46 = z2
         f"v_pk_mov_b32 v[52:53], %[z], %[z] op_sel:[0,1]",   # the carried {z1, z2} if no chunk runs
         "s_mov_b32 %[it], 0",
         "s_mov_b32 %[cc], -3",
         "s_mov_b32 %[r], 0",               # c mod 3 once c >= 0
-    ] + (["s_mov_b32 %[q], 0"] if y_slot(pg) == 5 else []) + [   # c mod 5 once c >= 0
         f"L_top_{u}:",
         "s_cmp_lt_i32 %[cc], 0",
         f"s_cbranch_scc1 L_pre_{u}",
         "s_cmp_ge_i32 %[cc], %[nch]",
         f"s_cbranch_scc1 L_drain_{u}",
-        # output slot c mod 4 (or 5: y_slot)
-    ] + yo_lines(pg, SLOT) + [
+        # output slot c mod 4
+        "s_and_b32 %[yo], %[cc], 3",
+        f"s_mul_i32 %[yo], %[yo], {SLOT}",
         "v_add_u32 v54, %[yo], %[ybase]",
         "s_cmp_eq_u32 %[r], 0",
         f"s_cbranch_scc1 L_r0_{u}",
@@ -255,7 +226,6 @@ def lpf_loop(pg=16):
         "s_add_u32 %[r], %[r], 1",
         "s_cmp_eq_u32 %[r], 3",
         "s_cselect_b32 %[r], 0, %[r]",
-    ] + q_step(pg) + [
         f"L_next_{u}:",
         "s_cmp_lt_u32 %[it], %[nit]",
         f"s_cbranch_scc1 L_top_{u}",
@@ -266,30 +236,31 @@ def lpf_loop(pg=16):
     return out
 
 
-def lpf_loop_interleaved(pg=16):
+def lpf_loop_interleaved():
     """lpf_loop() with the LDS traffic spread through the VALU stream: sub-blocks are numbered g = 4c + sb across
     chunks and live in buffer g mod 3; while sub-block g runs, after each 4-sample quad t its output quad is written
     and quad t of sub-block g + 2 is read (for sb = 2, 3 that is the next chunk's sub-block 0, 1, complete in its
     ring slot).  So at the barrier only the chunk's last write is outstanding (lgkmcnt(1)), and the first two
     sub-blocks of the next chunk are already in registers.  The last chunk's reads of a next chunk fetch a stale
     ring slot and are never used; the block drains them (lgkmcnt(0)) before it ends."""
-    SLOT = slot_bytes(pg)
     out = []
     u = "%="
-    out += ["s_mov_b64 %[sv], exec"] + exec_streams(pg) + [
+    out += [
+        "s_mov_b64 %[sv], exec",
+        "s_mov_b64 exec, 0xffff",
         "s_nop 4",
         "v_pk_mov_b32 v[46:47], %[z], %[z] op_sel:[1,0]",
         "v_pk_mov_b32 v[52:53], %[z], %[z] op_sel:[0,1]",
         "s_mov_b32 %[it], 0",
         "s_mov_b32 %[cc], -3",
         "s_mov_b32 %[r], 0",
-    ] + (["s_mov_b32 %[q], 0"] if y_slot(pg) == 5 else []) + [
         f"L_top_{u}:",
         "s_cmp_lt_i32 %[cc], 0",
         f"s_cbranch_scc1 L_pre_{u}",
         "s_cmp_ge_i32 %[cc], %[nch]",
         f"s_cbranch_scc1 L_drain_{u}",
-    ] + yo_lines(pg, SLOT) + [
+        "s_and_b32 %[yo], %[cc], 3",
+        f"s_mul_i32 %[yo], %[yo], {SLOT}",
         "v_add_u32 v54, %[yo], %[ybase]",
         "s_cmp_eq_u32 %[r], 0",
         f"s_cbranch_scc1 L_r0_{u}",
@@ -341,7 +312,6 @@ def lpf_loop_interleaved(pg=16):
         "s_add_u32 %[r], %[r], 1",
         "s_cmp_eq_u32 %[r], 3",
         "s_cselect_b32 %[r], 0, %[r]",
-    ] + q_step(pg) + [
         f"L_next_{u}:",
         "s_cmp_lt_u32 %[it], %[nit]",
         f"s_cbranch_scc1 L_top_{u}",
@@ -392,9 +362,6 @@ def main():
         print("    " + ", ".join(regs[i:i + 16]) + (", \\" if i + 16 < len(regs) else ""))
     print("#define SDRG_LPF_CHUNK_CLOBBERS SDRG_CHUNK_CLOBBERS")
     print(f"#define SDRG_LPF_LOOP_SLOT_BYTES {SLOT}")
-    print("// the product loop for 32-stream workgroups (SDRG_PIPE_PG 32): 32 stream lanes, 32-stream ring slots")
-    emit("SDRG_LPF_LOOP_IL_ASM_PG32", lpf_loop_interleaved(32))
-    print(f"#define SDRG_LPF_LOOP_SLOT_BYTES_PG32 {slot_bytes(32)}")
 
 
 if __name__ == "__main__":
