@@ -17,8 +17,8 @@
 //
 // The constants are glibc's published data (e_logf_data.c, e_log10f.c).  tests/cpp/libm_exact.cpp checks the
 // host instantiation and tests/cpp/libm_exact.hip the device one against the running glibc on every
-// non-negative float, infinities included; NaN and negative inputs never reach these calls on the hot path
-// (the operands are power + 1e-20 and focus lengths) and are not handled like glibc.
+// non-negative float, infinities included; negative and NaN inputs give a NaN as glibc's do (not necessarily the
+// same NaN bits), -0 gives -inf.
 #pragma once
 
 #include <stdint.h>
@@ -75,7 +75,7 @@ SDRG_HD float u2f(uint32_t u) {
 
 SDRG_HD double fma_d(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
-// e_logf.c (__logf) for x >= 0: +0 gives -inf, +inf gives +inf.  `tab` is the 16-entry table (a copy in LDS
+// e_logf.c (__logf): +-0 gives -inf, +inf gives +inf, negative or NaN gives NaN.  `tab` is the 16-entry table (a copy in LDS
 // on the device: the index is data-dependent, and an LDS read is far shorter than a global one).
 SDRG_HD float logf_with(float x, const LogfEntry *tab) {
     const double Ln2 = 0x1.62e42fefa39efp-1;
@@ -85,6 +85,7 @@ SDRG_HD float logf_with(float x, const LogfEntry *tab) {
     if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
         if (ix * 2 == 0) return -__builtin_inff();
         if (ix == 0x7f800000u) return x;
+        if ((ix & 0x80000000u) || ix * 2 >= 0xff000000u) return __builtin_nanf("");  // negative or NaN: NaN
         ix = f2u(x * 0x1p23f);  // subnormal: normalise
         ix -= 23u << 23;
     }
@@ -113,6 +114,7 @@ SDRG_HD float log10f_with(float x, const LogfEntry *tab) {
     int32_t k = 0;
     if (hx < 0x00800000) {
         if ((hx & 0x7fffffff) == 0) return -__builtin_inff();
+        if (hx < 0) return __builtin_nanf("");  // log(-x) = NaN
         k -= 25;
         x *= two25;
         hx = (int32_t)f2u(x);
@@ -128,6 +130,46 @@ SDRG_HD float log10f_with(float x, const LogfEntry *tab) {
     const float z = a + b;
     const float c = y * log10_2hi;
     return z + c;
+}
+
+// log10f_with for a positive, normal, finite x (FLT_MIN <= x <= FLT_MAX): the same operations without the special
+// cases -- no branch on the path the statistics take (their operands are power + 1e-20).  For x == 1 the logf
+// step gives +0 without glibc's explicit check (r = 0, y0 = 0, table entry 9 = {1, 0}).
+SDRG_HD float log10f_posnormal(float x, const LogfEntry *tab) {
+    const float ivln10 = 4.3429449201e-01f, log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
+    const double Ln2 = 0x1.62e42fefa39efp-1;
+    const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+    const int32_t hx = (int32_t)f2u(x);
+    const int32_t k = (hx >> 23) - 127;
+    const int32_t i = (int32_t)((uint32_t)k >> 31);                           // m in [0.5, 1) when k < 0
+    const uint32_t ix = (uint32_t)((hx & 0x007fffff) | ((0x7f - i) << 23));  // the bits of m
+    const float y = (float)(k + i);
+    // logf(m), m in [0.5, 2): normal, so e_logf.c's special cases never apply
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int ti = (int)((tmp >> (23 - 4)) & 15u);
+    const int kk = (int32_t)tmp >> 23;
+    const uint32_t iz = ix - (tmp & 0xff800000u);
+    const double invc = tab[ti].invc, logc = tab[ti].logc;
+    const double z = (double)u2f(iz);
+    const double r = fma_d(z, invc, -1.0);
+    const double y0 = fma_d((double)kk, Ln2, logc);
+    const double r2 = r * r;
+    double yy = fma_d(A1, r, A2);
+    yy = fma_d(A0, r2, yy);
+    yy = fma_d(yy, r2, y0 + r);
+    const float lnm = (float)yy;
+    const float a = y * log10_2lo;
+    const float b = ivln10 * lnm;
+    const float zz = a + b;
+    const float c = y * log10_2hi;
+    return zz + c;
+}
+
+// log10f_with, branch-free for positive normal finite x (the common case), the general path otherwise
+SDRG_HD float log10f_fast(float x, const LogfEntry *tab) {
+    const uint32_t u = f2u(x);
+    if (__builtin_expect(u - 0x00800000u < 0x7f000000u, 1)) return log10f_posnormal(x, tab);  // [FLT_MIN, FLT_MAX]
+    return log10f_with(x, tab);
 }
 
 SDRG_HD float logf(float x) { return logf_with(x, logf_table()); }

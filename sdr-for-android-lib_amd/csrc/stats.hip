@@ -51,7 +51,7 @@ __device__ __forceinline__ void load_logf_tab() {
     if (threadIdx.x < 16) s_logf_tab[threadIdx.x] = glibc::logf_table()[threadIdx.x];
 }
 __device__ __forceinline__ float db_of(float p) {  // refPower = 1
-    return 10.0f * glibc::log10f_with(p / 1.0f + 1e-20f, s_logf_tab);
+    return 10.0f * glibc::log10f_fast(p / 1.0f + 1e-20f, s_logf_tab);
 }
 
 struct WinScan {

@@ -33,7 +33,8 @@ __global__ void eval(uint32_t base, uint32_t count, float *out_ln, float *out_lg
     out_lg[i] = lg;
     // the LDS-table instantiation must agree with the constant-table one bit for bit
     const int bad = (__float_as_uint(sdrg::glibc::logf_with(x, tab)) != __float_as_uint(ln)) +
-                    (__float_as_uint(sdrg::glibc::log10f_with(x, tab)) != __float_as_uint(lg));
+                    (__float_as_uint(sdrg::glibc::log10f_with(x, tab)) != __float_as_uint(lg)) +
+                    (__float_as_uint(sdrg::glibc::log10f_fast(x, tab)) != __float_as_uint(lg));  // the stats' path
     if (bad) atomicAdd(lds_bad, (unsigned long long)bad);
 }
 

@@ -1,15 +1,15 @@
 #!/bin/bash
-# statistics parity, then c2 / c5 lines: product library vs lib/libsdrg_${B:-statsold}.so, alternating
+# Statistics variants, alternating: the product (dB via the glibc log10f restatement, focus dB only near the
+# largest power), lab "glibc" (the restatement on every focus bin), lab "ocml" (round 2: ocml's log10f).
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_any_n.py tests/test_gpu_edges.py tests/test_gpu_engine_api.py tests/test_gpu_multi_rank.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/stats_parity.log 2>&1 || { echo "parity failed"; tail -30 gpurun_out/stats_parity.log; exit 1; }
-tail -1 gpurun_out/stats_parity.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_stats_exact.py tests/test_gpu_stats_geometry.py tests/test_gpu_parity.py tests/test_gpu_any_n.py tests/test_gpu_edges.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/sab_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/sab_tests.log; exit 1; }
+tail -1 gpurun_out/sab_tests.log
 L=$PWD/sdr-for-android-lib_amd/lib
-for i in 1 2; do
-  for lib in libsdrg.so libsdrg_${B:-statsold}.so; do
-    for a in "--config c2" "--config c5 --focus 5" ""; do
-      SDRG_LIB_PATH=$L/$lib timeout -k 10 120 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-labelled $a > gpurun_out/sab.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/sab.log; exit 1; }
-      tail -1 gpurun_out/sab.log | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); k=d['kernel_ms']; print('$lib', '${a:-c3}', d['value'], d['ms_per_step'], k['spectrum_ms'], k['stats_ms'], k['ssb_ms'])"
-    done
-  done
-done
+run() {  # variant tag [extra]
+  lib=""; [ "$1" != product ] && lib=$L/libsdrg_$1.so
+  SDRG_LIB_PATH=$lib timeout -k 10 200 python bench.py --steps 300 --warmup 5 --no-cpu-baseline --no-labelled $3 > gpurun_out/sab_$1_$2.json 2> gpurun_out/sab_$1_$2.err || { echo "bench $1 failed"; tail -5 gpurun_out/sab_$1_$2.err; exit 1; }
+  echo "$1 $2 $(tail -1 gpurun_out/sab_$1_$2.json | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["kernel_ms"])')"
+}
+for r in a b; do run product $r && run glibc $r && run ocml $r || exit 1; done
+for r in c5a c5b; do run product $r "--config c5 --focus 200" && run glibc $r "--config c5 --focus 200" && run ocml $r "--config c5 --focus 200" || exit 1; done
