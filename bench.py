@@ -41,6 +41,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 ALG_BYTES_PER_SAMPLE = {"spectrum": 6.0}  # CS8: 2 B in + 4 B fftshifted float32 power out
 ISO_LAUNCHES = 30  # launches of the spectrum stage alone behind roofline_isolated
 N_INPUTS = 3  # distinct input batches rotated per step: 3 x 128 MiB > the 256 MiB Infinity Cache
+N_OUTPUTS = 3  # spectra / records buffers rotated per step (asynchronous statistics read a call's spectra late)
 # SSB floor: the sample-serial low-pass wave's own instruction issue.  Per sample it issues 6 VALU instructions
 # (the packed product of the previous output, 4 dependent adds, the packed product of the output before it) and
 # 0.5 LDS instructions (a 16-byte read and write per 4 samples); one wave issues at most one instruction per
@@ -259,6 +260,13 @@ def main() -> int:
                     help="untimed pre-roll before --warmup: the same step, in blocks of 25, until this much wall time has "
                          "passed, so the timed steps run at the chip's steady clock whatever --warmup is (reported as "
                          "prewarm_ms)")
+    ap.add_argument("--stats-async", default="auto", choices=["auto", "0", "1"],
+                    help="1: pipelined calls run their statistics on a stream of their own beside the next call's spectrum "
+                         "(SDRG_PIPELINE_STATS_ASYNC; every stage of every call still runs); 0: after the spectrum on the "
+                         "main stream; auto (default): 1 for the 65536-point configs[4] lines, whose four-step FFT leaves "
+                         "room beside it (measured 8 %% / 2 %% faster at 5 / 200 kHz), 0 for 16384 points, whose persistent "
+                         "spectrum kernel loses more to co-resident statistics than they gain (c2 0.18 vs 0.13 ms/step) "
+                         "and for N > 1 (the per-step gathers read the records on the main stream)")
     ap.add_argument("--launch-dry-run", action="store_true", help=argparse.SUPPRESS)
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
@@ -323,8 +331,9 @@ def main() -> int:
     # N_INPUTS distinct batches rotated per step, so no step reads inputs the Infinity Cache kept from the last
     iqs = [synth_device_frames(torch, dev, streams, seed=0x5D12 + 7919 * rank + k, n=n, cs16=c5)
            for k in range(N_INPUTS)]
-    spec = torch.empty((streams, n), dtype=torch.float32, device=dev)
-    rec = torch.zeros((streams, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    specs = [torch.empty((streams, n), dtype=torch.float32, device=dev) for _ in range(N_OUTPUTS)]
+    recs = [torch.zeros((streams, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev) for _ in range(N_OUTPUTS)]
+    spec, rec = specs[0], recs[0]
     plen = eng.pcm_len
     pcm = torch.empty((streams, plen), dtype=torch.int16, device=dev)
     torch.cuda.synchronize()
@@ -355,7 +364,9 @@ def main() -> int:
     calls = [0]
 
     def step(st=None):
+        nonlocal spec, rec
         iq = iqs[calls[0] % N_INPUTS]
+        spec, rec = specs[calls[0] % N_OUTPUTS], recs[calls[0] % N_OUTPUTS]
         calls[0] += 1
         eng.process_device(iq.data_ptr(), fmt, stages if st is None else st, spec.data_ptr(), rec.data_ptr(),
                            pcm.data_ptr(), now[0])
@@ -374,8 +385,12 @@ def main() -> int:
     # a pipelined call leaves its SSB stream running past the call, so a per-step PCM gather needs the joined schedule
     # the inputs are generated before the timed region and synchronised, so they are complete at every call
     pipelined = args.pipelined if not (gather_pcm and world > 1) else 0
+    async_ok = bool(pipelined and world == 1)
+    stats_async = async_ok and (args.stats_async == "1" or (args.stats_async == "auto" and c5))
+    pipe_mode = pipelined | (sdrg.PIPELINE_STATS_ASYNC if stats_async else 0)
+    c5_mode = pipelined | (sdrg.PIPELINE_STATS_ASYNC if async_ok and args.stats_async != "0" else 0)
     if pipelined:
-        eng.set_pipelining(pipelined)
+        eng.set_pipelining(pipe_mode)
     eng.set_profiling(True)
     # pre-roll: from idle the chip needs ~50 steps (~20 ms) of this load to reach its steady clock
     # (tools/lab/warm_trace.py), more than a short --warmup covers; blocks of 25 steps until prewarm_ms has passed
@@ -453,7 +468,7 @@ def main() -> int:
         """A separately labelled line measured in this same run: k_steps pipelined steps of stages st."""
         if variant_on:
             eng.set_ssb_variant(NCO_HZ, 127)
-        eng.set_pipelining(pipelined)
+        eng.set_pipelining(pipe_mode)
         for _ in range(3):
             step(st)
         eng.synchronize()
@@ -473,17 +488,19 @@ def main() -> int:
         e5 = sdrg.Engine(sdrg.SDRConfig(centerFrequency=CF, samplesPerReading=n5, sampleRate=FS,
                                         freqFocusRangeKhz=focus_c5, soundMode=1), s5, device=local)
         iq5 = [synth_device_frames(torch, dev, s5, seed=0xC5 + k, n=n5, cs16=True) for k in range(N_INPUTS)]
-        sp5 = torch.empty((s5, n5), dtype=torch.float32, device=dev)
-        rc5 = torch.zeros((s5, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        sp5 = [torch.empty((s5, n5), dtype=torch.float32, device=dev) for _ in range(N_OUTPUTS)]
+        rc5 = [torch.zeros((s5, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev) for _ in range(N_OUTPUTS)]
         st5 = sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS
         torch.cuda.synchronize()
         e5.set_profiling(True)
+        if pipelined:  # each call's statistics beside the next call's spectrum (--stats-async)
+            e5.set_pipelining(c5_mode)
         t5 = [1000]
 
         def run(k):
             for i in range(k):
-                e5.process_device(iq5[i % N_INPUTS].data_ptr(), sdrg.CS16, st5, sp5.data_ptr(), rc5.data_ptr(), None,
-                                  t5[0])
+                e5.process_device(iq5[i % N_INPUTS].data_ptr(), sdrg.CS16, st5, sp5[i % N_OUTPUTS].data_ptr(),
+                                  rc5[i % N_OUTPUTS].data_ptr(), None, t5[0])
                 t5[0] += n5 // 2000
         run(20)
         e5.synchronize()
@@ -504,6 +521,7 @@ def main() -> int:
                                                                                           / 1e6, 1),
                                  "frac": round(fft_bytes / tm["spectrum_ms"] / 1e6 / HBM_PEAK_GBS, 4)},
                 "roofline_step_frac": round(step_b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "stats_async": bool(c5_mode & sdrg.PIPELINE_STATS_ASYNC),
                 "workload": f"BASELINE configs[4]: {s5} streams x {n5}-pt CS16 frames @2 Msps, four-step FFT + |X|^2 "
                             f"+ fftshift + signal-strength stats over a {focus_c5} kHz focus; no SSB"}
 
@@ -592,7 +610,9 @@ def main() -> int:
                           "measured": "whole-step algorithmic bytes (IQ in, spectra, records, PCM out) / ms_per_step"},
         "pipelined": {0: "off (each step joins its SSB stream)",
                       1: "on (SSB stage forked from the main stream each step)",
-                      2: "on, inputs ready (resident inputs: the SSB stage does not wait on the main stream)"}[pipelined],
+                      2: "on, inputs ready (resident inputs: the SSB stage does not wait on the main stream)"}[pipelined]
+                     + ("; statistics on a stream of their own beside the next step's spectrum (SDRG_PIPELINE_STATS_ASYNC),"
+                        f" {N_OUTPUTS} spectra/records buffers rotated" if stats_async else ""),
         "inputs": f"{N_INPUTS} distinct {streams}x{n} {fmt_name} batches ({N_INPUTS * streams * n * in_bps / 2**20:.0f} "
                   "MiB) rotated per step in every leg, so inputs are not served from the 256 MiB Infinity Cache",
     }

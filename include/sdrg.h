@@ -427,9 +427,20 @@ int32_t sdrg_engine_set_stream(sdrg_engine *eng, void *hip_stream);
  *     host-synchronised copies or earlier, already-finished work, e.g. a resident ring of input frames); the
  *     SSB stage then does not wait for the main stream at all, which saves its stream one cross-stream wait
  *     per call.  Work the caller enqueues on the main stream that writes iq is NOT waited for in this mode.
+ * SDRG_PIPELINE_STATS_ASYNC may be added (OR) to ON or INPUTS_READY: a call's statistics and spectral pulse detector
+ *   run on a stream of their own after the call's spectrum, beside the next call's spectrum, instead of after it
+ *   on the main stream.  Every stage of every call still runs, in order per stream; the records and spectral-pulse
+ *   outputs are complete after sdrg_engine_synchronize, or on a stream after sdrg_engine_wait_outputs.  The engine
+ *   keeps the spectra a call's statistics read intact (a call writing the previous call's spectra buffer waits for
+ *   those statistics on the GPU; the host waits for the statistics of the call two before), so a caller rotating
+ *   two or more spectra buffers (and records buffers it reads back) overlaps the statistics fully.
  * Any other value returns SDRG_E_INVALID. */
-enum { SDRG_PIPELINE_OFF = 0, SDRG_PIPELINE_ON = 1, SDRG_PIPELINE_INPUTS_READY = 2 };
+enum { SDRG_PIPELINE_OFF = 0, SDRG_PIPELINE_ON = 1, SDRG_PIPELINE_INPUTS_READY = 2, SDRG_PIPELINE_STATS_ASYNC = 4 };
 int32_t sdrg_engine_set_pipelining(sdrg_engine *eng, int32_t mode);
+/* Enqueue on `hip_stream` (NULL = the engine's main stream) a wait for every output of the last call: spectra,
+ * records and spectral-pulse outputs, PCM and audio-pulse outputs, whichever streams produce them (a consumer of a
+ * pipelined call's outputs, e.g. an RCCL gather of the records, then follows them without a host synchronisation). */
+int32_t sdrg_engine_wait_outputs(sdrg_engine *eng, void *hip_stream);
 /* The INPUT of a call: the kernels read `iq` asynchronously after sdrg_engine_process_device returns -- the
  * spectrum on the main stream and the SSB pipeline on its own stream, which in pipelined mode runs on past the
  * call, beside the next call's spectrum.  The caller must not overwrite or free `iq` until the call has released

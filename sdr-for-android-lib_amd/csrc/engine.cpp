@@ -201,6 +201,20 @@ struct sdrg_engine {
     bool cf_changed_pending = false;
     bool pipelined = false;  // sdrg_engine_set_pipelining: no join of the SSB stream per call
     bool inputs_ready = false;  // SDRG_PIPELINE_INPUTS_READY: no fork wait on the main stream either
+    // SDRG_PIPELINE_STATS_ASYNC: a pipelined call's statistics (+ spectral pulse detector) run on s_stats after its
+    // spectrum, beside the next call's spectrum.  The engine keeps the spectra a call's statistics read intact:
+    // a call that writes the same spectra buffer as the call before waits (on the GPU) for that call's statistics,
+    // and the host waits for the statistics of the call two before (so a caller rotating two or more spectra
+    // buffers never waits on the GPU).
+    bool stats_async = false;
+    hipStream_t s_stats = nullptr;
+    hipEvent_t ev_spec_done = nullptr;  // after a call's spectrum on s_main, waited by s_stats
+    static constexpr int SA_RING = 3;
+    hipEvent_t ev_stats_end[SA_RING] = {};  // end of the statistics of call (sa_calls - k) at slot % SA_RING
+    const float *sa_spec[SA_RING] = {};     // the spectra buffer each of those calls' statistics read
+    bool sa_live[SA_RING] = {};
+    int64_t sa_calls = 0;
+    hipEvent_t last_stats_end = nullptr;    // the last asynchronous statistics (wait_outputs, synchronize)
     // NCO/short-FIR SSB variant (sdrg_engine_set_ssb_variant; a build extension, off by default)
     double nco_hz = 0.0;
     int fir_taps = 0;            // 0: the reference's 255
@@ -280,6 +294,7 @@ int32_t fold_slot(sdrg_engine *e, int slot) {
         t.spectrum_ms = ms;
     }
     if (ev.has_stats) {
+        if (ev.stats_marked) HIP_TRY(hipEventSynchronize(ev.stats));  // asynchronous statistics end on s_stats
         HIP_TRY(hipEventElapsedTime(&ms, ev.has_spec ? ev.spec : ev.t0, ev.stats_marked ? ev.stats : ev.end));
         t.stats_ms = ms;
     }
@@ -520,8 +535,9 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         // the SSB start marker sits on the SSB stream between the fork and the pipeline; pipelined, that
         // stream is the step's critical path, so only every 8th call carries one (its mean is the sample's)
         ev->ssb_timed = do_ssb && (!(e->pipelined && !join) || e->calls_profiled % 8 == 0);
-        // a joined call's end marker follows the wait for the SSB stream: the statistics get a marker of their own
-        ev->stats_marked = do_stats && !(e->pipelined && !join);
+        // a joined call's end marker follows the wait for the SSB stream, and asynchronous statistics end on a
+        // stream of their own: the statistics get a marker of their own
+        ev->stats_marked = do_stats && (!(e->pipelined && !join) || e->stats_async);
         e->calls_profiled++;
     }
     // Markers: every event recorded between two kernels of a stream costs that stream a gap (several us
@@ -552,6 +568,18 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipEventRecord(e->ev_fork_spec, e->s_main));
         HIP_TRY(hipStreamWaitEvent(e->s_spec, e->ev_fork_spec, 0));
     }
+    // asynchronous statistics (SDRG_PIPELINE_STATS_ASYNC): the statistics of earlier calls may still read their
+    // spectra on s_stats.  The host waits for the call two before; a spectrum that overwrites the buffer the
+    // previous call's statistics read waits for them on the GPU.
+    const bool async = e->stats_async && early_fork && do_stats && do_spec && !split;
+    if (e->stats_async && do_spec) {
+        const int64_t c = e->sa_calls;
+        if (c >= 2 && e->sa_live[(c - 2) % sdrg_engine::SA_RING])
+            HIP_TRY(hipEventSynchronize(e->ev_stats_end[(c - 2) % sdrg_engine::SA_RING]));
+        const int pv = (int)((c + sdrg_engine::SA_RING - 1) % sdrg_engine::SA_RING);
+        if (c >= 1 && e->sa_live[pv] && (e->sa_spec[pv] == spec || !async))
+            HIP_TRY(hipStreamWaitEvent(sm, e->ev_stats_end[pv], 0));
+    }
     if (do_spec) {
         HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, sm, do_ssb && early_fork && !split,
                                 split ? e->spec_cus : 0));
@@ -580,13 +608,27 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipEventRecord(mk_ssb_end, e->s_ssb));
     }
     if (do_stats) {
-        HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->d_pool, sm));
+        hipStream_t st = sm;
+        if (async) {  // after this call's spectrum, beside the next call's
+            HIP_TRY(hipEventRecord(e->ev_spec_done, sm));
+            HIP_TRY(hipStreamWaitEvent(e->s_stats, e->ev_spec_done, 0));
+            st = e->s_stats;
+        }
+        HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->d_pool, st));
         if (do_sp) {  // spectralPulseDetector.process(best1kHzSnrSigma, best1kHzCenterFreqHz) (:477-479)
             int32_t rc = pulse_bank_spectral(&e->spec_bank, &recs->best1khz_snr_sigma, &recs->best1khz_center_freq_hz,
-                                             (int)sizeof(sdrg_frame_record), e->spec_bank.d_out, sm);
+                                             (int)sizeof(sdrg_frame_record), e->spec_bank.d_out, st);
             if (rc) return rc;
         }
-        if (prof && ev->stats_marked) HIP_TRY(hipEventRecord(ev->stats, sm));
+        if (prof && ev->stats_marked) HIP_TRY(hipEventRecord(ev->stats, st));
+        if (async) {
+            const int k = (int)(e->sa_calls % sdrg_engine::SA_RING);
+            HIP_TRY(hipEventRecord(e->ev_stats_end[k], st));
+            e->sa_spec[k] = spec;
+            e->sa_live[k] = true;
+            e->sa_calls++;
+            e->last_stats_end = e->ev_stats_end[k];
+        }
     }
     // the main stream's end marker: input release (the spectrum reads iq), timing; joined calls place it after
     // the join, so total_ms spans both streams
@@ -780,13 +822,17 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     // the caller's stream (sdrg_engine_set_stream) must outlive the engine: synchronise it while it is set
     if (e->s_main) (void)hipStreamSynchronize(e->s_main);
     if (e->s_ssb) (void)hipStreamSynchronize(e->s_ssb);
+    if (e->s_stats) (void)hipStreamSynchronize(e->s_stats);
     e->spec_bank.last_stream = e->audio_bank.last_stream = nullptr;  // drained above
     void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_nco_tab, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch, e->d_pool,
                     e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (e->s_spec) (void)hipStreamSynchronize(e->s_spec);
-    hipEvent_t evs[] = {e->ev_fork, e->ev_join, e->ev_in_main, e->ev_in_ssb, e->ev_fork_spec, e->ev_join_spec};
+    for (hipEvent_t ev : e->ev_stats_end)
+        if (ev) (void)hipEventDestroy(ev);
+    hipEvent_t evs[] = {e->ev_fork, e->ev_join, e->ev_in_main, e->ev_in_ssb, e->ev_fork_spec, e->ev_join_spec,
+                        e->ev_spec_done};
     for (hipEvent_t ev : evs)
         if (ev) (void)hipEventDestroy(ev);
     for (auto &r : e->ring) {
@@ -799,6 +845,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (e->s_own) (void)hipStreamDestroy(e->s_own);
     if (e->s_ssb) (void)hipStreamDestroy(e->s_ssb);
     if (e->s_spec) (void)hipStreamDestroy(e->s_spec);
+    if (e->s_stats) (void)hipStreamDestroy(e->s_stats);
     delete e;
     return SDRG_OK;
 }
@@ -859,6 +906,17 @@ int32_t sdrg_engine_wait_input_released(sdrg_engine *e, void *hip_stream) {
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : e->s_main;
     if (e->last_in_main && s != e->s_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));
     if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_wait_outputs(sdrg_engine *e, void *hip_stream) {
+    if (!e) return fail(SDRG_E_INVALID, "null engine");
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : e->s_main;
+    if (e->last_in_main && s != e->s_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));  // spectra
+    if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));                    // PCM, audio pulse
+    if (e->stats_async && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));  // records
     return SDRG_OK;
 }
 
@@ -925,6 +983,7 @@ int32_t sdrg_engine_reset_state(sdrg_engine *e) {
     HIP_TRY(dscope.error());
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));
+    if (e->s_stats) HIP_TRY(hipStreamSynchronize(e->s_stats));
     HIP_TRY(hipMemset(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
     HIP_TRY(hipMemset(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
     e->ssb = SsbControl{};
@@ -939,14 +998,27 @@ int32_t sdrg_engine_set_pipelining(sdrg_engine *e, int32_t on) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     DeviceScope dscope(e->device);
     HIP_TRY(dscope.error());
-    if (e->pipelined && !on) {  // re-join what is in flight so later work on s_main follows it
+    const int mode = on & ~SDRG_PIPELINE_STATS_ASYNC;
+    const bool async = (on & SDRG_PIPELINE_STATS_ASYNC) != 0;
+    if ((mode != SDRG_PIPELINE_OFF && mode != SDRG_PIPELINE_ON && mode != SDRG_PIPELINE_INPUTS_READY) ||
+        (async && mode == SDRG_PIPELINE_OFF))
+        return fail(SDRG_E_INVALID, "pipelining mode must be 0, 1 or 2 (1 or 2 may add SDRG_PIPELINE_STATS_ASYNC), got %d",
+                    on);
+    if (e->pipelined && !mode) {  // re-join what is in flight so later work on s_main follows it
         HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
         HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));
     }
-    if (on != SDRG_PIPELINE_OFF && on != SDRG_PIPELINE_ON && on != SDRG_PIPELINE_INPUTS_READY)
-        return fail(SDRG_E_INVALID, "pipelining mode must be 0, 1 or 2, got %d", on);
-    e->pipelined = on != SDRG_PIPELINE_OFF;
-    e->inputs_ready = on == SDRG_PIPELINE_INPUTS_READY;
+    if (e->stats_async && !async && e->last_stats_end)  // the asynchronous statistics in flight, likewise
+        HIP_TRY(hipStreamWaitEvent(e->s_main, e->last_stats_end, 0));
+    if (async && !e->s_stats) {
+        const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+        HIP_TRY(hipStreamCreateWithFlags(&e->s_stats, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_spec_done, fl));
+        for (hipEvent_t &ev : e->ev_stats_end) HIP_TRY(hipEventCreateWithFlags(&ev, fl));
+    }
+    e->pipelined = mode != SDRG_PIPELINE_OFF;
+    e->inputs_ready = mode == SDRG_PIPELINE_INPUTS_READY;
+    e->stats_async = async;
     return SDRG_OK;
 }
 
@@ -991,6 +1063,7 @@ int32_t sdrg_engine_get_pulse_outputs(sdrg_engine *e, sdrg_pulse_output *spectra
     HIP_TRY(dscope.error());
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));
+    if (e->s_stats) HIP_TRY(hipStreamSynchronize(e->s_stats));
     const size_t bytes = sizeof(sdrg_pulse_output) * (size_t)e->n_streams;
     if (spectral) {
         if (!e->spec_bank_live) return fail(SDRG_E_INVALID, "the spectral pulse stage has not run");
@@ -1059,6 +1132,7 @@ int32_t sdrg_engine_synchronize(sdrg_engine *e) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));  // not joined into s_main when pipelined
+    if (e->s_stats) HIP_TRY(hipStreamSynchronize(e->s_stats));  // SDRG_PIPELINE_STATS_ASYNC
     static const bool stamps = [] {
         const char *v = lab_getenv("SDRG_PIPE_STAMPS");
         return v && v[0] == '1';

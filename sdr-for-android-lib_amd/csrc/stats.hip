@@ -136,7 +136,10 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
     // roles by wave: 0 chains, 1 records, 2-3 producers.  (Rotating the roles with the block index, so that the
     // frames sharing a CU put their chain waves on different SIMDs, measured slower: the chain wave then shares
     // its SIMD with the producers' issue-dense log10s.)
-    const int lane = threadIdx.x & 63, role = threadIdx.x >> 6;
+#ifndef SDRG_WIDE_ROTATE  // lab: roles rotated with the block index (frames sharing a CU put their chain waves apart)
+#define SDRG_WIDE_ROTATE 0
+#endif
+    const int lane = threadIdx.x & 63, role = ((threadIdx.x >> 6) + (SDRG_WIDE_ROTATE ? (int)blockIdx.x : 0)) & 3;
     const int fq = nwin - 1;
     // SC = 2^lg bins per window per chunk, the largest that fits; rows are RS = SC + 4 floats apart, so the chain
     // lanes' float4 accesses (one row each, same bin) fall in different LDS banks
@@ -228,14 +231,22 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
 #pragma unroll
                     for (int i = 0; i < 4; i++) X[i] = *reinterpret_cast<const float4 *>(src + u + 4 * i);
                 };
+#ifndef SDRG_CHAIN_SRC1  // the running sum as the adds' second operand (a partial-EXEC dependent chain issues
+#define SDRG_CHAIN_SRC1 0  // sooner that way, tools/lab/lpf_exec.hip); a + b == b + a exactly
+#endif
+                auto add = [&](float x) {
+                    if (SDRG_CHAIN_SRC1) asm volatile("v_add_f32 %0, %1, %0" : "+v"(acc) : "v"(x));
+                    else acc += x;
+                    return acc;
+                };
                 auto sum16 = [&](const float4 (&X)[4], int u) {
                     float4 r[4];
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
-                        acc += X[i].x; r[i].x = acc;
-                        acc += X[i].y; r[i].y = acc;
-                        acc += X[i].z; r[i].z = acc;
-                        acc += X[i].w; r[i].w = acc;
+                        r[i].x = add(X[i].x);
+                        r[i].y = add(X[i].y);
+                        r[i].z = add(X[i].z);
+                        r[i].w = add(X[i].w);
                     }
 #pragma unroll
                     for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];

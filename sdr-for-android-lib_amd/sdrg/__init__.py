@@ -30,6 +30,7 @@ CF32, CS8, CU8, CS16, CS12 = 0, 1, 2, 3, 4
 STAGE_SPECTRUM, STAGE_STATS, STAGE_SSB, STAGE_HOT_PATH = 1, 2, 4, 7
 STAGE_SPECTRAL_PULSE, STAGE_AUDIO_PULSE, STAGE_ALL = 8, 16, 31
 PIPELINE_OFF, PIPELINE_ON, PIPELINE_INPUTS_READY = 0, 1, 2  # sdrg_engine_set_pipelining modes
+PIPELINE_STATS_ASYNC = 4  # OR'ed with ON / INPUTS_READY: statistics on a stream of their own
 PULSE_SPECTRAL, PULSE_AUDIO = 0, 1
 STATUS = {0: "SDRG_OK", -1: "SDRG_E_INVALID", -2: "SDRG_E_UNSUPPORTED", -3: "SDRG_E_NOMEM", -4: "SDRG_E_HIP",
           -5: "SDRG_E_NODEVICE"}
@@ -80,7 +81,7 @@ EXPORTS = [
     "sdrg_abi_version", "sdrg_last_error", "sdrg_ssb_pcm_len", "sdrg_focus_window", "sdrg_host_alloc", "sdrg_host_free", "sdrg_ssb_design", "sdrg_engine_create", "sdrg_engine_destroy",
     "sdrg_engine_apply_config", "sdrg_engine_set_frequency", "sdrg_engine_set_frequency_focus_range",
     "sdrg_engine_set_sound_mode", "sdrg_engine_set_sample_rate", "sdrg_engine_set_samples_per_reading",
-    "sdrg_engine_input_released", "sdrg_engine_wait_input_released", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
+    "sdrg_engine_input_released", "sdrg_engine_wait_input_released", "sdrg_engine_wait_outputs", "sdrg_engine_set_upper_sideband", "sdrg_engine_get_config", "sdrg_engine_n_streams", "sdrg_engine_pcm_len",
     "sdrg_engine_reset_state", "sdrg_engine_process_device", "sdrg_engine_synchronize", "sdrg_engine_set_stream",
     "sdrg_engine_set_pipelining", "sdrg_engine_set_ssb_variant", "sdrg_engine_get_ssb_variant",
     "sdrg_engine_process_host", "sdrg_engine_signal_strength_device", "sdrg_engine_signal_strength_host",
@@ -218,6 +219,7 @@ def load() -> ctypes.CDLL:
         "sdrg_engine_reset_state": (_I32, [P]),
         "sdrg_engine_process_device": (_I32, [P, P, _I32, _I32, P, P, P, _I64]),
         "sdrg_engine_synchronize": (_I32, [P]),
+        "sdrg_engine_wait_outputs": (_I32, [P, P]),
         "sdrg_engine_set_stream": (_I32, [P, P]),
         "sdrg_engine_set_pipelining": (_I32, [P, _I32]),
         "sdrg_engine_set_ssb_variant": (_I32, [P, ctypes.c_double, _I32]),
@@ -520,9 +522,14 @@ class Engine:
     def synchronize(self) -> None:
         _check(load().sdrg_engine_synchronize(self._h), "synchronize")
 
+    def wait_outputs(self, hip_stream: int | None = None) -> None:
+        """Enqueue on hip_stream (None: the engine's main stream) a wait for every output of the last call."""
+        _check(load().sdrg_engine_wait_outputs(self._h, hip_stream), "wait_outputs")
+
     def set_pipelining(self, mode) -> None:
         """Overlap each call's SSB stages with the next call's spectrum (see include/sdrg.h): False/PIPELINE_OFF,
-        True/PIPELINE_ON, or PIPELINE_INPUTS_READY (iq complete at call time: no wait on the main stream)."""
+        True/PIPELINE_ON, or PIPELINE_INPUTS_READY (iq complete at call time: no wait on the main stream); ON or
+        INPUTS_READY | PIPELINE_STATS_ASYNC also runs each call's statistics beside the next call's spectrum."""
         _check(load().sdrg_engine_set_pipelining(self._h, int(mode)), "set_pipelining")
 
     def set_ssb_variant(self, nco_hz: float = 0.0, fir_taps: int = 0) -> None:

@@ -325,8 +325,9 @@ def test_ingest_cs12_reads_to_engine(S, O):
 
 def test_pipelined_calls_equal_joined_calls(S, O):
     """sdrg_engine_set_pipelining: each call's SSB stages overlap the next call's spectrum; after synchronize
-    every output (spectra, records, PCM, both pulse detectors) equals the joined schedule bit for bit, in both
-    pipelined modes (the SSB stage forked from the main stream, and the inputs-ready mode with no fork)."""
+    every output (spectra, records, PCM, both pulse detectors) equals the joined schedule bit for bit, in every
+    pipelined mode (the SSB stage forked from the main stream, the inputs-ready mode with no fork, and both with the
+    statistics on a stream of their own, SDRG_PIPELINE_STATS_ASYNC)."""
     import torch
     n, fs, B, F = 16384, 2_000_000, 256, 4
     dev = torch.device("cuda:0")
@@ -334,7 +335,9 @@ def test_pipelined_calls_equal_joined_calls(S, O):
                                                       seed=100 * f + b)[0] for b in range(B)])).to(dev)
             for f in range(F)]
     outs = {}
-    for mode in (S.PIPELINE_OFF, S.PIPELINE_ON, S.PIPELINE_INPUTS_READY):
+    modes = (S.PIPELINE_OFF, S.PIPELINE_ON, S.PIPELINE_INPUTS_READY, S.PIPELINE_ON | S.PIPELINE_STATS_ASYNC,
+             S.PIPELINE_INPUTS_READY | S.PIPELINE_STATS_ASYNC)
+    for mode in modes:
         eng = engine(S, n, fs, B)
         eng.set_pipelining(mode)
         spec = [torch.empty((B, n), dtype=torch.float32, device=dev) for _ in range(F)]
@@ -349,7 +352,47 @@ def test_pipelined_calls_equal_joined_calls(S, O):
         outs[mode] = (torch.stack(spec).cpu(), torch.stack(rec).cpu(), torch.stack(pcm).cpu(), sp, au)
         eng.close()
     a = outs[S.PIPELINE_OFF]
-    for mode in (S.PIPELINE_ON, S.PIPELINE_INPUTS_READY):
+    for mode in modes[1:]:
         b = outs[mode]
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]), mode
         assert a[3].tobytes() == b[3].tobytes() and a[4].tobytes() == b[4].tobytes(), mode
+
+
+@pytest.mark.parametrize("shared_spectra", [True, False])
+def test_async_statistics_keep_their_spectra(S, O, shared_spectra):
+    """SDRG_PIPELINE_STATS_ASYNC with ONE spectra buffer for every call (the engine makes each spectrum wait for the
+    previous call's statistics) or three rotated ones (no wait): every call's records equal the joined schedule's
+    bit for bit, also at 65536 points (four-step FFT + the wide statistics kernel at 200 kHz); a consumer stream that
+    waits with sdrg_engine_wait_outputs sees each call's records complete."""
+    import torch
+    dev = torch.device("cuda:0")
+    for n, B, focus, fmt in ((16384, 256, 5, O.CS8), (65536, 16, 200, O.CS16)):
+        fs, F = 2_000_000, 6
+        raws = [torch.from_numpy(np.stack([O.synth_frames(1, n, fmt, tone_hz=700.0 * (b % 7) - 2000.0, fs=fs,
+                                                          seed=31 * f + b)[0] for b in range(B)])).to(dev)
+                for f in range(F)]
+        got = {}
+        for mode in (S.PIPELINE_OFF, S.PIPELINE_INPUTS_READY | S.PIPELINE_STATS_ASYNC):
+            eng = engine(S, n, fs, B, focus=focus)
+            eng.set_pipelining(mode)
+            nspec = 1 if (shared_spectra or mode == S.PIPELINE_OFF) else 3
+            spec = [torch.empty((B, n), dtype=torch.float32, device=dev) for _ in range(nspec)]
+            rec = [torch.zeros((B, S.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev) for _ in range(F)]
+            copies = [torch.zeros_like(r) for r in rec]
+            side = torch.cuda.Stream(dev)
+            torch.cuda.synchronize()
+            for f in range(F):
+                st = S.STAGE_SPECTRUM | S.STAGE_STATS | S.STAGE_SPECTRAL_PULSE
+                eng.process_device(raws[f].data_ptr(), fmt, st, spec[f % nspec].data_ptr(), rec[f].data_ptr(), None,
+                                   1000 + 8 * f)
+                eng.wait_outputs(side.cuda_stream)  # the consumer: copies this call's records on its own stream
+                with torch.cuda.stream(side):
+                    copies[f].copy_(rec[f])
+            eng.synchronize()
+            torch.cuda.synchronize()
+            got[mode] = (torch.stack(rec).cpu(), torch.stack(copies).cpu(), eng.pulse_outputs(audio=False)[0].tobytes())
+            eng.close()
+        a, b = got[S.PIPELINE_OFF], got[S.PIPELINE_INPUTS_READY | S.PIPELINE_STATS_ASYNC]
+        assert torch.equal(a[0], b[0]), n
+        assert torch.equal(b[0], b[1]), n  # the consumer stream saw complete records
+        assert a[2] == b[2], n
