@@ -50,9 +50,18 @@ private:
 // Launchers (defined in the .hip translation units).  All are asynchronous on `stream`.
 // ------------------------------------------------------------------------------------------------
 // Spectrum kernels, every N in [1, 2^20]: powers of two 64 .. 16384 one LDS-resident workgroup per frame,
-// 32768/65536 two-kernel four-step in waves of SPECTRUM_WAVE_FRAMES frames (intermediate in `scratch`,
-// spectrum_scratch_floats() floats); every other N through fftany.hip (mixed radix, four-step, Bluestein).
-constexpr int SPECTRUM_WAVE_FRAMES = 128;
+// 32768/65536 two-kernel four-step in waves of spectrum_wave_frames(n) frames, 128 MiB of complex intermediate
+// (`scratch`, spectrum_scratch_floats() floats) that stays in the 256 MiB Infinity Cache (measured at 65536:
+// 64 / 128 / 256 / 512 frames per wave 0.418 / 0.356 / 0.318 / 0.393 ms per 1024 frames); every other N through
+// fftany.hip (mixed radix, four-step, Bluestein).
+#ifndef SDRG_SPECTRUM_WAVE_FRAMES  // lab override of the 65536-point wave (tools/build_variant.sh); 0: 128 MiB
+#define SDRG_SPECTRUM_WAVE_FRAMES 0
+#endif
+constexpr size_t SPECTRUM_WAVE_BYTES = (size_t)128 << 20;
+inline int spectrum_wave_frames(int n) {
+    if (SDRG_SPECTRUM_WAVE_FRAMES > 0) return SDRG_SPECTRUM_WAVE_FRAMES * (65536 / n);
+    return (int)(SPECTRUM_WAVE_BYTES / ((size_t)n * 8));
+}
 bool spectrum_supported(int n);
 size_t spectrum_scratch_floats(int n, int n_frames);
 // Twiddle buffer the spectrum kernels read (floats) and its contents for frame size n.

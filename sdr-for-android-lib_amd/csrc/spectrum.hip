@@ -794,7 +794,7 @@ bool spectrum_supported(int n) { return n >= 1 && n <= (1 << 20); }
 size_t spectrum_scratch_floats(int n, int n_frames) {
     if (!pow2_kernels(n)) return any_scratch_floats(any_plan(n), n_frames);
     if (n <= 16384) return 0;
-    const int wave = n_frames < SPECTRUM_WAVE_FRAMES ? n_frames : SPECTRUM_WAVE_FRAMES;
+    const int wave = n_frames < spectrum_wave_frames(n) ? n_frames : spectrum_wave_frames(n);
     return (size_t)wave * n * 2;
 }
 
@@ -803,8 +803,8 @@ hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const f
     if (n_frames <= 0) return hipSuccess;
     if (!pow2_kernels(n)) return launch_spectrum_any(any_plan(n), iq, fmt, n_frames, twiddles, spectra, scratch, stream);
     switch (n) {
-    case 32768: return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
-    case 65536: return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, SPECTRUM_WAVE_FRAMES, stream);
+    case 32768: return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream);
+    case 65536: return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream);
     case 16384: return k16::launch_fmt(iq, fmt, n_frames, twiddles + spectrum_k16_tables_offset(), spectra, stream,
                                       beside_ssb ? 1 : 2, n_cus);
     case 64: return launch_n<6>(iq, fmt, n_frames, twiddles, spectra, stream);
