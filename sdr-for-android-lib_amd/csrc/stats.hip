@@ -130,16 +130,53 @@ struct WideScan {
     int peak_idx;
 };
 
+// Which wave takes which role of scan_wide.  SDRG_WIDE_MAP 0: by wave index (wave 0 chains).  1: by placement -- when the
+// workgroup's four waves sit on four distinct SIMDs (HW_ID SIMD_ID), the chain role goes to the wave on SIMD
+// (TG_ID mod 4), so the four frames sharing a CU (thread-group slots 0-3) put their chain waves on four different
+// SIMDs instead of all on the SIMD of wave 0; otherwise by wave index.  SDRG_WIDE_PRIO: the chain wave's issue
+// priority during the scan.
+#ifndef SDRG_WIDE_MAP
+#define SDRG_WIDE_MAP 0
+#endif
+#ifndef SDRG_WIDE_PRIO
+#define SDRG_WIDE_PRIO 0
+#endif
+// SDRG_WIDE_SETS: register sets of 16 bins the chain wave cycles through (its LDS reads run SETS - 1 half-steps
+// ahead of the adds); SDRG_WIDE_PF: chunks the producers fetch ahead into registers (1 or 2)
+#ifndef SDRG_WIDE_SETS
+#define SDRG_WIDE_SETS 2
+#endif
+#ifndef SDRG_WIDE_PF
+#define SDRG_WIDE_PF 1
+#endif
+#ifndef SDRG_WIDE_FULLEXEC
+#define SDRG_WIDE_FULLEXEC 0
+#endif
+__device__ __forceinline__ unsigned hw_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+    return v;
+}
+// sh_hw: the four waves' HW_ID words, written by wide_publish and read after a barrier
+__device__ __forceinline__ void wide_publish(unsigned *sh_hw) {
+    if (SDRG_WIDE_MAP && (threadIdx.x & 63) == 0) sh_hw[threadIdx.x >> 6] = hw_id();
+}
+__device__ __forceinline__ int wide_role(const unsigned *sh_hw) {
+    const int wv = threadIdx.x >> 6;
+    if (!SDRG_WIDE_MAP) return wv;
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) m |= 1u << ((sh_hw[i] >> 4) & 3);
+    if (m != 15) return wv;
+    const int tg = (sh_hw[0] >> 16) & 3;
+    return (int)(((sh_hw[wv] >> 4) & 3) - tg) & 3;
+}
+
 template <bool want_db>
 __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, const int *wlo, const int *whi, int w,
-                          WideScan &out) {
-    // roles by wave: 0 chains, 1 records, 2-3 producers.  (Rotating the roles with the block index, so that the
-    // frames sharing a CU put their chain waves on different SIMDs, measured slower: the chain wave then shares
-    // its SIMD with the producers' issue-dense log10s.)
-#ifndef SDRG_WIDE_ROTATE  // lab: roles rotated with the block index (frames sharing a CU put their chain waves apart)
-#define SDRG_WIDE_ROTATE 0
-#endif
-    const int lane = threadIdx.x & 63, role = ((threadIdx.x >> 6) + (SDRG_WIDE_ROTATE ? (int)blockIdx.x : 0)) & 3;
+                          int role, WideScan &out) {
+    // roles (0 chains, 1 records, 2-3 producers) are dealt to the waves by the caller (wide_role)
+    const int lane = threadIdx.x & 63;
     const int fq = nwin - 1;
     // SC = 2^lg bins per window per chunk, the largest that fits; rows are RS = SC + 4 floats apart, so the chain
     // lanes' float4 accesses (one row each, same bin) fall in different LDS banks
@@ -177,17 +214,19 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
     const int plo = wlo[pq], plen = whi[pq] - plo + 1;
     const float *Pq = P + plo;
     float va[PR], vb[PR];
-    auto fetch = [&](int c) {
+    float va2[SDRG_WIDE_PF == 2 ? PR : 1], vb2[SDRG_WIDE_PF == 2 ? PR : 1];  // the chunk after next (SDRG_WIDE_PF 2)
+    auto fetch_into = [&](auto &xa, auto &xb, int c) {
         const int c0 = c << lg;
 #pragma unroll
         for (int k = 0; k < PR; k++) {
             const int t = pk0 + PG * k, e = c0 + t;
             const bool ok = t < SC && e < plen;
-            va[k] = ok ? Pq[e] : 0.0f;
-            vb[k] = (ok && e >= w) ? Pq[e - w] : 0.0f;
+            xa[k] = ok ? Pq[e] : 0.0f;
+            xb[k] = (ok && e >= w) ? Pq[e - w] : 0.0f;
         }
     };
-    auto store = [&](int c) {
+    auto fetch = [&](int c) { fetch_into(va, vb, c); };
+    auto store_from = [&](const auto &va, const auto &vb, int c) {
         const int c0 = c << lg;
         float *row = ring + (c & 1) * slot_floats + pq * 3 * RS;
 #pragma unroll
@@ -209,21 +248,37 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
             __builtin_amdgcn_sched_barrier(0);  // one bin's log10 at a time: interleaved they would hold ~70 VGPRs
         }
     };
+    auto store = [&](int c) { store_from(va, vb, c); };
     if (prod && nch > 0) fetch(0);
+    if (SDRG_WIDE_PF == 2 && prod && nch > 1) fetch_into(va2, vb2, 1);
 
     unsigned long long busy = 0;
     for (int c = 0; c <= nch + 1; c++) {
         const unsigned long long t_in = SDRG_STATS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
         if (role >= 2) {
             if (prod && c < nch) {
-                store(c);
-                if (c + 1 < nch) fetch(c + 1);
+                if constexpr (SDRG_WIDE_PF == 2) {  // chunk c + 2 into the registers chunk c came from
+                    if ((c & 1) == 0) {
+                        store(c);
+                        if (c + 2 < nch) fetch(c + 2);
+                    } else {
+                        store_from(va2, vb2, c);
+                        if (c + 2 < nch) fetch_into(va2, vb2, c + 2);
+                    }
+                } else {
+                    store(c);
+                    if (c + 1 < nch) fetch(c + 1);
+                }
             }
         } else if (role == 0) {
-            if (c >= 1 && c <= nch && chain) {
+            if (SDRG_WIDE_PRIO && c == 1) __builtin_amdgcn_s_setprio(SDRG_WIDE_PRIO);
+            if (c >= 1 && c <= nch && (SDRG_WIDE_FULLEXEC || chain)) {
+                // SDRG_WIDE_FULLEXEC: the wave's other lanes replay lane 0 (window 0's sum: same row, same values,
+                // the same bytes written back), so the chain's adds issue with a full EXEC mask
+                const int cj = (SDRG_WIDE_FULLEXEC && !chain) ? 0 : j, cg = (SDRG_WIDE_FULLEXEC && !chain) ? 0 : grp;
                 const float *slot = ring + ((c - 1) & 1) * slot_floats;
-                const float *src = slot + (j * 3 + grp) * RS;  // x, rs terms, dB rows
-                float *dst = grp == 1 ? rsring + (((c - 1) & 1) * nwin + j) * RS : const_cast<float *>(src);
+                const float *src = slot + (cj * 3 + cg) * RS;  // x, rs terms, dB rows
+                float *dst = cg == 1 ? rsring + (((c - 1) & 1) * nwin + cj) * RS : const_cast<float *>(src);
                 // 16 bins per half-step, the next half's four float4 read before this half's adds (two register
                 // sets, no copies), so the LDS latency hides under 16 dependent adds
                 float4 A[4], B[4];
@@ -251,12 +306,45 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
 #pragma unroll
                     for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];
                 };
-                rd(A, 0);
-                for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
-                    rd(B, t + 16);
-                    sum16(A, t);
-                    if (t + 32 < SC) rd(A, t + 32);
-                    sum16(B, t + 16);
+                if constexpr (SDRG_WIDE_SETS == 2) {
+                    rd(A, 0);
+                    for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
+                        rd(B, t + 16);
+                        sum16(A, t);
+                        if (t + 32 < SC) rd(A, t + 32);
+                        sum16(B, t + 16);
+                    }
+                } else if constexpr (SDRG_WIDE_SETS == 3) {  // reads two half-steps ahead
+                    float4 C[4];
+                    rd(A, 0);
+                    rd(B, 16);
+                    for (int t = 0; t < SC; t += 48) {
+                        if (t + 32 < SC) rd(C, t + 32);
+                        sum16(A, t);
+                        if (t + 16 < SC) {
+                            if (t + 48 < SC) rd(A, t + 48);
+                            sum16(B, t + 16);
+                        }
+                        if (t + 32 < SC) {
+                            if (t + 64 < SC) rd(B, t + 64);
+                            sum16(C, t + 32);
+                        }
+                    }
+                } else {  // four sets: reads three half-steps ahead (SC a multiple of 64)
+                    float4 C[4], D[4];
+                    rd(A, 0);
+                    rd(B, 16);
+                    rd(C, 32);
+                    for (int t = 0; t < SC; t += 64) {
+                        rd(D, t + 48);
+                        sum16(A, t);
+                        if (t + 64 < SC) rd(A, t + 64);
+                        sum16(B, t + 16);
+                        if (t + 64 < SC) rd(B, t + 80);
+                        sum16(C, t + 32);
+                        if (t + 64 < SC) rd(C, t + 96);
+                        sum16(D, t + 48);
+                    }
                 }
             }
         } else if (c >= 2 && rec_lane) {
@@ -284,6 +372,7 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
         if (SDRG_STATS_STAMPS) busy += __builtin_amdgcn_s_memtime() - t_in;
         __syncthreads();
     }
+    if (SDRG_WIDE_PRIO && role == 0) __builtin_amdgcn_s_setprio(0);
     if (SDRG_STATS_STAMPS && lane == 0 && role <= 2 && blockIdx.x < 8192)
         g_stats_stamps[blockIdx.x * STAMP_PHASES + 6 + role] = busy;
     if (role >= 2) {  // first maximum over the producer threads (lower bin on ties)
@@ -649,6 +738,7 @@ __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restr
     extern __shared__ __attribute__((aligned(16))) float stage[];
     __shared__ int sh_woff[12];
     __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
+    __shared__ unsigned sh_hw[4];                   // wide_role
     __shared__ __attribute__((aligned(16))) int hist[256];
     __shared__ uint32_t sh_xch[2];
     __shared__ float w_mean_db[10], w_best1k_db[10];
@@ -908,6 +998,7 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ int w_lo[10], w_hi[10], order[10];
     __shared__ float sh_f[4];
     __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
+    __shared__ unsigned sh_hw[4];                   // wide_role
 
     const int lane = threadIdx.x;
     const size_t frame = blockIdx.x;
@@ -926,7 +1017,9 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
         sh_geo_lo[n_ref] = g.focus_lo;
         sh_geo_hi[n_ref] = g.focus_hi;
     }
+    wide_publish(sh_hw);
     __syncthreads();
+    const int role = wide_role(sh_hw);
     const float *P = spectra + frame * (size_t)g.n;
     float *pool = gpool + frame * (size_t)gpool_stride;
     StatsState st = state[frame];
@@ -942,9 +1035,9 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
         const bool spec_pool = n_ref >= 2 && n_bottom == 1;  // pooled-bin sum = one window's dB sum
         STATS_STAMP(0);
         if (spec_pool)
-            scan_wide<true>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, sh_wide);
+            scan_wide<true>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, role, sh_wide);
         else
-            scan_wide<false>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, sh_wide);
+            scan_wide<false>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, role, sh_wide);
         STATS_STAMP(1);
         const float abs_peak_db = sh_wide.peak_db;  // 6.2 focus peak (fft_process.cpp:142-154)
         const int peak_bin = sh_wide.peak_idx;
