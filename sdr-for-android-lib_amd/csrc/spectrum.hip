@@ -689,6 +689,127 @@ __global__ __launch_bounds__(TILE_B) void four_step_b(const f2 *__restrict__ Y, 
     tile_pass<N, N2, TP::RB, TP::RA, false, true, TILE_B>(lds, t_hi, t_lo, noload, store);
 }
 
+// Persistent forms of the two four-step kernels (SDRG_FOUR_PERSIST): a grid of a few workgroups per CU loops over
+// the wave's tiles, loads the twiddle tables once, and fetches the NEXT tile's inputs into registers (raw 8/16-bit
+// words for kernel A, the staged rows for kernel B) before running this tile's FFT, so HBM / Infinity Cache latency
+// overlaps the LDS passes instead of following them.  Same arithmetic as four_step_a / four_step_b.
+#ifndef SDRG_FOUR_PERSIST
+#define SDRG_FOUR_PERSIST 0
+#endif
+template <int FMT>
+__device__ __forceinline__ f2 convert_scaled(uint32_t v) {  // load_sample's value from its raw word
+    if constexpr (FMT == SDRG_IQ_CS8) {
+        return f2{(float)(int8_t)(v & 0xff), (float)(int8_t)((v >> 8) & 0xff)} * (1.0f / 128.0f);
+    } else if constexpr (FMT == SDRG_IQ_CU8) {
+        return (f2{(float)(v & 0xff), (float)((v >> 8) & 0xff)} - 127.4f) * (1.0f / 128.0f);
+    } else {
+        return f2{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * (1.0f / 32768.0f);
+    }
+}
+
+template <int LOG2N1, int LOG2N2, int FMT>
+__global__ __launch_bounds__(TILE_A) void four_step_a_p(const void *__restrict__ iq, f2 *__restrict__ Y,
+                                                         const f2 *__restrict__ tw, int n_frames) {
+    constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
+    using TP = TilePlan<N1, TILE_A>;
+    constexpr int C = TP::C, R = TP::RA, TPF = N2 / C, NB = (C * N1 / R) / TILE_A, JS = TILE_A / C;
+    constexpr int BPS = bytes_per_sample<FMT>();
+    __shared__ __attribute__((aligned(16))) f2 lds[C * TP::LP];
+    __shared__ f2 t_hi[N / 256], t_lo[256];
+    load_tw_tables<N>(tw, t_hi, t_lo);
+    __syncthreads();
+    const int total = n_frames * TPF;
+    const int c = threadIdx.x % C, jj = threadIdx.x / C;  // pass 1: column c, butterflies j = jj + b * JS
+    constexpr bool RAW = FMT != SDRG_IQ_CF32;
+    uint32_t raw[NB][R];
+    auto issue = [&](int tile) {
+        const int frame = tile / TPF, c0 = (tile % TPF) * C;
+        const __amdgpu_buffer_rsrc_t rs =
+            frame_rsrc(reinterpret_cast<const char *>(iq) + (size_t)frame * N * BPS, N * BPS);
+#pragma unroll
+        for (int b = 0; b < NB; b++)
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                raw[b][r] = load_raw_word<FMT>(rs, (c0 + c) * BPS, N2 * (jj + b * JS + r * (N1 / R)) * BPS);
+    };
+    int tile = blockIdx.x;
+    if constexpr (RAW)
+        if (tile < total) issue(tile);
+    for (; tile < total; tile += gridDim.x) {
+        const int frame = tile / TPF, c0 = (tile % TPF) * C;
+        f2 x[NB][R];
+        if constexpr (RAW) {
+#pragma unroll
+            for (int b = 0; b < NB; b++)
+#pragma unroll
+                for (int r = 0; r < R; r++) x[b][r] = convert_scaled<FMT>(raw[b][r]);
+            if (tile + (int)gridDim.x < total) issue(tile + gridDim.x);
+        } else {
+            const f2 *src = reinterpret_cast<const f2 *>(iq) + (size_t)frame * N;
+#pragma unroll
+            for (int b = 0; b < NB; b++)
+#pragma unroll
+                for (int r = 0; r < R; r++) x[b][r] = src[N2 * (jj + b * JS + r * (N1 / R)) + c0 + c];
+        }
+        // pass 1 (NS = 1): DFT over n1, outputs to the column's LDS slots j * R + r
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+            dft<R>(x[b]);
+#pragma unroll
+            for (int r = 0; r < R; r++) lds[c * TP::LP + (jj + b * JS) * R + r] = x[b][r];
+        }
+        __syncthreads();
+        f2 *y = Y + (size_t)frame * N;
+        auto noload = [](int, int) { return f2{0.0f, 0.0f}; };
+        auto store = [&](int cc, int k1, f2 v) {
+            const int n2 = c0 + cc;
+            y[k1 * N2 + n2] = cmul_v(v, tw_lds<1>(t_hi, t_lo, (n2 * k1) & (N - 1)));
+        };
+        // pass 2 reads the tile, then a barrier (inside), so the next tile's pass-1 writes are safe
+        tile_pass<N, N1, TP::RB, TP::RA, false, true, TILE_A>(lds, t_hi, t_lo, noload, store);
+    }
+}
+
+template <int LOG2N1, int LOG2N2>
+__global__ __launch_bounds__(TILE_B) void four_step_b_p(const f2 *__restrict__ Y, float *__restrict__ spectra,
+                                                         const f2 *__restrict__ tw, int n_frames) {
+    constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
+    using TP = TilePlan<N2, TILE_B>;
+    constexpr int C = TP::C, TPF = N1 / C, S = C * N2 / TILE_B;
+    __shared__ __attribute__((aligned(16))) f2 lds[C * TP::LP];
+    __shared__ f2 t_hi[N / 256], t_lo[256];
+    load_tw_tables<N>(tw, t_hi, t_lo);  // visible after the first staging barrier
+    const int total = n_frames * TPF;
+    f2 stage[S];
+    auto issue = [&](int tile) {
+        const int frame = tile / TPF, r0 = (tile % TPF) * C;
+        const f2 *y = Y + (size_t)frame * N + (size_t)r0 * N2;
+#pragma unroll
+        for (int i = 0; i < S; ++i) stage[i] = y[threadIdx.x + i * TILE_B];
+    };
+    int tile = blockIdx.x;
+    if (tile < total) issue(tile);
+    for (; tile < total; tile += gridDim.x) {
+        const int frame = tile / TPF, r0 = (tile % TPF) * C;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            const int e = threadIdx.x + i * TILE_B;
+            lds[(e / N2) * TP::LP + (e % N2)] = stage[i];
+        }
+        if (tile + (int)gridDim.x < total) issue(tile + gridDim.x);
+        __syncthreads();
+        float *out = spectra + (size_t)frame * N;
+        auto noload = [](int, int) { return f2{0.0f, 0.0f}; };
+        auto none = [](int, int, f2) {};
+        auto store = [&](int rho, int k2, f2 v) {
+            const int k = r0 + rho + N1 * k2;
+            out[(k + N / 2) & (N - 1)] = v.x * v.x + v.y * v.y;
+        };
+        tile_pass<N, N2, TP::RA, 1, false, false, TILE_B>(lds, t_hi, t_lo, noload, none);
+        tile_pass<N, N2, TP::RB, TP::RA, false, true, TILE_B>(lds, t_hi, t_lo, noload, store);
+    }
+}
+
 template <int LOG2N1, int LOG2N2, int FMT>
 hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, float *spectra, float *scratch,
                             int wave, hipStream_t s) {
@@ -698,6 +819,15 @@ hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, floa
     for (int f0 = 0; f0 < n_frames; f0 += wave) {
         const int nf = (n_frames - f0) < wave ? (n_frames - f0) : wave;
         const char *src = reinterpret_cast<const char *>(iq) + (size_t)f0 * N * bytes_per_sample<FMT>();
+        if (SDRG_FOUR_PERSIST) {
+            const int cus = k16::device_cus();
+            const int ta = nf * (N2 / TilePlan<N1, TILE_A>::C), tb = nf * (N1 / TilePlan<N2, TILE_B>::C);
+            const int ga = ta < 2 * cus ? ta : 2 * cus, gb = tb < 4 * cus ? tb : 4 * cus;
+            hipLaunchKernelGGL((four_step_a_p<LOG2N1, LOG2N2, FMT>), dim3(ga), dim3(TILE_A), 0, s, src, Y, tw, nf);
+            hipLaunchKernelGGL((four_step_b_p<LOG2N1, LOG2N2>), dim3(gb), dim3(TILE_B), 0, s, Y, spectra + (size_t)f0 * N,
+                               tw, nf);
+            continue;
+        }
         hipLaunchKernelGGL((four_step_a<LOG2N1, LOG2N2, FMT>), dim3(N2 / TilePlan<N1, TILE_A>::C, nf), dim3(TILE_A), 0,
                            s, src, Y, tw);
         hipLaunchKernelGGL((four_step_b<LOG2N1, LOG2N2>), dim3(N1 / TilePlan<N2, TILE_B>::C, nf), dim3(TILE_B), 0, s, Y,

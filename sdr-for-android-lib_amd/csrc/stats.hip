@@ -152,6 +152,9 @@ struct WideScan {
 #ifndef SDRG_WIDE_FULLEXEC
 #define SDRG_WIDE_FULLEXEC 0
 #endif
+#ifndef SDRG_WIDE_DBPOOL
+#define SDRG_WIDE_DBPOOL 0
+#endif
 __device__ __forceinline__ unsigned hw_id() {
     unsigned v;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
@@ -174,7 +177,7 @@ __device__ __forceinline__ int wide_role(const unsigned *sh_hw) {
 
 template <bool want_db>
 __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, const int *wlo, const int *whi, int w,
-                          int role, WideScan &out) {
+                          int role, float *__restrict__ dbp, int wst, WideScan &out) {
     // roles (0 chains, 1 records, 2-3 producers) are dealt to the waves by the caller (wide_role)
     const int lane = threadIdx.x & 63;
     const int fq = nwin - 1;
@@ -239,6 +242,9 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
                 row[RS + t] = (e >= w) ? v - vb[k] : v;
                 const float d = db_of(v);
                 if (want_db) row[2 * RS + t] = in ? d : 0.0f;
+                // SDRG_WIDE_DBPOOL: the reference windows' dB values also go to the frame's pool scratch, where the
+                // pooled-gap pass reads the bottom window's instead of evaluating its logs again
+                if (SDRG_WIDE_DBPOOL && want_db && in && pq < fq) dbp[pq * wst + e] = d;
                 // a thread sees its focus bins in increasing order: strict > keeps its first maximum
                 if (in && pq == fq && d > pk) {
                     pk = d;
@@ -1034,10 +1040,11 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
         const int n_bottom = n_bottom_of(n_ref);
         const bool spec_pool = n_ref >= 2 && n_bottom == 1;  // pooled-bin sum = one window's dB sum
         STATS_STAMP(0);
+        const int wst = (g.max_pool + 3) & ~3;  // SDRG_WIDE_DBPOOL: window q's dB values at pool + q * wst
         if (spec_pool)
-            scan_wide<true>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, role, sh_wide);
+            scan_wide<true>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, role, pool, wst, sh_wide);
         else
-            scan_wide<false>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, role, sh_wide);
+            scan_wide<false>(P, dyn, n_ref + 1, sh_geo_lo, sh_geo_hi, w1k, role, pool, wst, sh_wide);
         STATS_STAMP(1);
         const float abs_peak_db = sh_wide.peak_db;  // 6.2 focus peak (fft_process.cpp:142-154)
         const int peak_bin = sh_wide.peak_idx;
@@ -1109,15 +1116,26 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
                 if (cnt <= REG_POOL * WG) {
                     // gaps in registers: the select's passes read no memory
                     float v[REG_POOL];
+                    if constexpr (SDRG_WIDE_DBPOOL) {  // the scan's dB values of window wb
+                        const float *gd = pool + wb * wst;
 #pragma unroll
-                    for (int r = 0; r < REG_POOL; r++) {
-                        const int q = lane + WG * r;
-                        v[r] = q < cnt ? P[lo + q] : 0.0f;
-                    }
+                        for (int r = 0; r < REG_POOL; r++) {
+                            const int q = lane + WG * r;
+                            v[r] = q < cnt ? gd[q] : m;
+                        }
 #pragma unroll
-                    for (int r = 0; r < REG_POOL; r++) {
-                        v[r] = fabsf(db_of(v[r]) - m);
-                        __builtin_amdgcn_sched_barrier(0);  // one log10 at a time (register pressure)
+                        for (int r = 0; r < REG_POOL; r++) v[r] = fabsf(v[r] - m);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < REG_POOL; r++) {
+                            const int q = lane + WG * r;
+                            v[r] = q < cnt ? P[lo + q] : 0.0f;
+                        }
+#pragma unroll
+                        for (int r = 0; r < REG_POOL; r++) {
+                            v[r] = fabsf(db_of(v[r]) - m);
+                            __builtin_amdgcn_sched_barrier(0);  // one log10 at a time (register pressure)
+                        }
                     }
                     STATS_STAMP(3);
                     med = kth_smallest<WG>(
@@ -1190,9 +1208,17 @@ static int stage_bins(const StatsGeometry &geo) {
 }
 static bool wide_for(const StatsGeometry &geo) { return stage_bins(geo) > STAGE_MAX; }
 static bool global_pool_for(const StatsGeometry &geo) { return wide_for(geo); }
+// floats of pool scratch per frame: the pooled bins, or (SDRG_WIDE_DBPOOL, one bottom window) every reference window's
+// dB values, window q at q * wst
+static int pool_stride_for(const StatsGeometry &geo) {
+    const int wst = (geo.max_pool + 3) & ~3;
+    const int nb0 = (int)(geo.n_ref * 0.4f);
+    const bool spec_pool = geo.n_ref >= 2 && (nb0 > 1 ? nb0 : 1) == 1;
+    return (SDRG_WIDE_DBPOOL && spec_pool) ? geo.n_ref * wst : wst;
+}
 
 size_t stats_global_pool_floats(const StatsGeometry &geo, int n_frames) {
-    return global_pool_for(geo) ? (size_t)n_frames * (size_t)((geo.max_pool + 3) & ~3) : 0;
+    return global_pool_for(geo) ? (size_t)n_frames * (size_t)pool_stride_for(geo) : 0;
 }
 
 hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry &geo, int64_t now_ms,
@@ -1201,7 +1227,7 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
     const bool global_pool = global_pool_for(geo);
     if (global_pool && !gpool) return hipErrorInvalidValue;
     if (geo.n_ref > 10) return hipErrorInvalidValue;
-    const int pool_stride = (geo.max_pool + 3) & ~3;
+    const int pool_stride = pool_stride_for(geo);
     if (wide_for(geo)) {
         size_t lds = sizeof(float) * (size_t)RING_FLOATS;
         if (SDRG_STATS_STAMPS && lab_getenv("SDRG_STATS_LDS_KB")) {  // diagnostic: fewer frames per CU
