@@ -121,7 +121,10 @@ __device__ __forceinline__ WinScan scan_window(const float *__restrict__ W, int 
 //            `rs > bv` record (bv starts at the first window's sum, bin w - 1), whose start is bestStart.
 // One barrier per chunk.
 constexpr int WIDE_WG = 256;
-constexpr int RING_FLOATS = 9216;  // 36 KiB at most: (2 slots x 3 rows + 2 rs rows) x windows x (SC + 4)
+#ifndef SDRG_WIDE_RING  // lab: the ring's floats (a smaller ring leaves LDS to the four-step kernels running beside it)
+#define SDRG_WIDE_RING 9216
+#endif
+constexpr int RING_FLOATS = SDRG_WIDE_RING;  // 36 KiB at most: (2 slots x 3 rows + 2 rs rows) x windows x (SC + 4)
 
 struct WideScan {
     float sum[11], bv[11], dsum[11];
