@@ -582,7 +582,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     }
     if (do_spec) {
         HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, sm, do_ssb && early_fork && !split,
-                                split ? e->spec_cus : 0));
+                                split ? e->spec_cus : 0, do_stats && stats_uses_wide(geo)));
         if (prof) HIP_TRY(hipEventRecord(ev->spec, sm));
     }
     if (do_ssb) {  // fork

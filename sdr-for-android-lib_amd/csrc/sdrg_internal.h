@@ -72,8 +72,13 @@ void spectrum_fill_twiddles(int n, float *out);
 // N = 16384 kernel then launches one workgroup per CU, the one that co-resides with it (measured +2-3 % per
 // step over two), instead of two per CU for the chip alone.
 // n_cus: CUs the stream may use (0 = the device's; a CU-masked stream passes its share) for persistent grids.
+// beside_wide_stats: the call's statistics take the wide kernel (its workgroups share the CUs with the next call's
+// FFT): N = 32768 / 65536 then launch one tile per workgroup instead of the persistent four-step kernels.
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles,
-                           float *spectra, float *scratch, hipStream_t stream, bool beside_ssb = false, int n_cus = 0);
+                           float *spectra, float *scratch, hipStream_t stream, bool beside_ssb = false, int n_cus = 0,
+                           bool beside_wide_stats = false);
+// true when launch_stats runs this geometry with the wide kernel (stats.hip)
+bool stats_uses_wide(const StatsGeometry &geo);
 
 // gpool: [n_frames][stats_global_pool_floats / n_frames] device scratch for the pooled-bin median when the
 // pool exceeds what the kernel keeps in LDS (stats_global_pool_floats > 0; wide focus windows at N > 65536)

@@ -689,13 +689,13 @@ __global__ __launch_bounds__(TILE_B) void four_step_b(const f2 *__restrict__ Y, 
     tile_pass<N, N2, TP::RB, TP::RA, false, true, TILE_B>(lds, t_hi, t_lo, noload, store);
 }
 
-// Persistent forms of the two four-step kernels (SDRG_FOUR_PERSIST): a grid of a few workgroups per CU loops over
-// the wave's tiles, loads the twiddle tables once, and fetches the NEXT tile's inputs into registers (raw 8/16-bit
-// words for kernel A, the staged rows for kernel B) before running this tile's FFT, so HBM / Infinity Cache latency
-// overlaps the LDS passes instead of following them.  Same arithmetic as four_step_a / four_step_b.
-#ifndef SDRG_FOUR_PERSIST
-#define SDRG_FOUR_PERSIST 0
-#endif
+// Persistent forms of the two four-step kernels: a grid of a few workgroups per CU loops over the wave's tiles, loads
+// the twiddle tables once, and fetches the NEXT tile's inputs into registers (raw 8/16-bit words for kernel A, the
+// staged rows for kernel B) before running this tile's FFT, so HBM / Infinity Cache latency overlaps the LDS passes
+// instead of following them.  Same arithmetic as four_step_a / four_step_b (the same bits).  Measured at 1024 x
+// 65536 CS16 (tools/gpu_four_persist.sh): A 42.6 -> 40.7 us, B 32.4 -> 33.1 us per 256-frame wave, the configs[4]
+// 5 kHz step 0.320 -> 0.312 ms; beside the wide statistics kernel (200 kHz focus, asynchronous statistics) they are
+// 1 % slower than the one-tile-per-workgroup kernels, so launch_spectrum takes those there (persistent = false).
 template <int FMT>
 __device__ __forceinline__ f2 convert_scaled(uint32_t v) {  // load_sample's value from its raw word
     if constexpr (FMT == SDRG_IQ_CS8) {
@@ -812,14 +812,14 @@ __global__ __launch_bounds__(TILE_B) void four_step_b_p(const f2 *__restrict__ Y
 
 template <int LOG2N1, int LOG2N2, int FMT>
 hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, float *spectra, float *scratch,
-                            int wave, hipStream_t s) {
+                            int wave, hipStream_t s, bool persistent) {
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
     const f2 *tw = reinterpret_cast<const f2 *>(twf);
     f2 *Y = reinterpret_cast<f2 *>(scratch);
     for (int f0 = 0; f0 < n_frames; f0 += wave) {
         const int nf = (n_frames - f0) < wave ? (n_frames - f0) : wave;
         const char *src = reinterpret_cast<const char *>(iq) + (size_t)f0 * N * bytes_per_sample<FMT>();
-        if (SDRG_FOUR_PERSIST) {
+        if (persistent) {
             const int cus = k16::device_cus();
             const int ta = nf * (N2 / TilePlan<N1, TILE_A>::C), tb = nf * (N1 / TilePlan<N2, TILE_B>::C);
             const int ga = ta < 2 * cus ? ta : 2 * cus, gb = tb < 4 * cus ? tb : 4 * cus;
@@ -838,12 +838,12 @@ hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, floa
 
 template <int LOG2N1, int LOG2N2>
 hipError_t launch_four_step_fmt(const void *iq, int fmt, int n_frames, const float *tw, float *spectra,
-                                float *scratch, int wave, hipStream_t s) {
+                                float *scratch, int wave, hipStream_t s, bool pe) {
     switch (fmt) {
-    case SDRG_IQ_CS8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS8>(iq, n_frames, tw, spectra, scratch, wave, s);
-    case SDRG_IQ_CU8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CU8>(iq, n_frames, tw, spectra, scratch, wave, s);
-    case SDRG_IQ_CS16: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS16>(iq, n_frames, tw, spectra, scratch, wave, s);
-    case SDRG_IQ_CF32: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CF32>(iq, n_frames, tw, spectra, scratch, wave, s);
+    case SDRG_IQ_CS8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS8>(iq, n_frames, tw, spectra, scratch, wave, s, pe);
+    case SDRG_IQ_CU8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CU8>(iq, n_frames, tw, spectra, scratch, wave, s, pe);
+    case SDRG_IQ_CS16: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS16>(iq, n_frames, tw, spectra, scratch, wave, s, pe);
+    case SDRG_IQ_CF32: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CF32>(iq, n_frames, tw, spectra, scratch, wave, s, pe);
     default: return hipErrorInvalidValue;
     }
 }
@@ -929,12 +929,16 @@ size_t spectrum_scratch_floats(int n, int n_frames) {
 }
 
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles, float *spectra,
-                           float *scratch, hipStream_t stream, bool beside_ssb, int n_cus) {
+                           float *scratch, hipStream_t stream, bool beside_ssb, int n_cus, bool beside_wide_stats) {
     if (n_frames <= 0) return hipSuccess;
     if (!pow2_kernels(n)) return launch_spectrum_any(any_plan(n), iq, fmt, n_frames, twiddles, spectra, scratch, stream);
     switch (n) {
-    case 32768: return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream);
-    case 65536: return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream);
+    case 32768:
+        return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream,
+                                          !beside_wide_stats);
+    case 65536:
+        return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream,
+                                          !beside_wide_stats);
     case 16384: return k16::launch_fmt(iq, fmt, n_frames, twiddles + spectrum_k16_tables_offset(), spectra, stream,
                                       beside_ssb ? 1 : 2, n_cus);
     case 64: return launch_n<6>(iq, fmt, n_frames, twiddles, spectra, stream);

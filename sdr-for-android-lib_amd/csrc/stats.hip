@@ -1211,6 +1211,7 @@ static int stage_bins(const StatsGeometry &geo) {
 }
 static bool wide_for(const StatsGeometry &geo) { return stage_bins(geo) > STAGE_MAX; }
 static bool global_pool_for(const StatsGeometry &geo) { return wide_for(geo); }
+bool stats_uses_wide(const StatsGeometry &geo) { return wide_for(geo); }
 // floats of pool scratch per frame: the pooled bins, or (SDRG_WIDE_DBPOOL, one bottom window) every reference window's
 // dB values, window q at q * wst
 static int pool_stride_for(const StatsGeometry &geo) {
