@@ -155,8 +155,13 @@ struct WideScan {
 #ifndef SDRG_WIDE_FULLEXEC
 #define SDRG_WIDE_FULLEXEC 0
 #endif
+// SDRG_WIDE_DBPOOL: where the pooled-gap pass (one bottom window) gets the bottom window's dB values -- 0: evaluates
+// its 13107 logs again; 1 (lab): the producers also store every reference bin's dB value to the frame's pool scratch
+// (their stores then share vmcnt with the next chunk's loads: slower); 2 (product): the record wave copies the dB rows
+// of the ring to the pool scratch (it issues no loads).  Measured at 65536 / 200 kHz: pool phase 56k -> 6.7k cycles per
+// frame, configs[4] 200 kHz step 0.5135 -> 0.4955 ms (tools/gpu_wide_db2.sh).
 #ifndef SDRG_WIDE_DBPOOL
-#define SDRG_WIDE_DBPOOL 0
+#define SDRG_WIDE_DBPOOL 2
 #endif
 __device__ __forceinline__ unsigned hw_id() {
     unsigned v;
@@ -179,7 +184,7 @@ __device__ __forceinline__ int wide_role(const unsigned *sh_hw) {
 }
 
 template <bool want_db>
-__device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, const int *wlo, const int *whi, int w,
+__device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, const int *wlo, const int *whi, int w,
                           int role, float *__restrict__ dbp, int wst, WideScan &out) {
     // roles (0 chains, 1 records, 2-3 producers) are dealt to the waves by the caller (wide_role)
     const int lane = threadIdx.x & 63;
@@ -220,8 +225,9 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
     const int plo = wlo[pq], plen = whi[pq] - plo + 1;
     const float *Pq = P + plo;
     float va[PR], vb[PR];
-    float va2[SDRG_WIDE_PF == 2 ? PR : 1], vb2[SDRG_WIDE_PF == 2 ? PR : 1];  // the chunk after next (SDRG_WIDE_PF 2)
-    auto fetch_into = [&](auto &xa, auto &xb, int c) {
+    // the chunk after next (SDRG_WIDE_PF 2), or the next chunk fetched before this chunk's stores (SDRG_WIDE_PF 3)
+    float va2[SDRG_WIDE_PF >= 2 ? PR : 1], vb2[SDRG_WIDE_PF >= 2 ? PR : 1];
+    auto fetch_into = [&](auto &xa, auto &xb, int c) __attribute__((always_inline)) {
         const int c0 = c << lg;
 #pragma unroll
         for (int k = 0; k < PR; k++) {
@@ -232,7 +238,7 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
         }
     };
     auto fetch = [&](int c) { fetch_into(va, vb, c); };
-    auto store_from = [&](const auto &va, const auto &vb, int c) {
+    auto store_from = [&](const auto &va, const auto &vb, int c) __attribute__((always_inline)) {
         const int c0 = c << lg;
         float *row = ring + (c & 1) * slot_floats + pq * 3 * RS;
 #pragma unroll
@@ -247,7 +253,7 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
                 if (want_db) row[2 * RS + t] = in ? d : 0.0f;
                 // SDRG_WIDE_DBPOOL: the reference windows' dB values also go to the frame's pool scratch, where the
                 // pooled-gap pass reads the bottom window's instead of evaluating its logs again
-                if (SDRG_WIDE_DBPOOL && want_db && in && pq < fq) dbp[pq * wst + e] = d;
+                if (SDRG_WIDE_DBPOOL == 1 && want_db && in && pq < fq) dbp[pq * wst + e] = d;
                 // a thread sees its focus bins in increasing order: strict > keeps its first maximum
                 if (in && pq == fq && d > pk) {
                     pk = d;
@@ -266,7 +272,15 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
         const unsigned long long t_in = SDRG_STATS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
         if (role >= 2) {
             if (prod && c < nch) {
-                if constexpr (SDRG_WIDE_PF == 2) {  // chunk c + 2 into the registers chunk c came from
+                if constexpr (SDRG_WIDE_PF == 3) {  // chunk c + 1's loads issue before chunk c's stores
+                    if ((c & 1) == 0) {
+                        if (c + 1 < nch) fetch_into(va2, vb2, c + 1);
+                        store(c);
+                    } else {
+                        if (c + 1 < nch) fetch(c + 1);
+                        store_from(va2, vb2, c);
+                    }
+                } else if constexpr (SDRG_WIDE_PF == 2) {  // chunk c + 2 into the registers chunk c came from
                     if ((c & 1) == 0) {
                         store(c);
                         if (c + 2 < nch) fetch(c + 2);
@@ -287,7 +301,12 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
                 const int cj = (SDRG_WIDE_FULLEXEC && !chain) ? 0 : j, cg = (SDRG_WIDE_FULLEXEC && !chain) ? 0 : grp;
                 const float *slot = ring + ((c - 1) & 1) * slot_floats;
                 const float *src = slot + (cj * 3 + cg) * RS;  // x, rs terms, dB rows
-                float *dst = cg == 1 ? rsring + (((c - 1) & 1) * nwin + cj) * RS : const_cast<float *>(src);
+                // running values: the rs lanes' go to the rs ring (the record wave reads them); the window and dB
+                // sums' are never read and go back over their own row -- with SDRG_WIDE_DBPOOL 2 the dB lanes' over
+                // the window's bins row instead (beside its sum lane's, same addresses, bins already consumed), so the
+                // dB row stays intact for the record wave's copy to the pool scratch
+                float *dst = cg == 1 ? rsring + (((c - 1) & 1) * nwin + cj) * RS
+                                     : const_cast<float *>(src) - ((SDRG_WIDE_DBPOOL == 2 && cg == 2) ? 2 * RS : 0);
                 // 16 bins per half-step, the next half's four float4 read before this half's adds (two register
                 // sets, no copies), so the LDS latency hides under 16 dependent adds
                 float4 A[4], B[4];
@@ -356,7 +375,31 @@ __device__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, co
                     }
                 }
             }
-        } else if (c >= 2 && rec_lane) {
+        } else {
+            // SDRG_WIDE_DBPOOL 2: the record wave copies chunk c - 1's dB rows of the reference windows (the slot the
+            // chain reads this iteration) to the frame's pool scratch; it issues no loads, so its stores never hold
+            // up a vmcnt wait
+            if (SDRG_WIDE_DBPOOL == 2 && want_db && role == 1 && c >= 1 && c <= nch) {
+                const int c0 = (c - 1) << lg, q4 = SC >> 2;
+                const float *slot = ring + ((c - 1) & 1) * slot_floats;
+                for (int i = lane; i < fq * q4; i += WAVE) {
+                    const int q = i / q4, t = (i - q * q4) << 2, e = c0 + t, len = whi[q] - wlo[q] + 1;
+                    const float4 v = *reinterpret_cast<const float4 *>(slot + (q * 3 + 2) * RS + t);
+                    float *o = dbp + q * wst + e;
+                    if (e + 3 < len) {
+                        o[0] = v.x;
+                        o[1] = v.y;
+                        o[2] = v.z;
+                        o[3] = v.w;
+                    } else {
+                        if (e < len) o[0] = v.x;
+                        if (e + 1 < len) o[1] = v.y;
+                        if (e + 2 < len) o[2] = v.z;
+                    }
+                }
+            }
+        }
+        if (role == 1 && c >= 2 && rec_lane) {
             // chunk c - 2's running sums: lane k of window rq's group visits bins k, k + G, ... in increasing order
             const int c0 = (c - 2) << lg;
             const float *rsrow = rsring + ((c & 1) * nwin + rq) * RS;  // (c - 2) & 1
@@ -579,7 +622,7 @@ __device__ __forceinline__ void finish_record(sdrg_frame_record &rec, const Stat
 // bucket holding the k-th element.  Same element as the reference's std::sort + gaps[k].
 // visit(f) calls f(bits) once for every value this thread holds (an LDS/HBM array or registers).
 template <int WG, class Visit>
-__device__ float kth_smallest(Visit visit, int k, int *hist, uint32_t *xch) {
+__device__ __forceinline__ float kth_smallest(Visit visit, int k, int *hist, uint32_t *xch) {
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
     uint32_t band = 0xffffffffu, bor = 0u;
     visit([&](uint32_t b) {
@@ -657,7 +700,7 @@ __device__ float kth_smallest(Visit visit, int k, int *hist, uint32_t *xch) {
 }
 
 template <int WG>
-__device__ float kth_smallest_of(const float *vals, int cnt, int k, int *hist, uint32_t *xch) {
+__device__ __forceinline__ float kth_smallest_of(const float *vals, int cnt, int k, int *hist, uint32_t *xch) {
     return kth_smallest<WG>(
         [&](auto f) {
             for (int q = threadIdx.x; q < cnt; q += WG) f(__float_as_uint(vals[q]));
