@@ -163,6 +163,9 @@ struct WideScan {
 #ifndef SDRG_WIDE_DBPOOL
 #define SDRG_WIDE_DBPOOL 2
 #endif
+#ifndef SDRG_WIDE_FSPLIT
+#define SDRG_WIDE_FSPLIT 0
+#endif
 __device__ __forceinline__ unsigned hw_id() {
     unsigned v;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
@@ -181,6 +184,63 @@ __device__ __forceinline__ int wide_role(const unsigned *sh_hw) {
     if (m != 15) return wv;
     const int tg = (sh_hw[0] >> 16) & 3;
     return (int)(((sh_hw[wv] >> 4) & 3) - tg) & 3;
+}
+
+// The focus peak of fft_process.cpp:142-154 (first strict maximum of the dB values, seeded at -130) from the largest
+// focus power pmax = out.peak_db (on entry), by monotonicity: dB(p) = 10 log10f(p + 1e-20) never decreases with p
+// (glibc's log10f is monotone: checked over every float, tests/test_libm_exact.py), so the bins whose dB equals the
+// maximum d* = dB(pmax) are exactly those with p >= p_lo, the smallest float whose dB is d*; the peak is the first of
+// them.  p_lo: the WG threads test pmax's 256 float neighbours below it, then (only when all of them share d*, e.g.
+// powers where the 1e-20 dominates) one thread bisects the float bit patterns below.  Every thread calls this.
+template <int WG>
+__device__ __forceinline__ void focus_peak_monotone(const float *__restrict__ P, int flo, int flen, WideScan &out) {
+    __shared__ int s_t, s_plo, s_first;
+    const int tid = threadIdx.x;
+    const float pm = out.peak_db;
+    const float ds = db_of(pm);
+    if (tid == 0) {
+        s_t = WG;
+        s_first = 0x7fffffff;
+    }
+    __syncthreads();
+    const int bm = __float_as_int(pm);
+    const int b = bm - tid;
+    if (ds > -130.0f && b >= 0 && db_of(__int_as_float(b)) != ds) atomicMin(&s_t, tid);
+    __syncthreads();
+    if (tid == 0 && ds > -130.0f) {
+        const int T = s_t;
+        int plo = bm - (T - 1);
+        if (T == WG) {  // every tested neighbour shares d*: bisect [0, bm - WG + 1]
+            int lo = 0, hi = bm - (WG - 1);
+            if (hi <= 0) {
+                lo = 0;
+            } else {
+                while (lo < hi) {
+                    const int mid = lo + ((hi - lo) >> 1);
+                    if (db_of(__int_as_float(mid)) == ds) hi = mid;
+                    else lo = mid + 1;
+                }
+            }
+            plo = lo;
+        }
+        s_plo = plo < 0 ? 0 : plo;
+    }
+    __syncthreads();
+    if (ds > -130.0f) {
+        const float plo = __int_as_float(s_plo);
+        for (int i = tid; i < flen; i += WG)
+            if (P[flo + i] >= plo) {
+                atomicMin(&s_first, i);
+                break;
+            }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const bool hit = ds > -130.0f && s_first != 0x7fffffff;
+        out.peak_db = hit ? ds : -130.0f;
+        out.peak_idx = hit ? flo + s_first : flo;
+    }
+    __syncthreads();
 }
 
 template <bool want_db>
@@ -219,9 +279,16 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
     // ends chunk c, so their HBM latency overlaps the consumers' work instead of following it.
     constexpr int PTHREADS = WIDE_WG - 128;
     constexpr int PR = 9;  // >= SC / PG for every nwin <= 11 (SC from the ring size above)
-    const int PG = PTHREADS / nwin, pw = role >= 2 ? ((role - 2) << 6) | lane : 0;
-    const int pq = min(pw / PG, fq), pk0 = pw - pq * PG;
-    const bool prod = role >= 2 && pw < PG * nwin;
+    // SDRG_WIDE_FSPLIT (one bottom window, three windows): wave 2 stages the two reference windows (32 lanes each),
+    // wave 3 the focus window alone, and wave 3 evaluates no logs -- the focus peak is found after the scan from the
+    // largest focus power (log10f is monotone, focus_peak_monotone) -- so its log instructions are not issued at all
+    const bool fsplit = SDRG_WIDE_FSPLIT && want_db && nwin == 3;
+    const int pw = role >= 2 ? ((role - 2) << 6) | lane : 0;
+    const int PG = fsplit ? (role == 3 ? 64 : 32) : PTHREADS / nwin;
+    const int pq = fsplit ? (role == 3 ? fq : lane >> 5) : min(pw / PG, fq);
+    const int pk0 = fsplit ? (role == 3 ? lane : lane & 31) : pw - pq * PG;
+    const bool prod = role >= 2 && (fsplit || pw < PG * nwin);
+    float pmx = -INFINITY;  // fsplit: the largest focus power this thread staged
     const int plo = wlo[pq], plen = whi[pq] - plo + 1;
     const float *Pq = P + plo;
     float va[PR], vb[PR];
@@ -244,7 +311,12 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
 #pragma unroll
         for (int k = 0; k < PR; k++) {
             const int t = pk0 + PG * k, e = c0 + t;
-            if (t < SC) {
+            if (t < SC && fsplit && role == 3) {  // the focus window: bins and running-sum terms, no dB
+                const float v = va[k];
+                row[t] = v;
+                row[RS + t] = (e >= w) ? v - vb[k] : v;
+                if (e < plen) pmx = fmaxf(pmx, v);
+            } else if (t < SC) {
                 const bool in = e < plen;
                 const float v = va[k];
                 row[t] = v;
@@ -427,7 +499,12 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
     if (SDRG_WIDE_PRIO && role == 0) __builtin_amdgcn_s_setprio(0);
     if (SDRG_STATS_STAMPS && lane == 0 && role <= 2 && blockIdx.x < 8192)
         g_stats_stamps[blockIdx.x * STAMP_PHASES + 6 + role] = busy;
-    if (role >= 2) {  // first maximum over the producer threads (lower bin on ties)
+    if (fsplit) {
+        if (role == 3) {  // the largest focus power
+            for (int off = WAVE / 2; off > 0; off >>= 1) pmx = fmaxf(pmx, __shfl_xor(pmx, off));
+            if (lane == 0) out.peak_db = pmx;  // (the power here; focus_peak_monotone turns it into the peak)
+        }
+    } else if (role >= 2) {  // first maximum over the producer threads (lower bin on ties)
         for (int off = WAVE / 2; off > 0; off >>= 1) {
             const float ob = __shfl_xor(pk, off);
             const int oi = __shfl_xor(pki, off);
@@ -462,7 +539,9 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
     if (chain && grp == 0) out.sum[j] = acc;
     if (chain && grp == 2) out.dsum[j] = acc;
     __syncthreads();
-    if (role == 2 && lane == 0) {
+    if (fsplit) {
+        focus_peak_monotone<WIDE_WG>(P, wlo[fq], whi[fq] - wlo[fq] + 1, out);
+    } else if (role == 2 && lane == 0) {
         const bool other = pk > out.peak_db || (pk == out.peak_db && pki < out.peak_idx);
         if (other) {
             out.peak_db = pk;

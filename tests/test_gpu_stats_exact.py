@@ -92,16 +92,18 @@ def test_ulp_ties_bit_exact(S, O, n, focus):
     eng.close()
 
 
-def test_denormal_and_zero_spectra_bit_exact(S, O):
-    """Powers in the denormal range and exact zeros (the 1e-20 floor dominates) through both log branches."""
-    n, B = 16384, 8
+@pytest.mark.parametrize("n,focus", [(16384, 5), (65536, 200)])
+def test_denormal_and_zero_spectra_bit_exact(S, O, n, focus):
+    """Powers in the denormal range and exact zeros (the 1e-20 floor dominates) through both log branches; at 65536 /
+    200 kHz the wide kernel's focus peak from the largest power meets dB plateaus thousands of floats wide."""
+    B = 8
     rng = np.random.default_rng(5)
     spec = np.zeros((B, n), np.float32)
     for b in range(1, B):
         spec[b] = rng.integers(1, 1 << (3 * b), n).astype(np.uint32).view(np.float32)  # denormals of growing size
     spec[B - 1, ::7] = 0.0
-    eng = S.Engine(S.SDRConfig(centerFrequency=CF, samplesPerReading=n, sampleRate=FS, freqFocusRangeKhz=5), B)
-    fst = [O.FftState(CF, FS, n, 5) for _ in range(B)]
+    eng = S.Engine(S.SDRConfig(centerFrequency=CF, samplesPerReading=n, sampleRate=FS, freqFocusRangeKhz=focus), B)
+    fst = [O.FftState(CF, FS, n, focus) for _ in range(B)]
     rec = eng.signal_strength(spec, 1000)
     want = np.stack([fst[b].signal_strength(spec[b], 1000) for b in range(B)])
     assert_records_equal(rec, want, msg="denormal")
