@@ -252,6 +252,15 @@ int32_t validate_config(const sdrg_config *cfg) {
     return SDRG_OK;
 }
 
+// hipMemset is enqueued on the null stream, which the engine's non-blocking streams are not ordered with: without
+// the wait, a kernel or copy enqueued next on s_main could run before (or under) the fill -- e.g. a fresh staging
+// buffer zeroed after the caller's spectra were copied into it.  Fills happen at allocation and reset only.
+hipError_t memset_sync(void *p, int v, size_t bytes) {
+    hipError_t e = hipMemset(p, v, bytes);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    return e;
+}
+
 template <typename T>
 int32_t ensure_device(T **p, size_t *have, size_t need, bool zero = false) {
     if (*have >= need && *p) return SDRG_OK;
@@ -260,7 +269,7 @@ int32_t ensure_device(T **p, size_t *have, size_t need, bool zero = false) {
     *have = 0;
     if (need == 0) return SDRG_OK;
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(p), need * sizeof(T)));
-    if (zero) HIP_TRY(hipMemset(*p, 0, need * sizeof(T)));
+    if (zero) HIP_TRY(memset_sync(*p, 0, need * sizeof(T)));
     *have = need;
     return SDRG_OK;
 }
@@ -425,8 +434,8 @@ int32_t prepare_ssb(sdrg_engine *e, SsbControl &c, uint32_t &nco_phase, SsbParam
 int32_t alloc_state(sdrg_engine *e) {
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_stats), sizeof(StatsState) * (size_t)e->n_streams));
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_ssb), sizeof(SsbStreamState) * (size_t)e->n_streams));
-    HIP_TRY(hipMemset(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
-    HIP_TRY(hipMemset(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
+    HIP_TRY(memset_sync(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
+    HIP_TRY(memset_sync(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
     return SDRG_OK;
 }
 
@@ -984,8 +993,8 @@ int32_t sdrg_engine_reset_state(sdrg_engine *e) {
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));
     if (e->s_stats) HIP_TRY(hipStreamSynchronize(e->s_stats));
-    HIP_TRY(hipMemset(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
-    HIP_TRY(hipMemset(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
+    HIP_TRY(memset_sync(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
+    HIP_TRY(memset_sync(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
     e->ssb = SsbControl{};
     e->nco_phase = 0;
     e->cf_changed_pending = false;

@@ -182,7 +182,9 @@ int32_t pulse_bank_init(sdrg_pulse_bank *b, int kind, const sdrg_pulse_config *c
     if (kind == SDRG_PULSE_SPECTRAL && (rc = dev_alloc(&b->d_fh, (size_t)n_streams * 2 * PULSE_FH_SLOTS))) return rc;
     if (kind == SDRG_PULSE_AUDIO && (rc = dev_alloc(&b->d_new_count, (size_t)n_streams))) return rc;
     if ((rc = alloc_rings(b, cap_for(*cfg)))) return rc;
+    // (the null stream's fill, waited for: the bank's kernels run on non-blocking streams)
     PB_TRY(hipMemset(b->d_out, 0, sizeof(sdrg_pulse_output) * (size_t)n_streams));
+    PB_TRY(hipStreamSynchronize(nullptr));
     b->reset_pending = true;
     return SDRG_OK;
 }
