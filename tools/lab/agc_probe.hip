@@ -11,13 +11,13 @@
 
 #pragma clang fp contract(off)
 
-enum { HW_HI, HW_LO, S_DN_ONLY, S_UP_ONLY, D_NO_NEWTON_1, D_NEWTON_1, D_NO_NEWTON_2, NCOUNT };
+enum { HW_HI, HW_LO, S_DN_ONLY, S_UP_ONLY, D_NO_NEWTON_1, D_NEWTON_1, D_NO_NEWTON_2, S_F64, S_RSQ, NCOUNT };
 
 __device__ __forceinline__ float dn1(float s) { return __int_as_float(__float_as_int(s) - 1); }
 __device__ __forceinline__ float up1(float s) { return __int_as_float(__float_as_int(s) + 1); }
 
 __global__ void sweep(unsigned lo, unsigned hi, const float *targets, int nt, unsigned long long *cnt) {
-    unsigned long long c[NCOUNT] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long c[NCOUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned stride = gridDim.x * blockDim.x;
     for (unsigned long long b = lo + (blockIdx.x * blockDim.x + threadIdx.x); b <= hi; b += stride) {
         const float m = __uint_as_float((unsigned)b);
@@ -31,6 +31,11 @@ __global__ void sweep(unsigned lo, unsigned hi, const float *targets, int nt, un
         const float su = (fmaf(-u, s, m) > 0.0f) ? u : s;
         c[S_DN_ONLY] += sd != ok;
         c[S_UP_ONLY] += su != ok;
+        // the hardware double sqrt of the float, rounded once to float
+        c[S_F64] += (float)__builtin_amdgcn_sqrt((double)m) != ok;
+        // m * rsq(m) with one residual step: s1 = s0 + r/2 * e, e = m - s0*s0
+        const float r0 = __builtin_amdgcn_rsqf(m), s0 = m * r0;
+        c[S_RSQ] += fmaf(fmaf(-s0, s0, m), 0.5f * r0, s0) != ok;
         const float den = ok + 1e-6f;
         for (int t = 0; t < nt; t++) {
             const float n = targets[t], q_ok = n / den;
@@ -66,8 +71,9 @@ int main() {
     unsigned long long h[NCOUNT];
     if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return 2;
     printf("operands %u: hw sqrt above %llu below %llu | down-only fix wrong %llu, up-only fix wrong %llu | "
-           "div (4 targets): rcp+1 corr wrong %llu, newton+1 corr wrong %llu, rcp+2 corr wrong %llu\n",
+           "div (4 targets): rcp+1 corr wrong %llu, newton+1 corr wrong %llu, rcp+2 corr wrong %llu | "
+           "sqrt via f64 wrong %llu, via rsq + 1 step wrong %llu\n",
            0x7f7fffffu - lo + 1, h[HW_HI], h[HW_LO], h[S_DN_ONLY], h[S_UP_ONLY], h[D_NO_NEWTON_1], h[D_NEWTON_1],
-           h[D_NO_NEWTON_2]);
+           h[D_NO_NEWTON_2], h[S_F64], h[S_RSQ]);
     return 0;
 }
