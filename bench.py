@@ -267,6 +267,10 @@ def main() -> int:
                          "room beside it (measured 8 %% / 2 %% faster at 5 / 200 kHz), 0 for 16384 points, whose persistent "
                          "spectrum kernel loses more to co-resident statistics than they gain (c2 0.18 vs 0.13 ms/step) "
                          "and for N > 1 (the per-step gathers read the records on the main stream)")
+    ap.add_argument("--process-group", action="store_true",
+                    help="N = 1: start a one-rank torch.distributed group anyway (nccl = RCCL, or gloo with "
+                         "--rehearse-gloo) and run the N > 1 code path -- per-step gathers on the engine's stream, "
+                         "barriers, max-over-ranks timing, the full-spectra gather -- on the one GPU (a rehearsal line)")
     ap.add_argument("--launch-dry-run", action="store_true", help=argparse.SUPPRESS)
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
@@ -282,7 +286,13 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    rehearse = args.rehearse_gloo and world > 1
+    dist_on = world > 1 or args.process_group  # a process group (one rank included): the N > 1 code path
+    rehearse = args.rehearse_gloo and dist_on
+    if dist_on and world == 1:  # a one-rank group started without torch.distributed.run
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
     if world > 1 and args.gpus not in (1, world):
         log(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
         return 3
@@ -292,13 +302,13 @@ def main() -> int:
     if rehearse:
         local = 0
         dist.init_process_group("gloo")
-    elif world > 1:
+    elif dist_on:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     ranks_info = None
-    if world > 1:
+    if dist_on:
         if dist.get_world_size() != world:
             log(f"bench: process group has {dist.get_world_size()} ranks, expected {world}")
             return 3
@@ -353,7 +363,7 @@ def main() -> int:
     f_stage = torch.empty((streams, f_n), dtype=torch.float32, device=dev) if focus else None
     f_out = torch.empty((world * streams, f_n), dtype=torch.float32, device=gdev) if focus and rank == 0 else None
     host = (lambda t: t.cpu()) if rehearse else (lambda t: t)
-    if world > 1:
+    if dist_on:
         # the engine enqueues on a torch stream that is current for the collectives too, so the RCCL gather is
         # ordered after each step on the GPU without a host synchronisation, and the next step's kernels
         # follow the gather (a real stream: the legacy default stream has no handle to pass)
@@ -371,7 +381,7 @@ def main() -> int:
         eng.process_device(iq.data_ptr(), fmt, stages if st is None else st, spec.data_ptr(), rec.data_ptr(),
                            pcm.data_ptr(), now[0])
         now[0] += n // 2000  # frame duration in ms at 2 Msps (8 ms for 16384)
-        if world > 1:
+        if dist_on:
             shard.gather_records(host(rec), world, rank, dst=0, out=gathered)  # records (peaks, stats) to rank 0
             if gather_pcm:
                 shard.gather_records(host(pcm.view(torch.uint8)), world, rank, dst=0, out=p_out)
@@ -384,8 +394,8 @@ def main() -> int:
 
     # a pipelined call leaves its SSB stream running past the call, so a per-step PCM gather needs the joined schedule
     # the inputs are generated before the timed region and synchronised, so they are complete at every call
-    pipelined = args.pipelined if not (gather_pcm and world > 1) else 0
-    async_ok = bool(pipelined and world == 1)
+    pipelined = args.pipelined if not (gather_pcm and dist_on) else 0
+    async_ok = bool(pipelined and not dist_on)
     stats_async = async_ok and (args.stats_async == "1" or (args.stats_async == "auto" and c5))
     pipe_mode = pipelined | (sdrg.PIPELINE_STATS_ASYNC if stats_async else 0)
     c5_mode = pipelined | (sdrg.PIPELINE_STATS_ASYNC if async_ok and args.stats_async != "0" else 0)
@@ -407,7 +417,7 @@ def main() -> int:
     eng.synchronize()
     torch.cuda.synchronize()
     eng.reset_timing_stats()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -415,11 +425,11 @@ def main() -> int:
         step()
     eng.synchronize()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     spectra_gather = None
-    if world > 1 and args.spectra_gather_steps > 0:
+    if dist_on and args.spectra_gather_steps > 0:
         # the full spectra of every frame (fftCallback payload) to rank 0, timed on its own: outside the metric
         eng.synchronize()
         s_out = torch.empty((world * streams, n), dtype=torch.float32, device=gdev) if rank == 0 else None
@@ -442,8 +452,9 @@ def main() -> int:
                           "note": "every rank's full [streams, N] float32 spectra gathered to rank 0 (the fftCallback "
                                   "payload, SURVEY 8e), after the timed region; not part of value"}
         del s_out
+    # every rank hashes what it contributed to the last step's gathers; rank 0 checks its gathered blocks (any backend)
     rehearsal_check = rehearsal_verify(torch, dist, world, rank, streams, rec, f_stage, pcm, gather_pcm, gathered, f_out,
-                                       p_out) if rehearse else None
+                                       p_out) if dist_on else None
     ts = eng.timing_stats()
     # the spectrum kernel alone (no SSB sharing the chip), a few launches after the timed region: its
     # isolated HBM rate, reported beside the timed-region one
@@ -526,7 +537,7 @@ def main() -> int:
                             f"+ fftshift + signal-strength stats over a {focus_c5} kHz focus; no SSB"}
 
     labelled = {}
-    if world == 1 and args.config == "c3" and args.stages == "all" and not variant and not args.no_labelled:
+    if not dist_on and args.config == "c3" and args.stages == "all" and not variant and not args.no_labelled:
         eng.set_profiling(False)
         labelled["configs1_fft_stats"] = dict(labelled_rate(sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS, args.steps),
                                               workload="BASELINE configs[1]: same batch, FFT + |X|^2 + fftshift + "
@@ -537,7 +548,7 @@ def main() -> int:
                                                     "+ 127-tap FIR decim 41, every other stage as the headline")
         labelled["configs4_c5_5khz"] = c5_line(5, args.steps)
         labelled["configs4_c5_200khz"] = c5_line(200, args.steps)
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -586,7 +597,7 @@ def main() -> int:
                    "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (
                        (", RCCL gather of records" + (" + PCM" if gather_pcm else "")
                         + (f" + {f_n}-bin focus spectra" if focus else ""))
-                       if world > 1 else "")},
+                       if dist_on else "")},
         "kernel_ms": {k: round(v, 4) for k, v in ts.items() if k != "count"},
         "roofline": {"kernel": f"{kname} (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -644,7 +655,11 @@ def main() -> int:
                      f"per sample at one instruction per 4 cycles, tools/lab/lat.hip) / {MAX_CLOCK_GHZ} GHz max clock",
             "ssb_ms_alone": round(ssb_iso_ms, 4), "frac_alone": round(floor_ms / ssb_iso_ms, 4),
             "ssb_ms_coresident": round(ts["ssb_ms"], 4),
-            "frac_coresident": round(floor_ms / ts["ssb_ms"], 4) if ts["ssb_ms"] > 0 else None}
+            "frac_coresident": round(floor_ms / ts["ssb_ms"], 4) if ts["ssb_ms"] > 0 else None,
+            "coresident_basis": ("every timed step: the SSB stream's time per step in the pipelined timed region, from "
+                                 "one step's SSB end marker to the next (the SSB pipeline kernel + the audio pulse "
+                                 "detector + their launch gaps; the first step from its own start marker)"
+                                 if pipelined else "every timed step: the SSB stream's start to end marker")}
         # the same kernel against HBM: the step's longest kernel by GPU time, and latency-bound (the floor above)
         ssb_bytes = streams * n * in_bps + streams * 2 * plen
         ssb_traffic = pmc_traffic("ssb_pipe_kernel", streams)
@@ -657,18 +672,36 @@ def main() -> int:
                 "traffic_source": ssb_traffic[1] if ssb_traffic else None,
                 "note": "the longest kernel by GPU time, measured co-resident in the timed region; it is bound by the "
                         "sample-serial recurrences (ssb_latency_floor), not by HBM: IQ in (I used) + PCM out"}
+    if args.stages == "all" and ts["ssb_ms"] > 0:
+        # the kernel with the most GPU time per step, against HBM: pipelined, the SSB stream (the pipeline kernel and
+        # the audio detector) and the main stream (spectrum, statistics, spectral detector) each fill the step
+        cand = {"ssb_pipe_kernel": (ts["ssb_ms"], streams * n * in_bps + streams * 2 * plen),
+                "spectrum16k_kernel" if not c5 else "four_step_a + four_step_b": (spec_ms, alg_bytes),
+                "stats_kernel": (ts["stats_ms"], None)}
+        dom = max((k for k in cand if cand[k][1] is not None), key=lambda k: cand[k][0])
+        d_ms, d_bytes = cand[dom]
+        d_gbs = d_bytes / (d_ms * 1e-3) / 1e9
+        d_traffic = pmc_traffic(dom, streams)
+        out["roofline_dominant"] = {
+            "kernel": dom, "ms_per_step": round(d_ms, 4), "bound": "hbm", "achieved": round(d_gbs, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(d_gbs / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": d_bytes,
+            "traffic": d_traffic[0] if d_traffic else None, "traffic_source": d_traffic[1] if d_traffic else None,
+            "kernel_ms_per_step": {k: round(v[0], 4) for k, v in cand.items()},
+            "note": "the kernel with the most GPU time per step (its stream time in the timed region); ssb_pipe_kernel "
+                    "is bound by the sample-serial recurrences (ssb_latency_floor), not by HBM"}
     if labelled:
         out["labelled"] = labelled
     if rehearse:
         out["rehearsal"] = "gloo, every rank on cuda:0: a functional check of the N > 1 path, not a measurement"
-        out["rehearsal_check"] = rehearsal_check
+    if dist_on:
+        out["rehearsal_check" if rehearse else "gather_check"] = rehearsal_check
     if variant:
         out["ssb_variant"] = {"nco_hz": NCO_HZ, "fir_taps": 127, "note": "not the reference's chain; no CPU baseline"}
     if args.config != "c3":
         out["labelled_config"] = args.config
     elif args.stages != "all":
         out["ablation_stages"] = args.stages
-    if (rank == 0 and world == 1 and not args.no_cpu_baseline and args.stages == "all" and not variant
+    if (rank == 0 and not dist_on and not args.no_cpu_baseline and args.stages == "all" and not variant
             and args.config == "c3"):
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads or host_cores()[0])
@@ -677,7 +710,7 @@ def main() -> int:
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     return 0
 

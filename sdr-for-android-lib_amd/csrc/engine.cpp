@@ -123,7 +123,8 @@ struct PinnedVec {
 struct EvSet {
     hipEvent_t t0 = nullptr, spec = nullptr, stats = nullptr, ssb0 = nullptr, ssb1 = nullptr, end = nullptr;
     bool has_spec = false, has_stats = false, has_ssb = false, pending = false;
-    bool ssb_timed = false;  // ssb0 recorded: this call's SSB duration is measured
+    bool ssb_timed = false;  // ssb0 recorded: this call's SSB duration is measured from its own start marker
+    int64_t seq = -1;        // the call's number among profiled calls (pipelined SSB: interval to call seq - 1)
     bool stats_marked = false;  // `stats` recorded after the statistics (joined calls, whose `end` follows the join)
 };
 
@@ -161,7 +162,8 @@ struct sdrg_engine {
     sdrg_timings last_timings{};
     double sum_spec = 0, sum_stats = 0, sum_ssb = 0, sum_total = 0;
     int n_acc = 0, n_ssb = 0;
-    int calls_profiled = 0;
+    int64_t calls_profiled = 0;
+    int64_t seq_reset = 0;  // seq of the first profiled call after the last reset of the timing statistics
 
     // device state / buffers
     StatsState *d_stats = nullptr;
@@ -185,6 +187,8 @@ struct sdrg_engine {
     size_t iq_stage_bytes = 0;
     float *d_spec_stage = nullptr;
     size_t spec_stage_elems = 0;
+    float *d_ss_stage = nullptr;  // signal_strength_host's copy of the caller's spectra
+    size_t ss_stage_elems = 0;
     sdrg_frame_record *d_rec_stage = nullptr;
     int16_t *d_pcm_stage = nullptr;
     size_t pcm_stage_elems = 0;
@@ -307,11 +311,24 @@ int32_t fold_slot(sdrg_engine *e, int slot) {
         HIP_TRY(hipEventElapsedTime(&ms, ev.has_spec ? ev.spec : ev.t0, ev.stats_marked ? ev.stats : ev.end));
         t.stats_ms = ms;
     }
+    bool ssb_measured = false;
     if (ev.has_ssb && ev.ssb_timed) {
         // pipelined calls never join the SSB stream into ev.end's stream: wait for its own end event
         HIP_TRY(hipEventSynchronize(ev.ssb1));
         HIP_TRY(hipEventElapsedTime(&ms, ev.ssb0, ev.ssb1));
         t.ssb_ms = ms;
+        ssb_measured = true;
+    } else if (ev.has_ssb) {
+        // pipelined: no start marker (it would sit on the SSB stream, the step's critical path); the call's SSB
+        // stream time is the interval from the previous call's SSB end marker to its own.  The previous slot still
+        // holds that marker while its seq is this call's - 1 (enqueue folds a slot's successor before reusing it).
+        const EvSet &pv = e->ring[(slot + sdrg_engine::RING - 1) % sdrg_engine::RING];
+        if (pv.seq == ev.seq - 1 && pv.has_ssb && ev.seq > e->seq_reset) {
+            HIP_TRY(hipEventSynchronize(ev.ssb1));
+            HIP_TRY(hipEventElapsedTime(&ms, pv.ssb1, ev.ssb1));
+            t.ssb_ms = ms;
+            ssb_measured = true;
+        }
     }
     HIP_TRY(hipEventElapsedTime(&ms, ev.t0, ev.end));
     t.total_ms = ms;
@@ -319,7 +336,7 @@ int32_t fold_slot(sdrg_engine *e, int slot) {
     if (slot == e->ring_last) e->last_timings = t;
     e->sum_spec += t.spectrum_ms;
     e->sum_stats += t.stats_ms;
-    if (ev.has_ssb && ev.ssb_timed) {
+    if (ssb_measured) {
         e->sum_ssb += t.ssb_ms;
         e->n_ssb++;
     }
@@ -537,13 +554,21 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             int32_t rc = fold_slot(e, slot);
             if (rc) return rc;
         }
+        // the next slot's call measures its pipelined SSB interval from this slot's end marker, about to be reused
+        const int nx = (slot + 1) % sdrg_engine::RING;
+        if (e->ring[nx].pending) {
+            int32_t rc = fold_slot(e, nx);
+            if (rc) return rc;
+        }
         ev = &e->ring[slot];
         ev->has_spec = do_spec;
         ev->has_stats = do_stats;
         ev->has_ssb = do_ssb;
-        // the SSB start marker sits on the SSB stream between the fork and the pipeline; pipelined, that
-        // stream is the step's critical path, so only every 8th call carries one (its mean is the sample's)
-        ev->ssb_timed = do_ssb && (!(e->pipelined && !join) || e->calls_profiled % 8 == 0);
+        // the SSB start marker sits on the SSB stream between the fork and the pipeline; pipelined, that stream is
+        // the step's critical path, so only the first call of a timing window carries one: every later call's SSB
+        // time is measured from the previous call's SSB end marker to its own (fold_slot)
+        ev->ssb_timed = do_ssb && (!(e->pipelined && !join) || e->calls_profiled == e->seq_reset);
+        ev->seq = e->calls_profiled;
         // a joined call's end marker follows the wait for the SSB stream, and asynchronous statistics end on a
         // stream of their own: the statistics get a marker of their own
         ev->stats_marked = do_stats && (!(e->pipelined && !join) || e->stats_async);
@@ -834,7 +859,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (e->s_stats) (void)hipStreamSynchronize(e->s_stats);
     e->spec_bank.last_stream = e->audio_bank.last_stream = nullptr;  // drained above
     void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_nco_tab, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch, e->d_pool,
-                    e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_rec_stage, e->d_pcm_stage};
+                    e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_ss_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (e->s_spec) (void)hipStreamSynchronize(e->s_spec);
@@ -1019,11 +1044,12 @@ int32_t sdrg_engine_set_pipelining(sdrg_engine *e, int32_t on) {
     }
     if (e->stats_async && !async && e->last_stats_end)  // the asynchronous statistics in flight, likewise
         HIP_TRY(hipStreamWaitEvent(e->s_main, e->last_stats_end, 0));
-    if (async && !e->s_stats) {
+    if (async) {  // created lazily, each handle on its own: a failed earlier attempt leaves no null behind in use
         const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
-        HIP_TRY(hipStreamCreateWithFlags(&e->s_stats, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&e->ev_spec_done, fl));
-        for (hipEvent_t &ev : e->ev_stats_end) HIP_TRY(hipEventCreateWithFlags(&ev, fl));
+        if (!e->s_stats) HIP_TRY(hipStreamCreateWithFlags(&e->s_stats, hipStreamNonBlocking));
+        if (!e->ev_spec_done) HIP_TRY(hipEventCreateWithFlags(&e->ev_spec_done, fl));
+        for (hipEvent_t &ev : e->ev_stats_end)
+            if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, fl));
     }
     e->pipelined = mode != SDRG_PIPELINE_OFF;
     e->inputs_ready = mode == SDRG_PIPELINE_INPUTS_READY;
@@ -1103,6 +1129,9 @@ static int32_t signal_strength(sdrg_engine *e, const float *spectra, sdrg_frame_
     geo.cf_changed = e->cf_changed_pending ? 1 : 0;
     int32_t rc = ensure_device(&e->d_pool, &e->pool_elems, stats_global_pool_floats(geo, B));
     if (rc) return rc;
+    // asynchronous statistics of an earlier pipelined call (SDRG_PIPELINE_STATS_ASYNC) may still run on s_stats and
+    // read / write the same stream state (d_stats) and pool scratch: this launch follows them
+    if (e->stats_async && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(e->s_main, e->last_stats_end, 0));
     HIP_TRY(launch_stats(spectra, B, geo, now_ms, e->d_stats, records, e->d_pool, e->s_main));
     e->cf_changed_pending = false;
     return SDRG_OK;
@@ -1124,12 +1153,14 @@ int32_t sdrg_engine_signal_strength_host(sdrg_engine *e, const float *spectra, s
     DeviceScope dscope(e->device);
     HIP_TRY(dscope.error());
     const int n = e->cfg.samples_per_reading, B = e->n_streams;
-    int32_t rc = ensure_device(&e->d_spec_stage, &e->spec_stage_elems, (size_t)B * n, true);
+    // a staging buffer of its own: process_host's d_spec_stage carries each stream's never-written bin N-1 for odd N
+    // (fft_process.cpp:92-97), which the caller's spectra must not replace
+    int32_t rc = ensure_device(&e->d_ss_stage, &e->ss_stage_elems, (size_t)B * n);
     if (rc) return rc;
     if (!e->d_rec_stage)
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&e->d_rec_stage), sizeof(sdrg_frame_record) * (size_t)B));
-    HIP_TRY(hipMemcpyAsync(e->d_spec_stage, spectra, sizeof(float) * (size_t)B * n, hipMemcpyHostToDevice, e->s_main));
-    rc = signal_strength(e, e->d_spec_stage, e->d_rec_stage, now_ms);
+    HIP_TRY(hipMemcpyAsync(e->d_ss_stage, spectra, sizeof(float) * (size_t)B * n, hipMemcpyHostToDevice, e->s_main));
+    rc = signal_strength(e, e->d_ss_stage, e->d_rec_stage, now_ms);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(records, e->d_rec_stage, sizeof(sdrg_frame_record) * (size_t)B, hipMemcpyDeviceToHost,
                            e->s_main));
@@ -1287,6 +1318,8 @@ int32_t sdrg_engine_reset_timing_stats(sdrg_engine *e) {
     if (rc) return rc;
     e->sum_spec = e->sum_stats = e->sum_ssb = e->sum_total = 0;
     e->n_acc = e->n_ssb = 0;
+    // a pipelined call's SSB interval starts at the previous call's end marker: the window's first call has none
+    e->seq_reset = e->calls_profiled;
     return SDRG_OK;
 }
 

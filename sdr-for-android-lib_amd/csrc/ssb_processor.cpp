@@ -53,8 +53,11 @@ struct sdrg_ssb_processor {
     std::condition_variable cv, idle_cv;
     std::deque<Item> q;
     bool busy = false;  // the worker holds a popped frame
-    std::thread worker;
-    std::mutex join_mu;  // stop() may race with another stop (stopReading vs close from different threads)
+    std::thread worker;  // guarded by join_mu
+    std::mutex join_mu;  // start / stop / destroy may run on different threads (stopReading vs close)
+    // the running worker's id, set by the worker itself before its loop starts: the self-thread checks (a callback
+    // that stops, restarts or destroys its own processor) read it without join_mu, which a joiner may hold
+    std::atomic<std::thread::id> worker_id{};
     std::atomic<bool> running{false};
     sdrg_ssb_callbacks cbs{};
     std::atomic<int32_t> sound_mode{1};
@@ -163,14 +166,19 @@ int32_t sdrg_ssb_processor_stop(sdrg_ssb_processor *p) {
     }
     p->cv.notify_one();
     // a callback on the worker thread that stops its own processor cannot join itself: the loop ends after it
-    if (p->worker.joinable() && p->worker.get_id() == std::this_thread::get_id()) return SDRG_OK;
+    if (p->worker_id.load() == std::this_thread::get_id()) return SDRG_OK;
     std::lock_guard<std::mutex> jl(p->join_mu);  // one joiner at a time
     if (p->worker.joinable()) p->worker.join();
+    p->worker_id.store(std::thread::id());
     return SDRG_OK;
 }
 
 int32_t sdrg_ssb_processor_destroy(sdrg_ssb_processor *p) {
     if (!p) return SDRG_OK;
+    // from the worker's own callback the worker is still inside run_frame on this object: refuse (stop() from the
+    // callback ends the loop; destroy from another thread afterwards)
+    if (p->worker_id.load() == std::this_thread::get_id())
+        return fail(SDRG_E_INVALID, "destroy from the worker's own callback");
     sdrg_ssb_processor_stop(p);
     if (p->eng) sdrg_engine_destroy(p->eng);
     delete p;
@@ -179,16 +187,17 @@ int32_t sdrg_ssb_processor_destroy(sdrg_ssb_processor *p) {
 
 int32_t sdrg_ssb_processor_start(sdrg_ssb_processor *p, const sdrg_ssb_callbacks *cbs) {
     if (!p) return fail(SDRG_E_INVALID, "null processor");
+    if (p->worker_id.load() == std::this_thread::get_id())
+        return p->running.load() ? SDRG_OK : fail(SDRG_E_INVALID, "start from the worker's own callback");
+    std::lock_guard<std::mutex> jl(p->join_mu);
     if (p->running.load()) return SDRG_OK;  // "SSB processing already running" (:28-31)
-    if (p->worker.joinable()) {  // a loop stopped from its own callback has ended or is ending: reap it
-        if (p->worker.get_id() == std::this_thread::get_id())
-            return fail(SDRG_E_INVALID, "start from the worker's own callback");
-        std::lock_guard<std::mutex> jl(p->join_mu);
-        if (p->worker.joinable()) p->worker.join();
-    }
+    if (p->worker.joinable()) p->worker.join();  // a loop stopped from its own callback has ended or is ending: reap it
     p->cbs = cbs ? *cbs : sdrg_ssb_callbacks{};
     p->running.store(true);
-    p->worker = std::thread([p] { p->loop(); });
+    p->worker = std::thread([p] {
+        p->worker_id.store(std::this_thread::get_id());
+        p->loop();
+    });
     return SDRG_OK;
 }
 

@@ -24,13 +24,15 @@ def gather_records(records, world: int, rank: int, dst: int = 0, group=None, out
     Returns the [world*B, record_bytes] concatenation (global stream order) on `dst`, None elsewhere.  The
     tensor must live where the process group's backend expects it (HIP memory for nccl/RCCL, host for gloo).
     `out` (on dst): a preallocated [world*B, record_bytes] tensor to gather into (no per-step allocation);
-    with RCCL the gather is ordered on the current stream, so no host synchronisation is needed.
+    with RCCL the gather is ordered on the current stream, so no host synchronisation is needed.  With a process
+    group initialised the collective runs at every world size, one rank included (so a one-GPU job drives the same
+    RCCL path as an 8-GPU one); without one, world must be 1 and the tensor itself is returned.
     """
     import torch
     import torch.distributed as dist
 
-    if world == 1:
-        return records
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
+        return records  # no process group: nothing to gather
     if rank == dst:
         if out is None:
             out = torch.empty((world * records.shape[0],) + tuple(records.shape[1:]), dtype=records.dtype,

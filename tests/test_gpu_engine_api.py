@@ -243,3 +243,59 @@ def test_dynamic_lds_limit_survives_large_small_large(S, O):
         assert spec.tobytes() == spec1.tobytes(), n
         np.testing.assert_array_equal(rec["peak_bin"], rec1["peak_bin"])
     eng.close()
+
+
+def _ss_after_calls(S, O, torch, raws, ss_spec, n, fs, focus, mode):
+    """F calls (spectrum + statistics on device buffers), each followed by signal_strength on host spectra, on one
+    engine in pipelining `mode`; returns every record (device calls and signal_strength calls) as bytes."""
+    dev = torch.device("cuda:0")
+    B, F = raws.shape[1], raws.shape[0]
+    eng = engine(S, n, fs, B, focus=focus)
+    if mode:
+        eng.set_pipelining(mode)
+    src = [torch.from_numpy(raws[f]).to(dev) for f in range(F)]
+    spec = [torch.empty((B, n), dtype=torch.float32, device=dev) for _ in range(F)]
+    rec = [torch.zeros((B, S.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev) for _ in range(F)]
+    torch.cuda.synchronize()
+    ss = []
+    for f in range(F):
+        eng.process_device(src[f].data_ptr(), S.CS8, S.STAGE_SPECTRUM | S.STAGE_STATS, spec[f].data_ptr(),
+                           rec[f].data_ptr(), None, 1000 + 33 * f)
+        ss.append(eng.signal_strength(ss_spec[f], now_ms=1010 + 33 * f).tobytes())
+    eng.synchronize()
+    out = [r.cpu().numpy().tobytes() for r in rec], ss
+    eng.close()
+    return out
+
+
+def test_signal_strength_follows_async_statistics(S, O):
+    """signal_strength after a pipelined call with asynchronous statistics (SDRG_PIPELINE_STATS_ASYNC)
+    must wait for them -- both update the same stream state (tracking latch, detection ring).  Records of the device
+    calls and of the signal_strength calls equal the joined schedule's bit for bit (65536 points, 200 kHz focus:
+    the wide statistics kernel, the longest asynchronous launch)."""
+    import torch
+    n, fs, B, F = 65536, 2_000_000, 32, 4
+    raws = frames(O, B, F, n=n, fs=fs)
+    rng = np.random.default_rng(5)
+    ss_spec = rng.exponential(1.0, size=(F, B, n)).astype(np.float32)
+    ss_spec[:, :, n // 2 + 100] *= 1e4  # a peak inside the focus
+    want = _ss_after_calls(S, O, torch, raws, ss_spec, n, fs, 200, 0)
+    got = _ss_after_calls(S, O, torch, raws, ss_spec, n, fs, 200, S.PIPELINE_INPUTS_READY | S.PIPELINE_STATS_ASYNC)
+    for k in range(F):
+        assert got[0][k] == want[0][k], f"device call {k}"
+        assert got[1][k] == want[1][k], f"signal_strength call {k}"
+
+
+def test_signal_strength_host_keeps_odd_n_carried_bin(S, O):
+    """for odd N the spectrum never writes bin N-1 (fft_process.cpp:92-97) and the host path carries the
+    stream's own value there (0 from a fresh vector); a signal_strength call on caller spectra in between must not
+    replace it (it stages the caller's spectra in a buffer of its own)."""
+    n, fs, B = 4099, 2_000_000, 4
+    eng = engine(S, n, fs, B)
+    raw = np.stack([O.synth_frames(2, n, O.CS8, tone_hz=500.0 * (b + 1), fs=fs, seed=60 + b) for b in range(B)])
+    spec0, _, _ = eng.process(raw[:, 0], fmt=S.CS8, stages=S.STAGE_SPECTRUM | S.STAGE_STATS, now_ms=1000)
+    assert np.all(spec0[:, n - 1] == 0)
+    eng.signal_strength(np.full((B, n), 7.0, np.float32), now_ms=1005)
+    spec1, _, _ = eng.process(raw[:, 1], fmt=S.CS8, stages=S.STAGE_SPECTRUM | S.STAGE_STATS, now_ms=1010)
+    assert np.all(spec1[:, n - 1] == 0), spec1[:, n - 1]
+    eng.close()

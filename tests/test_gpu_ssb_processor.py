@@ -79,3 +79,30 @@ def test_queue_keeps_up_with_sound_mode_switch(S, O):
     for a, b in zip(got, want):
         np.testing.assert_array_equal(a, b)
     proc.close()
+
+
+def test_callback_cannot_destroy_its_own_processor(S, O):
+    """A callback on the worker thread may stop its processor (the loop ends after the frame) but not destroy it
+    (the worker is still inside that frame): destroy returns SDRG_E_INVALID there and succeeds afterwards from
+    another thread; start from the stopped worker's callback is refused likewise."""
+    raw = O.synth_frames(2, 8192, O.CF32, tone_hz=900.0, fs=FS, seed=79)
+    lib = S.load()
+    rcs = {}
+    proc = S.SSBProcessor()
+
+    def on_pcm(_p):
+        rcs["destroy"] = lib.sdrg_ssb_processor_destroy(proc._h)
+        rcs["stop"] = lib.sdrg_ssb_processor_stop(proc._h)
+        rcs["start"] = lib.sdrg_ssb_processor_start(proc._h, None)
+
+    proc.startProcessing(on_pcm)
+    proc.enqueueData(raw[0], FS)
+    proc.drain()
+    assert rcs == {"destroy": -1, "stop": 0, "start": -1}, rcs
+    assert proc.counters()["processed"] == 1
+    proc.stopProcessing()  # joins the ended loop
+    proc.startProcessing(lambda p: rcs.setdefault("again", len(p)))  # restartable from another thread
+    proc.enqueueData(raw[1], FS)
+    proc.drain()
+    assert rcs.get("again", 0) > 0
+    proc.close()

@@ -94,3 +94,38 @@ def test_stream_range():
     from sdrg import shard
     assert shard.stream_range(0, 2, 4096) == (0, 4096)
     assert shard.stream_range(1, 2, 4096) == (4096, 8192)
+
+
+def _one_rank_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    sys.path[:0] = [os.path.join(ROOT, "sdr-for-android-lib_amd")]
+    try:
+        import torch
+        import torch.distributed as dist
+        from sdrg import shard
+        rec = torch.arange(5 * 72, dtype=torch.int64).remainder(251).to(torch.uint8).reshape(5, 72)
+        bare = shard.gather_records(rec, 1, 0)  # no process group: the tensor itself
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        out = torch.zeros_like(rec)
+        got = shard.gather_records(rec, 1, 0, out=out)  # a one-rank group: the collective runs
+        spec = torch.rand(5, 64)
+        foc = shard.gather_focus(spec, 10, 7, 1, 0)
+        dist.destroy_process_group()
+        q.put(("ok", bare is rec, got is out and torch.equal(out, rec), torch.equal(foc, spec[:, 10:17])))
+    except Exception as exc:  # reported to the parent
+        q.put(("error", repr(exc), None, None))
+
+
+def test_one_rank_group_runs_the_collective():
+    """with a process group initialised, shard.gather_* run the collective at world size 1 too
+    (the one-GPU box then drives the same RCCL path bench.py uses at N > 1); without one they return the input."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_one_rank_worker, args=(port, q))
+    p.start()
+    res = q.get(timeout=120)
+    p.join(timeout=60)
+    assert res == ("ok", True, True, True), res
