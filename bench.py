@@ -277,6 +277,11 @@ def main() -> int:
     rc = maybe_launch(args, argv)
     if rc is not None:
         return rc
+    # this process is a rank: the ONE JSON line goes to the real stdout, everything else (RCCL's version banner,
+    # which it prints on stdout at communicator creation, library warnings) to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -708,7 +713,7 @@ def main() -> int:
         except Exception as exc:  # the baseline is informative; never fail the bench line on it
             out["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     eng.close()
     if dist_on:
         dist.destroy_process_group()

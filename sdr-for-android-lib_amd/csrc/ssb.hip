@@ -338,6 +338,12 @@ constexpr int PG = 16;          // streams per workgroup
 #ifndef SDRG_SERIAL_FULL_EXEC
 #define SDRG_SERIAL_FULL_EXEC 0x0
 #endif
+// lanes of the three hand-scheduled serial roles (DC, low-pass, AGC): 0 = lanes 0-15 (stream = lane), 1 = lanes
+// {0-3, 16-19, 32-35, 48-51} (EXEC 0x000f000f000f000f, stream = 4 x (lane / 16) + lane % 4): a dependent add chain
+// issues at 25.4 instead of 30.6 cycles per sample with that mask (tools/lab/lpf_exec.hip, profiles/r3b_pg32_stamps.md)
+#ifndef SDRG_SERIAL_LANES
+#define SDRG_SERIAL_LANES 0
+#endif
 constexpr int CH = 64;          // samples per chunk
 constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_read_b128 by stream lanes
 constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
@@ -559,6 +565,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         for (int i = tid; i < 2 * 1024 * 2; i += PIPE_T) nco_lds[i] = p.nco_tab[i];
 
     const int my_s = lane & (PG - 1);  // serial roles: lane = 16 x copy + stream (all 64 lanes run; lanes < PG store)
+    // the hand-scheduled serial roles' lanes (SDRG_SERIAL_LANES): ser_on = the lane holds stream ser_s
+    const bool ser_on = SDRG_SERIAL_LANES ? (lane & 12) == 0 : lane < PG;
+    const int ser_s = SDRG_SERIAL_LANES ? (((lane >> 4) << 2) | (lane & 3)) : my_s;
     const float demod_k = p.upper ? 2.0f : 0.0f;  // demodSSB(y, y) = y + y or y - y (:89-94) as y * k
     const bool serial_live = (wave < 3 || wave == W_EQ) && (lane < PG) && (s0 + lane < n_frames);
     const bool high = (prio_mask >> wave) & 1;  // masks are per role  // default: the recurrences (waves 0-2) own their SIMD's issue slots
@@ -623,10 +632,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             // the frame's last chunk runs whole too: dc restarts every frame and the samples past the frame end
             // (zeros from the loader) only feed outputs nothing reads
             const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
-            if (SDRG_DC_ASM && !(SDRG_SERIAL_FULL_EXEC & 1) && c >= 0 && c < nch && lane < PG) {
+            if (SDRG_DC_ASM && !(SDRG_SERIAL_FULL_EXEC & 1) && c >= 0 && c < nch && ser_on) {
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 const f2v om2 = {one_minus, one_minus}, a02 = {a0, a0};
-                const uint32_t src = lds_addr(&L.re[c & 1][my_s * ROW]), dst = lds_addr(&L.a[c % NA][my_s * ROW]);
+                const uint32_t src = lds_addr(&L.re[c & 1][ser_s * ROW]), dst = lds_addr(&L.a[c % NA][ser_s * ROW]);
                 if (SDRG_DC_ASM == 2)
                     asm volatile(SDRG_DC_CHUNK_IL_ASM
                                  : [dc] "+v"(dc)
@@ -649,24 +658,31 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         });
     } else if (wave == W_LPF) {
         float z1 = 0.0f, z2 = 0.0f;  // rfFilter state, carried across frames
-        if (s0 + my_s < n_frames) {
-            z1 = state[s0 + my_s].lpf_z1;
-            z2 = state[s0 + my_s].lpf_z2;
+        const bool lpf_asm_loop = LA && SDRG_LPF_ASM == 1 && !(SDRG_SERIAL_FULL_EXEC & 2) && S % CH == 0;
+        const int ls = lpf_asm_loop ? ser_s : my_s;  // this lane's stream
+        if (s0 + ls < n_frames) {
+            z1 = state[s0 + ls].lpf_z1;
+            z2 = state[s0 + ls].lpf_z2;
         }
         // y = ((((a0 x + a1 z1) + a2 z2) - b1 z1) - b2 z2): the four products as two packed multiplies (each
         // lane of v_pk_mul_f32 rounds like v_mul_f32), the adds in order; the subtractions are additions of
         // (-b) z (a - b == a + (-b) exactly, and (-b) z == -(b z))
         const f2v c1 = {p.lpf[1], -p.lpf[3]}, c2 = {p.lpf[2], -p.lpf[4]};
         static_assert(BUFF * 4 == SDRG_LPF_LOOP_SLOT_BYTES, "ring slot stride of the generated loop");
-        if (LA && SDRG_LPF_ASM == 1 && !(SDRG_SERIAL_FULL_EXEC & 2) && S % CH == 0) {
+        if (lpf_asm_loop) {
             // the whole loop as one block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py): nch + 8 + LA iterations
             // with one s_barrier each, the same count as every other role's chunk_loop
             f2v z = {z1, z2};
-            const uint32_t abase = lds_addr(&L.a[0][my_s * ROW]), ybase = lds_addr(&L.y[0][my_s * ROW]);
+            const uint32_t abase = lds_addr(&L.a[0][ser_s * ROW]), ybase = lds_addr(&L.y[0][ser_s * ROW]);
             const int nit = nch + 8 + LA;
             unsigned long long sv;
             int t_it, t_cc, t_r, t_yo;
-            if (SDRG_LPF_INTERLEAVE)
+            if (SDRG_LPF_INTERLEAVE && SDRG_SERIAL_LANES)
+                asm volatile(SDRG_LPF_LOOP_IL_SPREAD_ASM
+                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
+                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+            else if (SDRG_LPF_INTERLEAVE)
                 asm volatile(SDRG_LPF_LOOP_IL_ASM
                              : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                              : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
@@ -750,9 +766,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 }
             }
         });
-        if (serial_live) {
-            state[s0 + my_s].lpf_z1 = z1;
-            state[s0 + my_s].lpf_z2 = z2;
+        if ((lpf_asm_loop ? ser_on : lane < PG) && s0 + ls < n_frames) {
+            state[s0 + ls].lpf_z1 = z1;
+            state[s0 + ls].lpf_z2 = z2;
         }
     } else if (wave == W_AGC) {
         float gain = 1.0f;  // adaptiveAGC: reset per call (:102)
@@ -764,10 +780,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         chunk_loop([&](int it) {
             // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
             const int c = it - 4 - LA;
-            if (SDRG_AGC_ASM && !(SDRG_SERIAL_FULL_EXEC & 4) && c >= 0 && c < nch && lane < PG) {
+            if (SDRG_AGC_ASM && !(SDRG_SERIAL_FULL_EXEC & 4) && c >= 0 && c < nch && ser_on) {
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 f2v g = {gain, gain};
-                const uint32_t src = lds_addr(&L.d[c & 1][my_s * ROW]), dst = lds_addr(&L.g[c & 1][my_s * ROW]);
+                const uint32_t src = lds_addr(&L.d[c & 1][ser_s * ROW]), dst = lds_addr(&L.g[c & 1][ser_s * ROW]);
                 if (SDRG_AGC_ASM == 2)
                     asm volatile(SDRG_AGC_CHUNK_IL_ASM
                                  : [g] "+v"(g)
@@ -1060,6 +1076,7 @@ unsigned long long *ssb_stamps_buffer(int n_frames) {
             hipSuccess)
             return nullptr;
         (void)hipMemset(g_stamps, 0, sizeof(unsigned long long) * per_call * STAMP_CALLS);
+        (void)hipStreamSynchronize(nullptr);  // the null-stream fill before any kernel on the engine's streams
         g_stamps_groups = groups;
         g_stamp_call = 0;
     }
@@ -1110,6 +1127,7 @@ void ssb_report_stamps() {
     }
     g_stamp_call = 0;  // the next report covers the calls after this one
     (void)hipMemset(g_stamps, 0, sizeof(unsigned long long) * per_call * STAMP_CALLS);
+    (void)hipStreamSynchronize(nullptr);
 }
 
 // Outputs whose window can overlap one chunk: floor((CH + NT - 2) / D) + 1; the FIR keeps one accumulator

@@ -33,7 +33,7 @@ constexpr int STAGE_MAX = 8192;  // bins staged into LDS for the window scans (3
 #ifndef SDRG_STATS_STAMPS
 #define SDRG_STATS_STAMPS 0
 #endif
-constexpr int STAMP_PHASES = 10;
+constexpr int STAMP_PHASES = 12;
 
 
 __device__ unsigned long long g_stats_stamps[STAMP_PHASES * 8192];
@@ -166,6 +166,17 @@ struct WideScan {
 #ifndef SDRG_WIDE_FSPLIT
 #define SDRG_WIDE_FSPLIT 0
 #endif
+// SDRG_WIDE_LDSBAR: the wide scans' per-chunk barrier orders LDS only (s_waitcnt lgkmcnt(0); s_barrier), so the
+// producers' loads of the next chunk stay in flight across it; __syncthreads() would wait for them (vmcnt(0)) at every
+// chunk.  Nothing global is exchanged between the waves inside the scan (the pool copies are read after it, behind a
+// __syncthreads).
+#ifndef SDRG_WIDE_LDSBAR
+#define SDRG_WIDE_LDSBAR 1
+#endif
+__device__ __forceinline__ void wide_chunk_barrier() {
+    if (SDRG_WIDE_LDSBAR) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else __syncthreads();
+}
 __device__ __forceinline__ unsigned hw_id() {
     unsigned v;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
@@ -494,7 +505,7 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
             }
         }
         if (SDRG_STATS_STAMPS) busy += __builtin_amdgcn_s_memtime() - t_in;
-        __syncthreads();
+        wide_chunk_barrier();
     }
     if (SDRG_WIDE_PRIO && role == 0) __builtin_amdgcn_s_setprio(0);
     if (SDRG_STATS_STAMPS && lane == 0 && role <= 2 && blockIdx.x < 8192)
@@ -703,6 +714,7 @@ __device__ __forceinline__ void finish_record(sdrg_frame_record &rec, const Stat
 template <int WG, class Visit>
 __device__ __forceinline__ float kth_smallest(Visit visit, int k, int *hist, uint32_t *xch) {
     const int tid = threadIdx.x, lane = tid & (WAVE - 1), wave = tid / WAVE;
+    constexpr int XB = 2 * (WG / WAVE) > 8 ? 2 * (WG / WAVE) : 8;  // xch: the waves' AND / OR, then [XB, XB + 1]
     uint32_t band = 0xffffffffu, bor = 0u;
     visit([&](uint32_t b) {
         band &= b;
@@ -763,13 +775,13 @@ __device__ __forceinline__ float kth_smallest(Visit visit, int k, int *hist, uin
 #pragma unroll
                 for (int u = 0; u < 3; u++)
                     if (u < j) acc += hv[u];
-                xch[8] = (uint32_t)(4 * L + j);
-                xch[9] = (uint32_t)acc;
+                xch[XB] = (uint32_t)(4 * L + j);
+                xch[XB + 1] = (uint32_t)acc;
             }
         }
         __syncthreads();
-        const uint32_t d = xch[8];
-        k -= (int)xch[9];
+        const uint32_t d = xch[XB];
+        k -= (int)xch[XB + 1];
         prefix |= d << lo;
         mask |= dm << lo;
         top = lo - 1;
@@ -1321,6 +1333,631 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Wide statistics, four frames per workgroup (stats_wide_multi_kernel), for the geometries whose pooled gaps are one
+// bottom window (n_ref 2..4) or none (n_ref < 2) -- BASELINE configs[4]: 65536 bins, 200 kHz focus, two reference
+// windows of 13107 bins.  The single-frame kernel above spends most of its VALU on glibc-exact log10s (~30 VALU each,
+// nine of them f64): every focus bin's (the focus peak), every reference bin's (the pooled mean's dB sums) and, for
+// the pool, the bottom window's again or through HBM scratch.  This kernel evaluates only the logs the reference's
+// results depend on bin by bin:
+//   * the focus peak from powers alone: dB(p) = 10 log10f(p + 1e-20) never decreases with p (glibc's log10f is
+//     monotone, checked over every float: tests/test_libm_exact.py), so the first maximum of the dB values is the
+//     first focus bin whose power reaches p_lo, the smallest float with the dB of the largest power M.  During the
+//     scan each producer lane keeps its largest power and up to MW_K candidate bins (index order) whose power came
+//     within MW_DELTA of its running maximum; after it, p_lo is found among the 256 floats below M, and the peak is
+//     the first candidate >= p_lo.  A frame whose candidates overflowed, or whose p_lo is not within MW_DELTA / 2
+//     of M (powers where the 1e-20 dominates), re-scans its focus window for the first bin >= p_lo instead;
+//   * the reference windows' dB values for their dB sums in the scan (the chain wave), as scan_wide;
+//   * the bottom window's pooled gaps again after the scan, in parallel, into registers: nothing per bin goes to
+//     HBM, and the pool costs one more read of that window (MALL-resident: the scan read it just before).
+// ONE chain wave runs the sequential sums of the four frames side by side (16 lanes per frame: window sums, running
+// sums, dB sums), one record wave takes the strict `rs > bv` records of all four, and the producer waves stream every
+// window of every frame into the four rings (three lanes on a reference window per lane on the focus: its bins carry
+// no log).  Sums, records and peaks are the reference's, in its order; results cross lanes through LDS keys (value,
+// then the lower index) so that one atomic max picks the same element as scan_wide's shuffle reductions.  Each frame's
+// tail (6.2-6.6) runs on wave f, its pooled median on MW_T / 4 threads (four radix selects at once).  One 1024-thread
+// workgroup per CU: 1024 frames fill the chip once.
+#ifndef SDRG_MW_T  // threads per multi-frame workgroup
+#define SDRG_MW_T 1024
+#endif
+constexpr int MW_T = SDRG_MW_T;
+// lab: SDRG_MW_STAMPS=1 records s_memtime per workgroup at the phase boundaries (and each scan role's busy cycles)
+#ifndef SDRG_MW_STAMPS
+#define SDRG_MW_STAMPS 0
+#endif
+#define MW_STAMP(k)                                                                                            \
+    do {                                                                                                       \
+        if (SDRG_MW_STAMPS && threadIdx.x == 0 && blockIdx.x < 8192)                                           \
+            g_stats_stamps[blockIdx.x * STAMP_PHASES + (k)] = __builtin_amdgcn_s_memtime();                    \
+    } while (0)
+constexpr int MW_F = 4;                     // frames per workgroup
+#ifndef SDRG_MW_RECW  // record waves: 1 (all frames) or MW_F (one per frame)
+#define SDRG_MW_RECW MW_F
+#endif
+#ifndef SDRG_MW_WREF  // producer lanes per reference-window lane per focus lane (a reference bin carries a log10)
+#define SDRG_MW_WREF 2
+#endif
+#ifndef SDRG_MW_ILP  // 1: the reference producers' log10s of several bins interleave (no scheduling barrier)
+#define SDRG_MW_ILP 1
+#endif
+#ifndef SDRG_MW_PRIO  // lab: the chain wave's issue priority during the scan
+#define SDRG_MW_PRIO 0
+#endif
+// SDRG_MW_MAP 1: the record waves are waves 4, 8, 12 and 1, so the chain wave (wave 0; wave w runs on SIMD w mod 4)
+// shares its SIMD with three record waves only and no producer (their f64 log10s would take its issue slots)
+#ifndef SDRG_MW_MAP
+#define SDRG_MW_MAP 0
+#endif
+constexpr int MW_RECW = SDRG_MW_RECW;
+constexpr int MW_P0 = 1 + MW_RECW;          // first producer wave
+constexpr int MW_PROD = MW_T - 64 * MW_P0;  // producer lanes
+constexpr int MW_PR = 12;                   // bins per producer lane per chunk at most (the host sizes SC for it)
+constexpr int MW_RING_FLOATS = 28672;       // 112 KiB of rings at most
+constexpr int MW_POOL = 13312;              // pooled gaps per frame held in registers
+constexpr int MW_K = 4;                     // focus candidates per producer lane
+constexpr float MW_DELTA = 1e-4f;           // candidates: power >= running maximum x (1 - MW_DELTA)
+
+// float -> uint32 with the float order (-0 taken as +0, as a float compare does); NaN never reaches it
+__device__ __forceinline__ uint32_t ord_f(float x) {
+    const uint32_t b = __float_as_uint(x + 0.0f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f(uint32_t o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+// key of (value, index): a larger value wins, then the lower index (scan_wide's `om > m || (om == m && oi < mi)`)
+__device__ __forceinline__ unsigned long long vi_key(float v, int i) {
+    return ((unsigned long long)ord_f(v) << 32) | (unsigned long long)(0xffffffffu - (uint32_t)i);
+}
+
+// producer lanes per focus item and per reference item: a reference bin costs about three times a focus bin (its
+// log10), so reference windows get three times the lanes; without dB sums, equal shares
+__host__ __device__ inline void mw_lanes(int n_ref, bool want_db, int *pgf, int *pgr) {
+    const int fq = n_ref, nwin = n_ref + 1;
+    if (want_db && fq > 0) {
+        *pgf = MW_PROD / (SDRG_MW_WREF * MW_F * fq + MW_F);
+        *pgr = (MW_PROD - MW_F * *pgf) / (MW_F * fq);
+    } else {
+        *pgf = *pgr = MW_PROD / (MW_F * nwin);
+    }
+}
+
+template <bool want_db>
+__global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256))) void stats_wide_multi_kernel(
+    const float *__restrict__ spectra, int n_frames, StatsGeometry g, int64_t now_ms, StatsState *__restrict__ state,
+    sdrg_frame_record *__restrict__ records, int lg) {
+    constexpr int F = MW_F, GT = MW_T / F, REG = (MW_POOL + GT - 1) / GT, LPFR = WAVE / F, GW = GT / WAVE;
+    extern __shared__ __attribute__((aligned(16))) float ring[];
+    __shared__ __attribute__((aligned(16))) int hist[F][256];
+    __shared__ uint32_t sxch[F][2];
+    __shared__ uint32_t sband[MW_T / WAVE][2];
+    __shared__ int s_wt[MW_T / WAVE];
+    __shared__ unsigned long long s_rec[F][11];
+    __shared__ uint32_t s_pmax[F];
+    __shared__ int s_ovf[F], s_t[F], s_first[F];
+    __shared__ float s_sum[F][11], s_dsum[F][11], s_med[F], s_plo[F];
+    __shared__ float w_mean_db[F][10], w_best1k_db[F][10], sh_f[F][2];
+    __shared__ int order[F][10], sh_best_start[F];
+    __shared__ int sh_geo_lo[11], sh_geo_hi[11];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n_ref = g.n_ref, nwin = n_ref + 1, fq = n_ref;
+    const int f0 = blockIdx.x * F;
+    load_logf_tab();
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        if (tid == i) {
+            sh_geo_lo[i] = g.win_lo[i];
+            sh_geo_hi[i] = g.win_hi[i];
+        }
+    }
+    if (tid == 0) {
+        sh_geo_lo[n_ref] = g.focus_lo;
+        sh_geo_hi[n_ref] = g.focus_hi;
+    }
+    if (tid < F) {
+        s_pmax[tid] = 0u;  // below every ordered float: no focus bin
+        s_ovf[tid] = 0;
+        s_t[tid] = 256;
+        s_first[tid] = 0x7fffffff;
+    }
+    if (tid < F * 11) s_rec[tid / 11][tid % 11] = 0ull;
+    __syncthreads();
+    MW_STAMP(0);
+
+    const int SC = 1 << lg, RS = SC + 4, slot_floats = 3 * RS * nwin, frame_floats = 8 * RS * nwin;
+    int max_len = 0;
+    for (int q = 0; q < nwin; q++) max_len = max(max_len, sh_geo_hi[q] - sh_geo_lo[q] + 1);
+    const int nch = (max_len + SC - 1) >> lg;
+    const int w = g.win_bins_1k;
+    auto frame_of = [&](int f) { return min(f0 + f, n_frames - 1); };  // loads of a missing frame: a real one
+    auto frame_ptr = [&](int f) { return spectra + (size_t)frame_of(f) * (size_t)g.n; };
+
+    // ---- chain wave: lane = LPFR x frame + j; j < nwin window sums, then running sums, then dB sums ----
+    const int cf = lane / LPFR, cjj = lane - cf * LPFR;
+    int cg = 3, cj = 0;
+    if (cjj < nwin) cg = 0, cj = cjj;
+    else if (cjj < 2 * nwin) cg = 1, cj = cjj - nwin;
+    else if (want_db && cjj < 3 * nwin - 1) cg = 2, cj = cjj - 2 * nwin;
+    const bool chain = wave == 0 && cg < 3;
+    float acc = 0.0f;
+    // ---- record waves: G lanes per (frame, window); one wave for all frames, or wave 1 + f for frame f ----
+    const int rfr = MW_RECW == 1 ? F : 1;  // frames per record wave
+    const int G = WAVE / (rfr * nwin), ritem = lane / G, rq0 = ritem % nwin, rk = lane - ritem * G;
+    const bool mapped = SDRG_MW_MAP && MW_RECW == MW_F && MW_T == 1024;
+    const int rwave = !mapped ? (wave >= 1 && wave <= MW_RECW ? wave - 1 : -1)
+                              : wave == 4 ? 0 : wave == 8 ? 1 : wave == 12 ? 2 : wave == 1 ? 3 : -1;  // record wave index
+    const int rf = MW_RECW == 1 ? ritem / nwin : rwave, rq = rq0;
+    const bool rec_lane = rwave >= 0 && ritem < rfr * nwin;
+    float rm = -INFINITY;
+    int ri = 0x7fffffff;
+    // ---- producers: the F focus items first (pgf lanes each), then the F x fq reference items (pgr lanes each) ----
+    int pgf, pgr;
+    mw_lanes(n_ref, want_db, &pgf, &pgr);
+    // producer ordinal: the waves that are neither the chain nor a record wave, in order
+    const int pwave = !mapped ? wave - MW_P0 : wave - 1 - (wave > 1) - (wave > 4) - (wave > 8) - (wave > 12);
+    const bool is_prod_wave = wave != 0 && rwave < 0;
+    const int pw = pwave * 64 + lane;
+    int pf = 0, pq = 0, pk0 = 0, PGc = 1;
+    bool prod = false;
+    if (is_prod_wave) {
+        if (want_db) {
+            if (pw < F * pgf) {
+                pf = pw / pgf, pq = fq, pk0 = pw - pf * pgf, PGc = pgf, prod = true;
+            } else if (fq > 0) {
+                const int r = pw - F * pgf, it = r / pgr;
+                pf = it / fq, pq = it - pf * fq, pk0 = r - it * pgr, PGc = pgr, prod = it < F * fq;
+            }
+        } else {
+            const int it = pw / pgf;
+            pf = it / nwin, pq = it - pf * nwin, pk0 = pw - it * pgf, PGc = pgf, prod = it < F * nwin;
+        }
+    }
+    const bool foc_lane = prod && pq == fq;
+    const int plo = sh_geo_lo[prod ? pq : 0], plen = sh_geo_hi[prod ? pq : 0] - plo + 1;
+    const float *Pq = frame_ptr(prod ? pf : 0) + plo;
+    float va[MW_PR], vb[MW_PR];
+    // focus candidates: the lane's running maximum cm, up to MW_K bins (index order) that came within MW_DELTA of it
+    float cm = -INFINITY, cv[MW_K];
+    int ci[MW_K], nc = 0;
+    bool ovf = false;
+#pragma unroll
+    for (int j = 0; j < MW_K; j++) {
+        cv[j] = 0.0f;
+        ci[j] = 0x7fffffff;
+    }
+    auto fetch = [&](int c) {
+        const int c0 = c << lg;
+#pragma unroll
+        for (int k = 0; k < MW_PR; k++) {
+            const int t = pk0 + PGc * k, e = c0 + t;
+            const bool ok = t < SC && e < plen;
+            va[k] = ok ? Pq[e] : 0.0f;
+            vb[k] = (ok && e >= w) ? Pq[e - w] : 0.0f;
+        }
+    };
+    auto store = [&](int c) {
+        const int c0 = c << lg;
+        float *row = ring + pf * frame_floats + (c & 1) * slot_floats + pq * 3 * RS;
+#pragma unroll
+        for (int k = 0; k < MW_PR; k++) {
+            const int t = pk0 + PGc * k, e = c0 + t;
+            if (t < SC) {
+                const bool in = e < plen;
+                const float v = va[k];
+                row[t] = v;
+                row[RS + t] = (e >= w) ? v - vb[k] : v;
+                if (foc_lane) {
+                    if (in) {
+                        // a lane sees its focus bins in increasing order.  A new maximum more than MW_DELTA above the
+                        // last drops every candidate (all are then below any p_lo the check below accepts)
+                        if (v > cm) {
+                            if (v * (1.0f - MW_DELTA) > cm) nc = 0;
+                            cm = v;
+                        }
+                        if (v >= cm * (1.0f - MW_DELTA)) {
+#pragma unroll
+                            for (int j = 0; j < MW_K; j++) {
+                                cv[j] = (nc == j) ? v : cv[j];
+                                ci[j] = (nc == j) ? plo + e : ci[j];
+                            }
+                            ovf = ovf || nc == MW_K;
+                            nc = min(nc + 1, MW_K);
+                        }
+                    }
+                } else if (want_db) {
+                    row[2 * RS + t] = in ? db_of(v) : 0.0f;
+                }
+            }
+            if (!SDRG_MW_ILP) __builtin_amdgcn_sched_barrier(0);  // one bin's log10 at a time
+        }
+    };
+    if (prod && nch > 0) fetch(0);
+
+    unsigned long long busy = 0;
+    if (SDRG_MW_PRIO && wave == 0) __builtin_amdgcn_s_setprio(SDRG_MW_PRIO);
+    for (int c = 0; c <= nch + 1; c++) {
+        const unsigned long long t_in = SDRG_MW_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+        if (is_prod_wave) {
+            if (prod && c < nch) {
+                store(c);
+                if (c + 1 < nch) fetch(c + 1);
+            }
+        } else if (wave == 0) {
+            if (c >= 1 && c <= nch && chain) {
+                const float *slot = ring + cf * frame_floats + ((c - 1) & 1) * slot_floats;
+                const float *src = slot + (cj * 3 + cg) * RS;  // x, rs terms, dB rows
+                float *rsring = ring + cf * frame_floats + 2 * slot_floats;
+                // running values: the rs lanes' go to the rs ring (the record wave reads them); the window and dB
+                // sums' are never read and go back over the consumed bins row
+                float *dst = cg == 1 ? rsring + (((c - 1) & 1) * nwin + cj) * RS : const_cast<float *>(slot + cj * 3 * RS);
+                float4 A[4], B[4];
+                auto rd = [&](float4 (&X)[4], int u) {
+#pragma unroll
+                    for (int i = 0; i < 4; i++) X[i] = *reinterpret_cast<const float4 *>(src + u + 4 * i);
+                };
+                auto sum16 = [&](const float4 (&X)[4], int u) {
+                    float4 r[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        acc += X[i].x;
+                        r[i].x = acc;
+                        acc += X[i].y;
+                        r[i].y = acc;
+                        acc += X[i].z;
+                        r[i].z = acc;
+                        acc += X[i].w;
+                        r[i].w = acc;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];
+                };
+                rd(A, 0);
+                for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
+                    rd(B, t + 16);
+                    sum16(A, t);
+                    if (t + 32 < SC) rd(A, t + 32);
+                    sum16(B, t + 16);
+                }
+            }
+        } else if (rec_lane && c >= 2) {
+            // chunk c - 2's running sums: lane k of the group visits bins k, k + G, ... in increasing order
+            const int c0 = (c - 2) << lg;
+            const float *rsrow = ring + rf * frame_floats + 2 * slot_floats + ((c & 1) * nwin + rq) * RS;
+            if (c0 + SC > w - 1) {
+                for (int t = rk; t < SC; t += G) {
+                    const float v = rsrow[t];
+                    const bool gt = c0 + t >= w - 1 && v > rm;  // strict: the lane keeps its first maximum
+                    rm = gt ? v : rm;
+                    ri = gt ? c0 + t : ri;
+                }
+            }
+        }
+        if (SDRG_MW_STAMPS) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            busy += __builtin_amdgcn_s_memtime() - t_in;
+        }
+        wide_chunk_barrier();
+    }
+    if (SDRG_MW_PRIO && wave == 0) __builtin_amdgcn_s_setprio(0);
+    if (SDRG_MW_STAMPS && lane == 0 && blockIdx.x < 8192) {  // chain, a record wave, a focus and a reference producer
+        const int slot = wave == 0 ? 7 : rwave == 0 ? 8 : (is_prod_wave && pwave == 0) ? 9 : wave == MW_T / 64 - 1 ? 10 : -1;
+        if (slot > 0) g_stats_stamps[blockIdx.x * STAMP_PHASES + slot] = busy;
+    }
+    // ---- per-frame results through LDS ----
+    if (foc_lane && cm > -INFINITY) atomicMax(&s_pmax[pf], ord_f(cm));
+    if (foc_lane && ovf) atomicOr(&s_ovf[pf], 1);
+    if (rec_lane) atomicMax(&s_rec[rf][rq], vi_key(rm, ri));
+    if (chain && cg == 0) s_sum[cf][cj] = acc;
+    if (chain && cg == 2) s_dsum[cf][cj] = acc;
+    __syncthreads();
+    MW_STAMP(1);
+
+    // ---- 6.2 focus peak (:142-154): p_lo among the 256 floats below each frame's largest focus power ----
+    const int sf = tid / GT, stid = tid - sf * GT;  // the frame this thread works for in the group phases
+    const int flo = sh_geo_lo[fq], flen = sh_geo_hi[fq] - flo + 1;
+    const uint32_t om = s_pmax[sf];
+    const float M = om ? unord_f(om) : 0.0f;
+    const float ds = om ? db_of(M) : -130.0f;
+    const int bm = __float_as_int(M);
+    for (int t = stid; t < 256; t += GT) {
+        const int b = bm - t;
+        if (ds > -130.0f && b >= 0 && db_of(__int_as_float(b)) != ds) atomicMin(&s_t[sf], t);
+    }
+    __syncthreads();
+    if (stid == 0 && ds > -130.0f) {
+        const int T = s_t[sf];
+        int plo_b = bm - (T - 1);
+        if (T == 256) {  // every tested neighbour shares the maximum's dB (the 1e-20 floor): bisect below them
+            int lo = 0, hi = bm - 255;
+            if (hi <= 0) {
+                lo = 0;
+            } else {
+                while (lo < hi) {
+                    const int mid = lo + ((hi - lo) >> 1);
+                    if (db_of(__int_as_float(mid)) == ds) hi = mid;
+                    else lo = mid + 1;
+                }
+            }
+            plo_b = lo;
+        }
+        const float pl = __int_as_float(plo_b < 0 ? 0 : plo_b);
+        s_plo[sf] = pl;
+        // the candidates hold every bin >= p_lo when p_lo is within MW_DELTA / 2 of M and no lane overflowed
+        if (s_ovf[sf] || !(pl >= M * (1.0f - 0.5f * MW_DELTA))) s_ovf[sf] = 2;
+    }
+    __syncthreads();
+    if (ds > -130.0f) {
+        const float pl = s_plo[sf];
+        if (s_ovf[sf]) {  // the frame's focus window, read again: the first bin >= p_lo
+            const float *Pf = frame_ptr(sf) + flo;
+            for (int i = stid; i < flen; i += GT)
+                if (Pf[i] >= pl) {
+                    atomicMin(&s_first[sf], flo + i);
+                    break;
+                }
+        }
+    }
+    if (foc_lane) {  // the lane's first candidate >= p_lo (every candidate frame's threads: only where no re-scan ran)
+        const float pl = s_plo[pf];
+        const uint32_t omf = s_pmax[pf];
+        if (omf && !s_ovf[pf] && db_of(unord_f(omf)) > -130.0f) {
+            int first = 0x7fffffff;
+#pragma unroll
+            for (int j = MW_K - 1; j >= 0; j--)
+                if (j < nc && cv[j] >= pl) first = ci[j];
+            if (first != 0x7fffffff) atomicMin(&s_first[pf], first);
+        }
+    }
+    __syncthreads();
+    MW_STAMP(2);
+
+    // ---- each frame's tail on wave f (6.2 focus sum, 6.3 reference windows, sort, 6.4a) ----
+    const bool tw = wave < F;
+    const int tf = tw ? wave : 0;
+    const uint32_t omt = s_pmax[tf];
+    const float ds_t = omt ? db_of(unord_f(omt)) : -130.0f;
+    const bool hit = ds_t > -130.0f && s_first[tf] != 0x7fffffff;
+    const float abs_peak_db = hit ? ds_t : -130.0f;
+    const int peak_bin = hit ? s_first[tf] : flo;
+    if (tw && lane <= n_ref) {
+        const int lo = sh_geo_lo[lane], hi = sh_geo_hi[lane], n = hi - lo + 1;
+        const unsigned long long rkey = s_rec[tf][lane];
+        WinScan ws;
+        ws.sum = s_sum[tf][lane];
+        ws.best_start = lo;
+        if (n <= 0) {
+            ws.best1k = 0.0f;
+        } else if (n < w) {
+            ws.best1k = ws.sum / n;
+        } else {
+            ws.best1k = unord_f((uint32_t)(rkey >> 32)) / w;  // as scan_window: RN(max rs / w)
+            ws.best_start = lo + (int)(0xffffffffu - (uint32_t)rkey) - w + 1;
+        }
+        if (lane == n_ref) {
+            sh_f[tf][0] = db_of(ws.sum / n);  // signalPowerDb (:155)
+            sh_f[tf][1] = ws.best1k;          // focusBest1kLinear (:302)
+            sh_best_start[tf] = ws.best_start;
+        } else {
+            w_mean_db[tf][lane] = db_of(ws.sum / n);
+            w_best1k_db[tf][lane] = db_of(ws.best1k);
+        }
+    }
+    __syncthreads();
+    const int valid = (n_ref >= 2);
+    if (valid && tw && lane < n_ref) {  // libstdc++'s insertion sort for <= 16 elements: (meanDb, index) order
+        const float ki = w_mean_db[tf][lane];
+        int rank = 0;
+        for (int k = 0; k < n_ref; k++) {
+            const float kk = w_mean_db[tf][k];
+            rank += (kk < ki || (kk == ki && k < lane)) ? 1 : 0;
+        }
+        order[tf][rank] = lane;
+    }
+    __syncthreads();
+    const float signal_power_db = sh_f[tf][0];
+    MW_STAMP(3);
+
+    // ---- 6.4b: the bottom window's pooled gaps |dB - mean| (:252-269), evaluated again into registers, and their
+    //      median: four radix selects at once, GT threads per frame ----
+    if (want_db && valid) {
+        const int wb = order[sf][0];
+        const int lo = sh_geo_lo[wb], cnt = sh_geo_hi[wb] - lo + 1;
+        const float m = s_dsum[sf][wb] / (float)cnt;
+        const float *Pw = frame_ptr(sf) + lo;
+        float v[REG];
+#pragma unroll
+        for (int r = 0; r < REG; r++) {
+            const int q = stid + GT * r;
+            v[r] = q < cnt ? Pw[q] : 0.0f;
+        }
+        // slots past the window hold all-ones bits: a gap is never negative (bit 31 clear), so bit 31 is never a
+        // differing bit of the real values and the select's prefix never matches them (no per-slot masks to keep)
+#pragma unroll
+        for (int r = 0; r < REG; r++) {
+            v[r] = stid + GT * r < cnt ? fabsf(db_of(v[r]) - m) : __uint_as_float(0xffffffffu);
+            if (!SDRG_MW_ILP) __builtin_amdgcn_sched_barrier(0);  // one log10 at a time
+        }
+        MW_STAMP(4);
+        uint32_t band = 0xffffffffu, bor = 0u;
+#pragma unroll
+        for (int r = 0; r < REG; r++) {
+            const uint32_t b = __float_as_uint(v[r]);
+            band &= b;
+            bor |= b == 0xffffffffu ? 0u : b;
+        }
+        for (int off = WAVE / 2; off > 0; off >>= 1) {
+            band &= (uint32_t)__shfl_xor((int)band, off);
+            bor |= (uint32_t)__shfl_xor((int)bor, off);
+        }
+        if (lane == 0) {
+            sband[wave][0] = band;
+            sband[wave][1] = bor;
+        }
+        __syncthreads();
+        for (int u = sf * GW; u < (sf + 1) * GW; u++) {
+            band &= sband[u][0];
+            bor |= sband[u][1];
+        }
+        const uint32_t diff = band ^ bor;
+        int top = diff ? 31 - __clz(diff) : -1;  // highest bit where the frame's values differ (-1: all equal)
+        uint32_t mask = top >= 31 ? 0u : ~((2u << top) - 1u);
+        uint32_t prefix = band & mask;
+        int k = cnt / 2;
+        {
+            // the first digit 12 bits wide, its 4096-bin histogram per frame over the (now idle) rings: the top
+            // differing bits of the gaps are mostly exponent bits, which 8-bit digits leave in a few bins, and every
+            // lane adding to the same bin serialises the atomics
+            int *h1 = reinterpret_cast<int *>(ring) + sf * 4096;
+            const bool act = top >= 0;
+            const int dlo = top >= 11 ? top - 11 : 0;
+            const uint32_t dm = act ? (1u << (top - dlo + 1)) - 1u : 0u;
+#pragma unroll
+            for (int i = 0; i < 4096 / (4 * GT); i++)
+                *reinterpret_cast<int4 *>(&h1[4 * (stid + GT * i)]) = make_int4(0, 0, 0, 0);
+            __syncthreads();
+            if (act) {
+#pragma unroll
+                for (int r = 0; r < REG; r++) {
+                    const uint32_t b = __float_as_uint(v[r]);
+                    if ((b & mask) == prefix) atomicAdd(&h1[(b >> dlo) & dm], 1);
+                }
+            }
+            __syncthreads();
+            // bins [16 stid, 16 stid + 16) per thread: their sum, the frame's inclusive prefix over its GT threads
+            constexpr int BPT = 4096 / GT;
+            int own = 0;
+            if (act) {
+#pragma unroll
+                for (int i = 0; i < BPT; i += 4) {
+                    const int4 h = *reinterpret_cast<const int4 *>(&h1[BPT * stid + i]);
+                    own += h.x + h.y + h.z + h.w;
+                }
+            }
+            int incl = own;
+#pragma unroll
+            for (int off = 1; off < WAVE; off <<= 1) {
+                const int t = __shfl_up(incl, off);
+                if (lane >= off) incl += t;
+            }
+            if (lane == WAVE - 1) s_wt[wave] = incl;
+            __syncthreads();
+            for (int u = sf * GW; u < wave; u++) incl += s_wt[u];
+            const int excl = incl - own;
+            if (act && excl <= k && k < incl) {  // this thread's bins hold the k-th value
+                int a = excl, j = 0;
+                for (; j < BPT; j++) {
+                    const int hv = h1[BPT * stid + j];
+                    if (a + hv > k) break;
+                    a += hv;
+                }
+                sxch[sf][0] = (uint32_t)(BPT * stid + j);
+                sxch[sf][1] = (uint32_t)a;
+            }
+            __syncthreads();
+            if (act) {
+                k -= (int)sxch[sf][1];
+                prefix |= sxch[sf][0] << dlo;
+                mask |= dm << dlo;
+                top = dlo - 1;
+            }
+        }
+        for (int pass = 0; pass < 3; pass++) {  // then 8-bit digits: 12 + 3 x 8 bits cover 32
+            const bool act = top >= 0;
+            const int dlo = top >= 7 ? top - 7 : 0;
+            const uint32_t dm = act ? (1u << (top - dlo + 1)) - 1u : 0u;
+            if (stid < 64) *reinterpret_cast<int4 *>(&hist[sf][4 * stid]) = make_int4(0, 0, 0, 0);
+            __syncthreads();
+            if (act) {
+#pragma unroll
+                for (int r = 0; r < REG; r++) {
+                    const uint32_t b = __float_as_uint(v[r]);
+                    if ((b & mask) == prefix) atomicAdd(&hist[sf][(b >> dlo) & dm], 1);
+                }
+            }
+            __syncthreads();
+            if (act && stid < 64) {  // the frame's first wave locates the bucket holding the k-th value
+                const int4 h = *reinterpret_cast<const int4 *>(&hist[sf][4 * stid]);
+                const int own = h.x + h.y + h.z + h.w;
+                int incl = own;
+#pragma unroll
+                for (int off = 1; off < WAVE; off <<= 1) {
+                    const int t = __shfl_up(incl, off);
+                    if (lane >= off) incl += t;
+                }
+                const unsigned long long over = __ballot(incl > k);
+                const int L = __ffsll((long long)over) - 1;
+                if (lane == L) {
+                    int a = incl - own;
+                    const int hv[4] = {h.x, h.y, h.z, h.w};
+                    int j = 3;
+#pragma unroll
+                    for (int t = 2; t >= 0; t--) {
+                        int before = a;
+#pragma unroll
+                        for (int u = 0; u < t; u++) before += hv[u];
+                        if (before + hv[t] > k) j = t;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 3; u++)
+                        if (u < j) a += hv[u];
+                    sxch[sf][0] = (uint32_t)(4 * L + j);
+                    sxch[sf][1] = (uint32_t)a;
+                }
+            }
+            __syncthreads();
+            if (act) {
+                k -= (int)sxch[sf][1];
+                prefix |= sxch[sf][0] << dlo;
+                mask |= dm << dlo;
+                top = dlo - 1;
+            }
+        }
+        if (stid == 0) s_med[sf] = __uint_as_float(diff ? prefix : band);
+        __syncthreads();
+        MW_STAMP(5);
+    }
+    // ---- 6.4c/d, 6.5, 6.6 and the record: lane 0 of wave f ----
+    if (tw && lane == 0 && f0 + tf < n_frames) {
+        // the stream state only now: held in registers across the pool phase it would crowd out the pooled gaps
+        StatsState st = state[f0 + tf];
+        if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
+        if (valid) mean_snr_6_4a(w_mean_db[tf], order[tf], n_ref, signal_power_db, st);  // 6.4a (:235-247)
+        sdrg_frame_record rec;
+        __builtin_memset(&rec, 0, sizeof(rec));  // tail padding included: records compare and gather as bytes
+        rec.peak_bin = peak_bin;
+        rec.abs_peak_db = abs_peak_db;
+        rec.signal_power_db = signal_power_db;
+        rec.valid = valid;
+        rec.n_ref_windows = n_ref;
+        if (!valid) {
+            st.mean_snr_db = st.mean_snr_sigma = 0.0f;
+            st.peak_above_noise_mean_db = st.max_bin_snr_db = st.max_bin_snr_sigma = 0.0f;
+            st.best1khz_snr_db = st.best1khz_snr_sigma = 0.0f;
+        } else {
+            const int n_bottom = 1;  // want_db: n_ref in 2..4 (nBottom = max(1, int(0.4 n_ref)), :233)
+            const int wb = order[tf][0];
+            const int cnt = sh_geo_hi[wb] - sh_geo_lo[wb] + 1;
+            const float per_bin_mean = s_dsum[tf][wb] / (float)cnt;
+            const float med = s_med[tf];
+            const float sigma_bin = (cnt > 0) ? fmax_ref(1.4816f * med, 1.0f) : 1.0f;
+            if (cnt > 0) st.per_bin_mean = per_bin_mean;
+            const float pbm = (cnt > 0) ? per_bin_mean : 0.0f;
+            snr_6_4cd(g, st, abs_peak_db, pbm, sigma_bin, n_bottom, w_best1k_db[tf], order[tf], sh_f[tf][1],
+                      sh_best_start[tf]);
+        }
+        track_detect_6_5_6_6(g, st, valid, abs_peak_db, peak_bin, now_ms);
+        finish_record(rec, st);
+        if (records) records[f0 + tf] = rec;
+        state[f0 + tf] = st;
+    }
+    if (SDRG_MW_STAMPS) {
+        __syncthreads();
+        MW_STAMP(6);
+    }
+}
+
 }  // namespace
 
 // spans beyond the LDS stage take the wide kernel (scan_wide), whose pool is in HBM scratch (the radix select's
@@ -1332,7 +1969,9 @@ static int stage_bins(const StatsGeometry &geo) {
     return o;
 }
 static bool wide_for(const StatsGeometry &geo) { return stage_bins(geo) > STAGE_MAX; }
-static bool global_pool_for(const StatsGeometry &geo) { return wide_for(geo); }
+static bool multi_runs(const StatsGeometry &geo);
+// the single-frame wide kernel's pool scratch (the multi-frame kernel keeps its pool in registers)
+static bool global_pool_for(const StatsGeometry &geo) { return wide_for(geo) && !multi_runs(geo); }
 bool stats_uses_wide(const StatsGeometry &geo) { return wide_for(geo); }
 // floats of pool scratch per frame: the pooled bins, or (SDRG_WIDE_DBPOOL, one bottom window) every reference window's
 // dB values, window q at q * wst
@@ -1341,6 +1980,35 @@ static int pool_stride_for(const StatsGeometry &geo) {
     const int nb0 = (int)(geo.n_ref * 0.4f);
     const bool spec_pool = geo.n_ref >= 2 && (nb0 > 1 ? nb0 : 1) == 1;
     return (SDRG_WIDE_DBPOOL && spec_pool) ? geo.n_ref * wst : wst;
+}
+
+// The multi-frame wide kernel's plan (stats_wide_multi_kernel): ok when the pool is one bottom window (n_ref 2..4)
+// or there is none (n_ref < 2), the pooled gaps fit the registers and the chains fit 16 lanes per frame; the
+// chunk's bins per window 2^lg from the ring budget and the producer lanes; want_db: the dB sums and the pool.
+struct MultiPlan {
+    bool ok = false, want_db = false;
+    int lg = 0;
+};
+static MultiPlan multi_for(const StatsGeometry &geo) {
+    MultiPlan mp;
+    const int nwin = geo.n_ref + 1;
+    const int nb0 = (int)(geo.n_ref * 0.4f);
+    const bool spec_pool = geo.n_ref >= 2 && (nb0 > 1 ? nb0 : 1) == 1;
+    if (geo.focus_len <= 0 || geo.n_ref > 10 || (geo.n_ref >= 2 && !spec_pool) || geo.max_pool > MW_POOL) return mp;
+    const int chains = 2 * nwin + (spec_pool ? nwin - 1 : 0);
+    if (chains > WAVE / MW_F || WAVE / (MW_F * nwin) < 1) return mp;
+    int pgf, pgr;
+    mw_lanes(geo.n_ref, spec_pool, &pgf, &pgr);
+    if (pgf < 1 || pgr < 1) return mp;
+    const int pg = pgf < pgr ? pgf : pgr;
+    for (int l = 6; l <= 10; l++)
+        if (MW_F * nwin * 8 * ((1 << l) + 4) <= MW_RING_FLOATS && (1 << l) <= MW_PR * pg) mp.lg = l;
+    mp.ok = mp.lg > 0;
+    mp.want_db = spec_pool;
+    return mp;
+}
+static bool multi_runs(const StatsGeometry &geo) {
+    return wide_for(geo) && multi_for(geo).ok && !(SDRG_STATS_STAMPS || lab_getenv("SDRG_WIDE_SINGLE"));
 }
 
 size_t stats_global_pool_floats(const StatsGeometry &geo, int n_frames) {
@@ -1354,7 +2022,40 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
     if (global_pool && !gpool) return hipErrorInvalidValue;
     if (geo.n_ref > 10) return hipErrorInvalidValue;
     const int pool_stride = pool_stride_for(geo);
-    if (wide_for(geo)) {
+    if (multi_runs(geo)) {
+        const MultiPlan mp = multi_for(geo);
+        // the rings; after the scan the same LDS holds each frame's 4096-bin first-digit histogram of the select
+        const size_t lds = std::max(sizeof(float) * (size_t)MW_F * (size_t)(8 * (4 + (1 << mp.lg)) * (geo.n_ref + 1)),
+                                    sizeof(int) * (size_t)MW_F * 4096);
+        const void *k = mp.want_db ? reinterpret_cast<const void *>(stats_wide_multi_kernel<true>)
+                                   : reinterpret_cast<const void *>(stats_wide_multi_kernel<false>);
+        hipError_t e = ensure_dynamic_lds(k, (int)lds);
+        if (e != hipSuccess) return e;
+        const dim3 grid((n_frames + MW_F - 1) / MW_F);
+        if (mp.want_db)
+            hipLaunchKernelGGL(stats_wide_multi_kernel<true>, grid, dim3(MW_T), lds, stream, spectra, n_frames, geo, now_ms,
+                               state, records, mp.lg);
+        else
+            hipLaunchKernelGGL(stats_wide_multi_kernel<false>, grid, dim3(MW_T), lds, stream, spectra, n_frames, geo, now_ms,
+                               state, records, mp.lg);
+        if (SDRG_MW_STAMPS) {  // lab: mean cycles per phase over the workgroups of this call
+            std::vector<unsigned long long> h((size_t)STAMP_PHASES * 8192);
+            if (hipStreamSynchronize(stream) == hipSuccess &&
+                hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_stats_stamps), h.size() * 8) == hipSuccess) {
+                const int nw = std::min((int)grid.x, 8192);
+                double d[10] = {};
+                for (int b = 0; b < nw; b++) {
+                    const unsigned long long *t = &h[(size_t)b * STAMP_PHASES];
+                    for (int k = 0; k < 6; k++) d[k] += (double)(t[k + 1] - t[k]);
+                    for (int k = 0; k < 4; k++) d[6 + k] += (double)t[7 + k];
+                }
+                fprintf(stderr, "[mw stamps] cycles/workgroup: scan %.0f (busy: chain %.0f, records %.0f, first producer %.0f, "
+                                "last producer %.0f) | peak %.0f | tail %.0f | pool logs %.0f | select %.0f | end %.0f\n",
+                        d[0] / nw, d[6] / nw, d[7] / nw, d[8] / nw, d[9] / nw, d[1] / nw, d[2] / nw, d[3] / nw, d[4] / nw,
+                        d[5] / nw);
+            }
+        }
+    } else if (wide_for(geo)) {
         size_t lds = sizeof(float) * (size_t)RING_FLOATS;
         if (SDRG_STATS_STAMPS && lab_getenv("SDRG_STATS_LDS_KB")) {  // diagnostic: fewer frames per CU
             lds = (size_t)atoi(lab_getenv("SDRG_STATS_LDS_KB")) * 1024;

@@ -51,3 +51,34 @@ def test_stats_geometry_vs_oracle(S, O, n, fs, focus):
             want[b] = fst[b].signal_strength(spec[b], now)
         assert_records_equal(rec, want, msg=f"n{n} fs{fs} focus{focus} f{f}")
     eng.close()
+
+
+@pytest.mark.parametrize("n,fs,focus", [(65536, 2_000_000, 200), (65536, 2_500_000, 100), (16384, 2_000_000, 200),
+                                        (65536, 2_000_000, 20)])
+@pytest.mark.parametrize("B", [1, 6, 9])
+def test_wide_statistics_partial_groups(S, O, n, fs, focus, B):
+    """The wide statistics kernel runs several frames per workgroup (csrc/stats.hip, stats_wide_multi_kernel): stream
+    counts that leave the last workgroup partly empty, on caller spectra (sdrg_engine_signal_strength_host), every
+    field bit-exact against the oracle, the stream state carried over three calls."""
+    rng = np.random.default_rng(n + B + focus)
+    cfg = S.SDRConfig(centerFrequency=100_000_000, samplesPerReading=n, sampleRate=fs, freqFocusRangeKhz=focus,
+                      soundMode=1)
+    eng = S.Engine(cfg, B)
+    fst = [O.FftState(100_000_000, fs, n, focus) for _ in range(B)]
+    for f in range(3):
+        spec = rng.exponential(1.0, size=(B, n)).astype(np.float32)
+        for b in range(B):  # a peak in the focus; a plateau of 40 equal maxima; one of 400 (more near-maximum bins
+            # than the multi-frame kernel keeps as candidates per lane: its focus re-scan); noise only
+            if b % 4 == 0:
+                spec[b, n // 2 + int(rng.integers(-50, 50))] = np.float32(1e4 * (1 + f))
+            elif b % 4 == 1:
+                spec[b, n // 2 - 20:n // 2 + 20] = np.float32(77.0)
+            elif b % 4 == 2:
+                spec[b, n // 2 - 200:n // 2 + 200] = np.float32(55.0 + f)
+        now = 1000 + 333 * f
+        rec = eng.signal_strength(spec, now_ms=now)
+        want = np.zeros(B, dtype=rec.dtype)
+        for b in range(B):
+            want[b] = fst[b].signal_strength(spec[b], now)
+        assert_records_equal(rec, want, msg=f"n{n} fs{fs} focus{focus} B{B} f{f}")
+    eng.close()

@@ -236,7 +236,7 @@ def lpf_loop():
     return out
 
 
-def lpf_loop_interleaved():
+def lpf_loop_interleaved(spread=False):
     """lpf_loop() with the LDS traffic spread through the VALU stream: sub-blocks are numbered g = 4c + sb across
     chunks and live in buffer g mod 3; while sub-block g runs, after each 4-sample quad t its output quad is written
     and quad t of sub-block g + 2 is read (for sb = 2, 3 that is the next chunk's sub-block 0, 1, complete in its
@@ -245,9 +245,9 @@ def lpf_loop_interleaved():
     ring slot and are never used; the block drains them (lgkmcnt(0)) before it ends."""
     out = []
     u = "%="
-    out += [
-        "s_mov_b64 %[sv], exec",
-        "s_mov_b64 exec, 0xffff",
+    # the 16 stream lanes: 0-15, or (spread) lanes {0-3, 16-19, 32-35, 48-51}
+    lanes = ["s_mov_b32 exec_lo, 0xf000f", "s_mov_b32 exec_hi, 0xf000f"] if spread else ["s_mov_b64 exec, 0xffff"]
+    out += ["s_mov_b64 %[sv], exec"] + lanes + [
         "s_nop 4",
         "v_pk_mov_b32 v[46:47], %[z], %[z] op_sel:[1,0]",
         "v_pk_mov_b32 v[52:53], %[z], %[z] op_sel:[0,1]",
@@ -349,6 +349,8 @@ def main():
     emit("SDRG_LPF_LOOP_ASM", lpf_loop())
     print("// the same loop with the chunk's LDS reads and writes interleaved quad by quad (SDRG_LPF_INTERLEAVE)")
     emit("SDRG_LPF_LOOP_IL_ASM", lpf_loop_interleaved())
+    print("// the same on the lanes {0-3, 16-19, 32-35, 48-51} (SDRG_SERIAL_LANES=1)")
+    emit("SDRG_LPF_LOOP_IL_SPREAD_ASM", lpf_loop_interleaved(spread=True))
     print("// the low-pass chunk with its VALU on all 64 lanes and the LDS operations on the caller's lanes; extra operand")
     print("// %[sv] (=&s, 64-bit): the caller's EXEC (lab option SDRG_LPF_ASM=2)")
     emit("SDRG_LPF_CHUNK_SPLIT_ASM", chunk("lpf", split=True))

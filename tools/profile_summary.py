@@ -18,7 +18,7 @@ from collections import defaultdict
 TAG = sys.argv[1] if len(sys.argv) > 1 else "r1"
 OUT = "profiles"
 os.makedirs(OUT, exist_ok=True)
-ENGINE = ("spectrum16k_kernel", "spectrum_kernel", "stats_narrow_kernel", "stats_wide_kernel", "stats_kernel", "ssb_pipe_kernel", "four_step_a", "four_step_b", "ssb_chain_kernel",
+ENGINE = ("spectrum16k_kernel", "spectrum_kernel", "stats_narrow_kernel", "stats_wide_multi_kernel", "stats_wide_kernel", "stats_kernel", "ssb_pipe_kernel", "four_step_a", "four_step_b", "ssb_chain_kernel",
           "ssb_fir_kernel", "ssb_eq_kernel", "spectral_pulse_kernel", "audio_pulse_kernel", "audio_front_kernel",
           "pulse_reset_kernel")
 
@@ -69,6 +69,31 @@ if trace_csv:
                   f"* with no SSB work on the chip ({len(alone)} launches: the isolated leg and the FFT + statistics "
                   f"labelled leg): avg {sum(alone) / len(alone):.1f} us",
                   "* the bench line's `roofline` / `roofline_isolated` time the same two situations with HIP events"]
+    # the SSB stream per step in the pipelined schedule: consecutive ssb_pipe_kernel launches that overlap a spectrum launch,
+    # start to start (the pipeline kernel + the audio pulse detector + launch gaps), against the profiled run's own line
+    spec = [iv(r) for r in allr if "spectrum16k_kernel" in r["Kernel_Name"]]
+    ssb_s = sorted(ssb)
+    cad = []
+    for (a0, a1), (b0, b1) in zip(ssb_s, ssb_s[1:]):
+        if any(s < a1 and a0 < e for s, e in spec) and any(s < b1 and b0 < e for s, e in spec) and b0 - a0 < 1_000_000:
+            cad.append((b0 - a0) / 1e6)
+    dur = [(e - s) / 1e6 for s, e in ssb_s]
+    prof_line = None
+    plog = f"gpurun_out/prof_bench_{TAG}.log"
+    if os.path.exists(plog):
+        for ln in open(plog):
+            if ln.startswith("{"):
+                prof_line = json.loads(ln)
+    if cad:
+        cad.sort()
+        med = cad[len(cad) // 2]
+        lines += ["", "## SSB stream per step (pipelined schedule) from the kernel trace", "",
+                  f"* ssb_pipe_kernel start to next start, both beside a spectrum launch: median {med:.4f} ms over "
+                  f"{len(cad)} intervals; ssb_pipe_kernel duration median {sorted(dur)[len(dur) // 2]:.4f} ms"]
+        if prof_line and prof_line.get("ssb_latency_floor"):
+            b = prof_line["ssb_latency_floor"]["ssb_ms_coresident"]
+            lines.append(f"* the profiled run's own bench line: ssb_ms_coresident {b:.4f} ms, ms_per_step "
+                         f"{prof_line['ms_per_step']:.4f} ({100 * (b / med - 1):+.1f} % against the trace)")
 bench = None
 blog = f"gpurun_out/bench_{TAG}.log"
 if os.path.exists(blog):
