@@ -271,6 +271,10 @@ def main() -> int:
                     help="N = 1: start a one-rank torch.distributed group anyway (nccl = RCCL, or gloo with "
                          "--rehearse-gloo) and run the N > 1 code path -- per-step gathers on the engine's stream, "
                          "barriers, max-over-ranks timing, the full-spectra gather -- on the one GPU (a rehearsal line)")
+    ap.add_argument("--gather-mode", default="sync", choices=["sync", "async"],
+                    help="N > 1 (or --process-group): sync (default) makes the engine's stream wait for each step's "
+                         "gathers; async leaves them on RCCL's stream, overlapping the next step's kernels (rotated "
+                         "buffers, all complete inside the timed region)")
     ap.add_argument("--launch-dry-run", action="store_true", help=argparse.SUPPRESS)
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
@@ -365,7 +369,9 @@ def main() -> int:
     # PCM travels as bytes: neither RCCL nor gloo has a 16-bit integer type
     p_out = torch.empty((world * streams, 2 * plen), dtype=torch.uint8, device=gdev) if gather_pcm and rank == 0 else None
     f_lo, f_n = sdrg.focus_window(FS, n, focus_khz)
-    f_stage = torch.empty((streams, f_n), dtype=torch.float32, device=dev) if focus else None
+    # one focus staging buffer per rotated output buffer: an asynchronous gather may still read the last ones
+    f_stages = [torch.empty((streams, f_n), dtype=torch.float32, device=dev) for _ in range(N_OUTPUTS)] if focus else None
+    f_stage = f_stages[0] if focus else None
     f_out = torch.empty((world * streams, f_n), dtype=torch.float32, device=gdev) if focus and rank == 0 else None
     host = (lambda t: t.cpu()) if rehearse else (lambda t: t)
     if dist_on:
@@ -377,16 +383,36 @@ def main() -> int:
         eng.set_stream(work_stream.cuda_stream)
 
     calls = [0]
+    # RCCL gathers run asynchronously on RCCL's stream (after this step's kernels on the engine's stream): the next
+    # step's kernels do not wait for them.  A step's buffers (records, focus staging) are rotated over N_OUTPUTS, so
+    # before a step rewrites them it waits (on the GPU) for the gathers of the step that last used them
+    async_gather = dist_on and not rehearse and not gather_pcm and args.gather_mode == "async"
+    pending = []
+
+    def drain_gathers(keep: int) -> None:
+        while len(pending) > keep:
+            for w in pending.pop(0):
+                w.wait()
 
     def step(st=None):
-        nonlocal spec, rec
+        nonlocal spec, rec, f_stage
+        if async_gather:
+            drain_gathers(N_OUTPUTS - 1)
         iq = iqs[calls[0] % N_INPUTS]
         spec, rec = specs[calls[0] % N_OUTPUTS], recs[calls[0] % N_OUTPUTS]
+        if focus:
+            f_stage = f_stages[calls[0] % N_OUTPUTS]
         calls[0] += 1
         eng.process_device(iq.data_ptr(), fmt, stages if st is None else st, spec.data_ptr(), rec.data_ptr(),
                            pcm.data_ptr(), now[0])
         now[0] += n // 2000  # frame duration in ms at 2 Msps (8 ms for 16384)
-        if dist_on:
+        if async_gather:
+            ws = [shard.gather_records(rec, world, rank, dst=0, out=gathered, async_op=True)[1]]
+            if focus:
+                ws.append(shard.gather_focus(spec, f_lo, f_n, world, rank, dst=0, out=f_out, staging=f_stage,
+                                             async_op=True)[1])
+            pending.append([w for w in ws if w is not None])
+        elif dist_on:
             shard.gather_records(host(rec), world, rank, dst=0, out=gathered)  # records (peaks, stats) to rank 0
             if gather_pcm:
                 shard.gather_records(host(pcm.view(torch.uint8)), world, rank, dst=0, out=p_out)
@@ -415,10 +441,12 @@ def main() -> int:
         for _ in range(25):
             step()
         prewarm_steps += 25
+        drain_gathers(0)
         eng.synchronize()
     prewarm_ms = (time.perf_counter() - t_pre) * 1e3
     for _ in range(args.warmup):
         step()
+    drain_gathers(0)
     eng.synchronize()
     torch.cuda.synchronize()
     eng.reset_timing_stats()
@@ -428,6 +456,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain_gathers(0)  # every step's gathers complete inside the timed region
     eng.synchronize()
     torch.cuda.synchronize()
     if dist_on:
@@ -649,6 +678,10 @@ def main() -> int:
     out["prewarm_steps"] = prewarm_steps
     if ranks_info:
         out.update(ranks_info)
+    if dist_on:
+        out["gather_mode"] = ("asynchronous: each step's RCCL gathers run on RCCL's stream after that step's kernels, "
+                              f"{N_OUTPUTS} rotated record / focus buffers, all complete inside the timed region"
+                              if async_gather else "synchronous: the engine's stream waits for each step's gathers")
     if spectra_gather:
         out["spectra_gather"] = spectra_gather
     if ssb_iso_ms:

@@ -18,7 +18,7 @@ def stream_range(rank: int, world: int, streams_per_rank: int) -> tuple[int, int
     return rank * streams_per_rank, (rank + 1) * streams_per_rank
 
 
-def gather_records(records, world: int, rank: int, dst: int = 0, group=None, out=None):
+def gather_records(records, world: int, rank: int, dst: int = 0, group=None, out=None, async_op: bool = False):
     """Gather each rank's [B, record_bytes] uint8 record tensor to `dst`.
 
     Returns the [world*B, record_bytes] concatenation (global stream order) on `dst`, None elsewhere.  The
@@ -27,12 +27,16 @@ def gather_records(records, world: int, rank: int, dst: int = 0, group=None, out
     with RCCL the gather is ordered on the current stream, so no host synchronisation is needed.  With a process
     group initialised the collective runs at every world size, one rank included (so a one-GPU job drives the same
     RCCL path as an 8-GPU one); without one, world must be 1 and the tensor itself is returned.
+    async_op: return (result, work) without making the current stream wait for the collective (RCCL runs it on its
+    own stream after the current stream's earlier work); the caller keeps `records` (and `out`) unchanged until it
+    has called work.wait() (a stream-level wait with RCCL), e.g. by rotating buffers.  work is None when no
+    collective ran.
     """
     import torch
     import torch.distributed as dist
 
     if world == 1 and not (dist.is_available() and dist.is_initialized()):
-        return records  # no process group: nothing to gather
+        return (records, None) if async_op else records  # no process group: nothing to gather
     if rank == dst:
         if out is None:
             out = torch.empty((world * records.shape[0],) + tuple(records.shape[1:]), dtype=records.dtype,
@@ -40,12 +44,13 @@ def gather_records(records, world: int, rank: int, dst: int = 0, group=None, out
         bufs = list(out.chunk(world, dim=0))
     else:
         bufs = None
-    dist.gather(records, bufs, dst=dst, group=group)
-    return out if rank == dst else None
+    work = dist.gather(records, bufs, dst=dst, group=group, async_op=async_op)
+    res = out if rank == dst else None
+    return (res, work) if async_op else res
 
 
 def gather_focus(spectra, first_bin: int, n_bins: int, world: int, rank: int, dst: int = 0, group=None, out=None,
-                 staging=None):
+                 staging=None, async_op: bool = False):
     """Gather each rank's focus-window spectrum slice [B, n_bins] (bins [first_bin, first_bin + n_bins) of the
     [B, N] fftshifted spectra, sdrg.focus_window) to `dst` as [world*B, n_bins] float32, global stream order.
 
@@ -57,7 +62,7 @@ def gather_focus(spectra, first_bin: int, n_bins: int, world: int, rank: int, ds
     if staging is None:
         staging = torch.empty((spectra.shape[0], n_bins), dtype=spectra.dtype, device=spectra.device)
     staging.copy_(sl)
-    return gather_records(staging, world, rank, dst=dst, group=group, out=out)
+    return gather_records(staging, world, rank, dst=dst, group=group, out=out, async_op=async_op)
 
 
 def gather_spectra(spectra, world: int, rank: int, dst: int = 0, group=None, out=None):
