@@ -347,22 +347,13 @@ constexpr int PG = 16;          // streams per workgroup
 constexpr int CH = 64;          // samples per chunk
 constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_read_b128 by stream lanes
 constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
-// SDRG_FIR_PAIRS (lab): one FIR wave whose lane holds TWO streams' accumulators of one output slot as a packed pair
-// (lane = stream pair x slot): each product is one v_pk_mul_f32 of the two streams' samples by the broadcast tap and
-// each sum one v_pk_add_f32, in the reference's k order per stream -- 2 VALU per sample for two streams instead of
-// 3 (a packed product of two samples, then two scalar adds) -- and no second FIR wave (11 waves).  The clamp role
-// writes its output rows interleaved by stream pair for it.
-#ifndef SDRG_FIR_PAIRS
-#define SDRG_FIR_PAIRS 0
-#endif
-constexpr int PIPE_ROLES = 12;  // role ids (PipeWave)
-constexpr int PIPE_WAVES = SDRG_FIR_PAIRS ? 11 : 12;  // hardware waves
+constexpr int PIPE_WAVES = 12;
 constexpr int PIPE_T = PIPE_WAVES * 64;
 enum PipeWave : int { W_DC = 0, W_LPF = 1, W_AGC = 2, W_LOAD = 3, W_FIR0 = 4, W_OUT = 5, W_EQ = 6, W_FIR1 = 7,
                       W_DES0 = 8, W_DES1 = 9, W_DES2 = 10, W_DES3 = 11 };
 // role of hardware wave w = nibble w: w0 DC, w1 LPF, w2 AGC, w3 load, w4 OUT, w5 EQ, w6 DES2, w7 FIR0,
 // w8 DES0, w9 DES1, w10 DES3, w11 FIR1
-constexpr unsigned long long DEFAULT_ROLE_MAP = SDRG_FIR_PAIRS ? 0xB984A653210ull : 0x7B984A653210ull;
+constexpr unsigned long long DEFAULT_ROLE_MAP = 0x7B984A653210ull;
 constexpr int MAX_SLOTS = 32;   // concurrent FIR outputs per stream (up to 4 per FIR lane)
 constexpr int MAX_DONE = 8;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
@@ -538,48 +529,6 @@ __device__ __forceinline__ void fir_chunk(PipeLds &L, int c, int t0, int o_lo, i
 #pragma unroll
     for (int j = 0; j < NP; j++)
         if (done[j]) L.fq[c & 1][sl * MAX_DONE + (slot_o[j] & (MAX_DONE - 1))] = acc[J0 + j];
-}
-
-// SDRG_FIR_PAIRS: the slots of stream pair sp over one chunk, lane = (pair, slot group); L.out rows interleaved by pair
-// (pair row = 2 x ROW floats: sample t of streams 2 sp and 2 sp + 1 at 2 t, 2 t + 1).  Slot g + 8 j holds the output o
-// with o == slot mod NSL, as fir_chunk; each stream's sum keeps the reference's k order.
-template <int NP>
-__device__ __forceinline__ void fir_chunk_pairs(PipeLds &L, int c, int t0, int o_lo, int o_hi, int g, int nsl_mask, int sp,
-                                                int D, int NT, f2v (&acc)[MAX_SLOTS / 8]) {
-    const int t1 = t0 + CH;
-    int k0[NP];
-    bool done[NP];
-    int slot_o[NP];
-#pragma unroll
-    for (int j = 0; j < NP; j++) {
-        const int slot = 8 * j + g;
-        const int o = o_lo + ((slot - o_lo) & nsl_mask);
-        const int base = D * o;
-        const bool active = slot <= nsl_mask && o <= o_hi;
-        done[j] = active && base + NT <= t1;
-        slot_o[j] = o;
-        if (active && base >= t0) acc[j] = f2v{0.0f, 0.0f};
-        k0[j] = active ? (t0 - base + CH) : 0;
-    }
-    const float4 *in = reinterpret_cast<const float4 *>(&L.out[c & 1][sp * 2 * ROW]);
-#pragma unroll 4
-    for (int i = 0; i < CH / 4; i++) {
-        const float4 xa = in[2 * i], xb = in[2 * i + 1];  // samples 4i, 4i + 1 and 4i + 2, 4i + 3 of both streams
-#pragma unroll
-        for (int j = 0; j < NP; j++) {
-            const float4 h = reinterpret_cast<const float4 *>(&L.taps_sh[k0[j] & 3][k0[j] & ~3])[i];
-            acc[j] = acc[j] + f2v{xa.x, xa.y} * f2v{h.x, h.x};
-            acc[j] = acc[j] + f2v{xa.z, xa.w} * f2v{h.y, h.y};
-            acc[j] = acc[j] + f2v{xb.x, xb.y} * f2v{h.z, h.z};
-            acc[j] = acc[j] + f2v{xb.z, xb.w} * f2v{h.w, h.w};
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < NP; j++)
-        if (done[j]) {
-            L.fq[c & 1][(2 * sp) * MAX_DONE + (slot_o[j] & (MAX_DONE - 1))] = acc[j].x;
-            L.fq[c & 1][(2 * sp + 1) * MAX_DONE + (slot_o[j] & (MAX_DONE - 1))] = acc[j].y;
-        }
 }
 
 template <int FMT, bool DMA>
@@ -933,21 +882,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 }
             }
         });
-    } else if (SDRG_FIR_PAIRS && wave == W_FIR0) {
-        f2v pacc[MAX_SLOTS / 8];  // (stream 2 sp, stream 2 sp + 1) accumulators of slots g + 8 j
-#pragma unroll
-        for (int j = 0; j < MAX_SLOTS / 8; j++) pacc[j] = f2v{0.0f, 0.0f};
-        chunk_loop([&](int it) {
-            const int c = it - 6 - LA;
-            if (c >= 0 && c < nch && PL > 0) {
-                const int4 r = chunk_out[c];
-                const int sp = lane & 7, g = lane >> 3;
-                const int t0 = c * CH;
-                if (nsl_mask == 31) fir_chunk_pairs<4>(L, c, t0, r.x, r.y, g, nsl_mask, sp, D, NT, pacc);
-                else if (nsl_mask == 15) fir_chunk_pairs<2>(L, c, t0, r.x, r.y, g, nsl_mask, sp, D, NT, pacc);
-                else fir_chunk_pairs<1>(L, c, t0, r.x, r.y, g, nsl_mask, sp, D, NT, pacc);
-            }
-        });
     } else if (wave == W_FIR0 || wave == W_FIR1) {
         float facc[MAX_SLOTS / 4] = {};  // FIR accumulators (slots j*4 + lane/16)
         chunk_loop([&](int it) {
@@ -1000,18 +934,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                             if (t + 2 * q + 1 >= S) o[q].y = 0.0f;
                         }
                     }
-                    if constexpr (SDRG_FIR_PAIRS) {  // rows interleaved by stream pair: sample t at 2 t + (stream & 1)
-                        float *dst = &L.out[c & 1][(sl >> 1) * 2 * ROW + 2 * within + (sl & 1)];
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            dst[4 * q] = o[q].x;
-                            dst[4 * q + 2] = o[q].y;
-                        }
-                    } else {
-                        float *dst = &L.out[c & 1][sl * ROW + within];
-                        *reinterpret_cast<float4 *>(dst) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
-                        *reinterpret_cast<float4 *>(dst + 4) = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
-                    }
+                    float *dst = &L.out[c & 1][sl * ROW + within];
+                    *reinterpret_cast<float4 *>(dst) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
+                    *reinterpret_cast<float4 *>(dst + 4) = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
                 }
             }
         });
@@ -1083,9 +1008,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         });
     }
     if (stamps && lane == 0) {  // diagnostic build only: per-wave work cycles and loop cycles
-        stamps[(blockIdx.x * PIPE_ROLES + wave) * 3] = st_work;
-        stamps[(blockIdx.x * PIPE_ROLES + wave) * 3 + 1] = __builtin_amdgcn_s_memtime() - st_t0;
-        stamps[(blockIdx.x * PIPE_ROLES + wave) * 3 + 2] = __builtin_amdgcn_s_memrealtime() - st_r0;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * 3] = st_work;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * 3 + 1] = __builtin_amdgcn_s_memtime() - st_t0;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * 3 + 2] = __builtin_amdgcn_s_memrealtime() - st_r0;
     }
 
     if (high) __builtin_amdgcn_s_setprio(0);
@@ -1144,7 +1069,7 @@ unsigned long long *ssb_stamps_buffer(int n_frames) {
     }();
     if (!on) return nullptr;
     const int groups = (n_frames + PG - 1) / PG;
-    const size_t per_call = (size_t)groups * PIPE_ROLES * 3;
+    const size_t per_call = (size_t)groups * PIPE_WAVES * 3;
     if (groups > g_stamps_groups) {
         if (g_stamps) (void)hipFree(g_stamps);
         if (hipMalloc(reinterpret_cast<void **>(&g_stamps), sizeof(unsigned long long) * per_call * STAMP_CALLS) !=
@@ -1155,31 +1080,30 @@ unsigned long long *ssb_stamps_buffer(int n_frames) {
         g_stamps_groups = groups;
         g_stamp_call = 0;
     }
-    return g_stamps + (size_t)(g_stamp_call++ % STAMP_CALLS) * (size_t)g_stamps_groups * PIPE_ROLES * 3;
+    return g_stamps + (size_t)(g_stamp_call++ % STAMP_CALLS) * (size_t)g_stamps_groups * PIPE_WAVES * 3;
 }
 
 // Per role: work / loop cycles, loop time and effective clock of the last call; then the same averaged over the
 // recorded calls except the first and the last (the steady state of a pipelined run).
 void ssb_report_stamps() {
     if (!g_stamps || g_stamp_call == 0) return;
-    const size_t per_call = (size_t)g_stamps_groups * PIPE_ROLES * 3;
+    const size_t per_call = (size_t)g_stamps_groups * PIPE_WAVES * 3;
     const int ncalls = g_stamp_call < STAMP_CALLS ? g_stamp_call : STAMP_CALLS;
     std::vector<unsigned long long> h(per_call * STAMP_CALLS);
     if (hipMemcpy(h.data(), g_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-    const char *names[PIPE_ROLES] = {"DC", "LPF", "AGC", "LOAD", "FIR-0", "OUT", "EQ", "FIR-1", "DES-0", "DES-1",
+    const char *names[PIPE_WAVES] = {"DC", "LPF", "AGC", "LOAD", "FIR-0", "OUT", "EQ", "FIR-1", "DES-0", "DES-1",
                                      "DES-2", "DES-3"};
     const int last = (g_stamp_call - 1) % STAMP_CALLS;
-    for (int w = 0; w < PIPE_ROLES; w++) {
-        if (SDRG_FIR_PAIRS && w == W_FIR1) continue;  // no such wave
+    for (int w = 0; w < PIPE_WAVES; w++) {
         double work = 0, loop = 0, real = 0, swork = 0, sloop = 0, sreal = 0;
         int sc = 0;
         for (int k = 0; k < ncalls; k++) {
             const unsigned long long *c = h.data() + (size_t)k * per_call;
             double a = 0, b = 0, r = 0;
             for (int g = 0; g < g_stamps_groups; g++) {
-                a += c[(g * PIPE_ROLES + w) * 3];
-                b += c[(g * PIPE_ROLES + w) * 3 + 1];
-                r += c[(g * PIPE_ROLES + w) * 3 + 2];
+                a += c[(g * PIPE_WAVES + w) * 3];
+                b += c[(g * PIPE_WAVES + w) * 3 + 1];
+                r += c[(g * PIPE_WAVES + w) * 3 + 2];
             }
             if (k == last) {
                 work = a;

@@ -1527,18 +1527,16 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
         cv[j] = 0.0f;
         ci[j] = 0x7fffffff;
     }
-    // bins of this lane per chunk: t = pk0 + PGc k < SC (the unrolled slots past kmax are branched over, not masked)
-    const int kmax = prod ? (SC - pk0 + PGc - 1) / PGc : 0;
+    // (the slots t >= SC are masked, not branched over: branches around each bin's log10 cost the producers 70 % more
+    // time, tools/gpu_r4g.sh)
     auto fetch = [&](int c) {
         const int c0 = c << lg;
 #pragma unroll
         for (int k = 0; k < MW_PR; k++) {
-            if (k < kmax) {
-                const int t = pk0 + PGc * k, e = c0 + t;
-                const bool ok = e < plen;
-                va[k] = ok ? Pq[e] : 0.0f;
-                vb[k] = (ok && e >= w) ? Pq[e - w] : 0.0f;
-            }
+            const int t = pk0 + PGc * k, e = c0 + t;
+            const bool ok = t < SC && e < plen;
+            va[k] = ok ? Pq[e] : 0.0f;
+            vb[k] = (ok && e >= w) ? Pq[e - w] : 0.0f;
         }
     };
     auto store = [&](int c) {
@@ -1547,7 +1545,7 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
 #pragma unroll
         for (int k = 0; k < MW_PR; k++) {
             const int t = pk0 + PGc * k, e = c0 + t;
-            if (k < kmax) {
+            if (t < SC) {
                 const bool in = e < plen;
                 const float v = va[k];
                 row[t] = v;
