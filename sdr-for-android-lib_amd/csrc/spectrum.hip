@@ -386,11 +386,13 @@ __device__ __forceinline__ void exch2(f2 *lds, f2 (&v)[E]) {
     for (int i = 0; i < E; ++i) v[i] = nxt[i];
 }
 
-// raw samples x[t + 512 r] of frame f into registers (zero-extended 16/32-bit words)
+// raw samples x[t + 512 r] of frame f into registers (zero-extended 16/32-bit words); live = false gives a
+// zero-sized resource, so the loads return 0 without touching memory
 template <int FMT>
-__device__ __forceinline__ void issue_raw(const void *iq, int f, int t, uint32_t (&raw)[E]) {
+__device__ __forceinline__ void issue_raw(const void *iq, int f, int t, uint32_t (&raw)[E], bool live = true) {
     constexpr int BPS = bytes_per_sample<FMT>();
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(reinterpret_cast<const char *>(iq) + (size_t)f * N * BPS, N * BPS);
+    const __amdgpu_buffer_rsrc_t rs =
+        frame_rsrc(reinterpret_cast<const char *>(iq) + (size_t)f * N * BPS, live ? N * BPS : 0);
 #pragma unroll
     for (int r = 0; r < E; ++r) raw[r] = load_raw_word<FMT>(rs, t * BPS, r * (N / 32) * BPS);
 }
@@ -408,13 +410,17 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
     for (int i = t; i < A2_F4; i += T) a2[i] = reinterpret_cast<const float4 *>(tabs + 2 * P1_F2)[i];
     __syncthreads();
     constexpr int BPS = bytes_per_sample<FMT>();
-    constexpr float S = power_scale<FMT>();
     const f2 *p1_row = p1 + (t & 31);  // pass 1: P1[r][k], k = t mod 32
 
     constexpr bool STAGE = FMT != SDRG_IQ_CF32;  // CF32 (8 B/sample) loads at the top of the iteration
     uint32_t raw[E];
-    if constexpr (STAGE)
-        if ((int)blockIdx.x < n_frames) issue_raw<FMT>(iq, blockIdx.x, t, raw);
+    if constexpr (STAGE) {
+        issue_raw<FMT>(iq, (int)blockIdx.x < n_frames ? blockIdx.x : 0, t, raw, (int)blockIdx.x < n_frames);
+        // opaque words into the frame loop: with the loop's own loads zero-extended too, the compiler would hoist the
+        // zero-extension behind the loop's phi and spend a v_and per word per frame on it (once here, before the loop)
+#pragma unroll
+        for (int r = 0; r < E; ++r) asm volatile("; raw word %0" : "+v"(raw[r]));
+    }
 
     for (int frame = blockIdx.x; frame < n_frames; frame += gridDim.x) {
         f2 v[E];
@@ -446,7 +452,18 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
                 wa = cmul_v(bw, f2{aw.x, aw.y});
                 wb = cmul_v(bw, f2{aw.z, aw.w});
             }
+            // the input scale (a power of two, sqrt of power_scale) rides on the pass-2 twiddles and on the two
+            // untwiddled rows: every product scales exactly, so |X|^2 comes out scaled by S with the same bits
+            // as scaling it afterwards, and the 16 per-output multiplies go
+            constexpr float SS = FMT == SDRG_IQ_CF32 ? 1.0f : FMT == SDRG_IQ_CS16 ? 1.0f / 32768.0f : 1.0f / 128.0f;
+            static_assert(SS * SS == power_scale<FMT>(), "scale split");
             f2 pa = wa, pb = wb;
+            if constexpr (SS != 1.0f) {
+                pa = wa * SS;
+                pb = wb * SS;
+                v[0] = v[0] * SS;
+                v[16] = v[16] * SS;
+            }
 #pragma unroll
             for (int r = 1; r < 16; ++r) {
                 if (r > 1) {
@@ -466,17 +483,19 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
         }
         // ---- |X|^2 at the fftshifted index: outputs j + 1024 r, j = 2t, 2t + 1 ----
         f2s pw[16];
+        // one v_mul + one v_fma per output (im^2, then re^2 + that: the contraction the packed form compiled to),
+        // written straight into the store pair: the packed form needed three moves per pair to transpose the two
+        // butterflies' (re, im) into (re0, re1), (im0, im1)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-            pw[r] = f2s{(x0[r].x * x0[r].x + x0[r].y * x0[r].y) * S, (x1[r].x * x1[r].x + x1[r].y * x1[r].y) * S};
-        if constexpr (STAGE) {
-            if (next < n_frames) {
-                issue_raw<FMT>(iq, next, t, raw);
-            } else {  // last frame: define raw on this path too, so it is dead between the convert and here
-#pragma unroll
-                for (int r = 0; r < E; ++r) raw[r] = 0;
-            }
+        for (int r = 0; r < 16; ++r) {
+            float q0, q1, p0, p1;
+            asm("v_mul_f32 %0, %1, %1" : "=v"(q0) : "v"(x0[r].y));
+            asm("v_mul_f32 %0, %1, %1" : "=v"(q1) : "v"(x1[r].y));
+            asm("v_fma_f32 %0, %1, %1, %2" : "=v"(p0) : "v"(x0[r].x), "v"(q0));
+            asm("v_fma_f32 %0, %1, %1, %2" : "=v"(p1) : "v"(x1[r].x), "v"(q1));
+            pw[r] = f2s{p0, p1};
         }
+        if constexpr (STAGE) issue_raw<FMT>(iq, next < n_frames ? next : frame, t, raw, next < n_frames);
         float *o = spectra + (size_t)frame * N + 2 * t;
         if constexpr (ABL & 16) {  // keep the values live without the stores
             float acc = 0.f;
@@ -484,9 +503,13 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
             for (int r = 0; r < 16; ++r) acc += pw[r].x + pw[r].y;
             if (acc == 1.2345f) o[0] = acc;
         } else {
+            // buffer stores: the fftshifted row offsets are scalar constants, so no 64-bit address adds per store
+            const __amdgpu_buffer_rsrc_t os = frame_rsrc(spectra + (size_t)frame * N, N * 4);
+            typedef unsigned u2 __attribute__((ext_vector_type(2)));
 #pragma unroll
             for (int r = 0; r < 16; ++r)
-                __builtin_nontemporal_store(pw[r], reinterpret_cast<f2s *>(o + ((r * 1024 + N / 2) & (N - 1))));
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, pw[r]), os, 8 * t,
+                                                      4 * ((r * 1024 + N / 2) & (N - 1)), 2 /* nt */);
         }
     }
 }

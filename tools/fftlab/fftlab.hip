@@ -166,7 +166,14 @@ int main(int argc, char **argv) {
         const double med = ms[reps / 2];
         const double gbs = v.bytes_per_sample * N * (double)B / (med * 1e-3) / 1e9;
         printf("%-14s %8.1f us  %7.1f GB/s  (%.1f%% of 8 TB/s)  min %.1f us", v.name, med * 1e3, gbs, gbs / 80.0, ms[0] * 1e3);
-        if (v.check) printf("  check: %d bad, worst err/tol %.3f", bad, worst);
+        if (v.check) {
+            // FNV-1a over every output bit pattern: equal hashes = the same spectra bit for bit
+            std::vector<uint32_t> all((size_t)B * N);
+            CK(hipMemcpy(all.data(), d_out, all.size() * 4, hipMemcpyDeviceToHost));
+            uint64_t h = 1469598103934665603ull;
+            for (uint32_t w : all) h = (h ^ w) * 1099511628211ull;
+            printf("  check: %d bad, worst err/tol %.3f, bits %016llx", bad, worst, (unsigned long long)h);
+        }
         printf("\n");
     }
     return 0;
