@@ -219,6 +219,15 @@ struct sdrg_engine {
     bool sa_live[SA_RING] = {};
     int64_t sa_calls = 0;
     hipEvent_t last_stats_end = nullptr;    // the last asynchronous statistics (wait_outputs, synchronize)
+    // the audio pulse detector (AudioPulseDetector::process after processSSB_opt, ssb_processor.cpp:109) runs on s_ap
+    // after the call's SSB pipeline, so the SSB stream (the pipelined step's critical path) carries the SSB kernels
+    // alone.  Call k's front end (inside its SSB kernel) writes energy-frame set k % NEW_SETS; before it does, the host
+    // waits for the detector of call k - NEW_SETS, which read that set.
+    hipStream_t s_ap = nullptr;
+    hipEvent_t ev_ap_end[sdrg_pulse_bank::NEW_SETS] = {};
+    bool ap_live[sdrg_pulse_bank::NEW_SETS] = {};
+    int64_t ap_calls = 0;
+    hipEvent_t last_ap_end = nullptr;       // the last detector (outputs, joins)
     // NCO/short-FIR SSB variant (sdrg_engine_set_ssb_variant; a build extension, off by default)
     double nco_hz = 0.0;
     int fir_taps = 0;            // 0: the reference's 255
@@ -628,18 +637,26 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         // AudioPulseDetector::process(pcm) after processSSB_opt (ssb_processor.cpp:109): its per-sample front
         // end runs inside the SSB kernel on the PCM it produces, the detector right after
         AudioFront af;
+        const int ap_set = (int)(e->ap_calls % sdrg_pulse_bank::NEW_SETS);
         if (do_ap) {
-            int32_t rc = pulse_bank_audio_front(&e->audio_bank, sp.pcm_len, &af, e->s_ssb);
+            if (e->ap_live[ap_set]) HIP_TRY(hipEventSynchronize(e->ev_ap_end[ap_set]));
+            int32_t rc = pulse_bank_audio_front(&e->audio_bank, sp.pcm_len, &af, e->s_ssb, ap_set);
             if (rc) return rc;
         }
         HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_chunk_table, e->d_ssb, e->d_ssb_scratch, pcm,
                            do_ap ? &af : nullptr, e->s_ssb));
-        if (do_ap) {
-            int32_t rc = pulse_bank_audio_detect(&e->audio_bank, e->audio_bank.d_out, e->s_ssb);
-            if (rc) return rc;
-        }
-        // the SSB stream's end marker: input release (the SSB pipeline, an iq reader, is done), join, timing
+        // the SSB stream's end marker: input release (the SSB pipeline, an iq reader, is done), join, timing, and
+        // the audio detector's start
         HIP_TRY(hipEventRecord(mk_ssb_end, e->s_ssb));
+        if (do_ap) {
+            HIP_TRY(hipStreamWaitEvent(e->s_ap, mk_ssb_end, 0));
+            int32_t rc = pulse_bank_audio_detect(&e->audio_bank, e->audio_bank.d_out, e->s_ap, ap_set);
+            if (rc) return rc;
+            HIP_TRY(hipEventRecord(e->ev_ap_end[ap_set], e->s_ap));
+            e->ap_live[ap_set] = true;
+            e->last_ap_end = e->ev_ap_end[ap_set];
+            e->ap_calls++;
+        }
     }
     if (do_stats) {
         hipStream_t st = sm;
@@ -670,7 +687,10 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         HIP_TRY(hipEventRecord(e->ev_join_spec, e->s_spec));
         HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join_spec, 0));
     }
-    if (do_ssb && !early_fork) HIP_TRY(hipStreamWaitEvent(e->s_main, mk_ssb_end, 0));  // join
+    if (do_ssb && !early_fork) {  // join
+        HIP_TRY(hipStreamWaitEvent(e->s_main, mk_ssb_end, 0));
+        if (do_ap) HIP_TRY(hipStreamWaitEvent(e->s_main, e->last_ap_end, 0));
+    }
     if (do_spec || prof) HIP_TRY(hipEventRecord(mk_main_end, e->s_main));
     if (prof) {
         ev->pending = true;
@@ -840,7 +860,11 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         return (v && atoi(v) == 1) ? (unsigned)hipEventDisableTiming
                                    : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
     }();
-    hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join, &e->ev_in_main, &e->ev_in_ssb};
+    if (hipStreamCreateWithFlags(&e->s_ap, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
+    hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join, &e->ev_in_main, &e->ev_in_ssb, &e->ev_ap_end[0], &e->ev_ap_end[1],
+                         &e->ev_ap_end[2]};
+    static_assert(sdrg_pulse_bank::NEW_SETS == 3, "ev_ap_end creation");
     for (auto p : evs)
         if (hipEventCreateWithFlags(p, ev_flags) != hipSuccess)
             return cleanup(fail(SDRG_E_HIP, "hipEventCreate failed"));
@@ -857,7 +881,9 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (e->s_main) (void)hipStreamSynchronize(e->s_main);
     if (e->s_ssb) (void)hipStreamSynchronize(e->s_ssb);
     if (e->s_stats) (void)hipStreamSynchronize(e->s_stats);
+    if (e->s_ap) (void)hipStreamSynchronize(e->s_ap);
     e->spec_bank.last_stream = e->audio_bank.last_stream = nullptr;  // drained above
+    e->spec_bank.detect_stream = e->audio_bank.detect_stream = nullptr;
     void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_nco_tab, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch, e->d_pool,
                     e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_ss_stage, e->d_rec_stage, e->d_pcm_stage};
     for (void *b : bufs)
@@ -866,7 +892,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     for (hipEvent_t ev : e->ev_stats_end)
         if (ev) (void)hipEventDestroy(ev);
     hipEvent_t evs[] = {e->ev_fork, e->ev_join, e->ev_in_main, e->ev_in_ssb, e->ev_fork_spec, e->ev_join_spec,
-                        e->ev_spec_done};
+                        e->ev_spec_done, e->ev_ap_end[0], e->ev_ap_end[1], e->ev_ap_end[2]};
     for (hipEvent_t ev : evs)
         if (ev) (void)hipEventDestroy(ev);
     for (auto &r : e->ring) {
@@ -880,6 +906,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (e->s_ssb) (void)hipStreamDestroy(e->s_ssb);
     if (e->s_spec) (void)hipStreamDestroy(e->s_spec);
     if (e->s_stats) (void)hipStreamDestroy(e->s_stats);
+    if (e->s_ap) (void)hipStreamDestroy(e->s_ap);
     delete e;
     return SDRG_OK;
 }
@@ -949,7 +976,8 @@ int32_t sdrg_engine_wait_outputs(sdrg_engine *e, void *hip_stream) {
     HIP_TRY(dscope.error());
     hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : e->s_main;
     if (e->last_in_main && s != e->s_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));  // spectra
-    if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));                    // PCM, audio pulse
+    if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));                    // PCM
+    if (e->last_ap_end) HIP_TRY(hipStreamWaitEvent(s, e->last_ap_end, 0));                    // audio pulse
     if (e->stats_async && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));  // records
     return SDRG_OK;
 }
@@ -1018,6 +1046,7 @@ int32_t sdrg_engine_reset_state(sdrg_engine *e) {
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));
     if (e->s_stats) HIP_TRY(hipStreamSynchronize(e->s_stats));
+    HIP_TRY(hipStreamSynchronize(e->s_ap));
     HIP_TRY(memset_sync(e->d_stats, 0, sizeof(StatsState) * (size_t)e->n_streams));
     HIP_TRY(memset_sync(e->d_ssb, 0, sizeof(SsbStreamState) * (size_t)e->n_streams));
     e->ssb = SsbControl{};
@@ -1041,6 +1070,7 @@ int32_t sdrg_engine_set_pipelining(sdrg_engine *e, int32_t on) {
     if (e->pipelined && !mode) {  // re-join what is in flight so later work on s_main follows it
         HIP_TRY(hipEventRecord(e->ev_join, e->s_ssb));
         HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_join, 0));
+        if (e->last_ap_end) HIP_TRY(hipStreamWaitEvent(e->s_main, e->last_ap_end, 0));
     }
     if (e->stats_async && !async && e->last_stats_end)  // the asynchronous statistics in flight, likewise
         HIP_TRY(hipStreamWaitEvent(e->s_main, e->last_stats_end, 0));
@@ -1099,6 +1129,7 @@ int32_t sdrg_engine_get_pulse_outputs(sdrg_engine *e, sdrg_pulse_output *spectra
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));
     if (e->s_stats) HIP_TRY(hipStreamSynchronize(e->s_stats));
+    HIP_TRY(hipStreamSynchronize(e->s_ap));
     const size_t bytes = sizeof(sdrg_pulse_output) * (size_t)e->n_streams;
     if (spectral) {
         if (!e->spec_bank_live) return fail(SDRG_E_INVALID, "the spectral pulse stage has not run");
@@ -1173,6 +1204,7 @@ int32_t sdrg_engine_synchronize(sdrg_engine *e) {
     HIP_TRY(hipStreamSynchronize(e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_ssb));  // not joined into s_main when pipelined
     if (e->s_stats) HIP_TRY(hipStreamSynchronize(e->s_stats));  // SDRG_PIPELINE_STATS_ASYNC
+    HIP_TRY(hipStreamSynchronize(e->s_ap));                      // the audio pulse detector
     static const bool stamps = [] {
         const char *v = lab_getenv("SDRG_PIPE_STAMPS");
         return v && v[0] == '1';

@@ -84,8 +84,15 @@ int32_t alloc_rings(sdrg_pulse_bank *b, int cap) {
 }
 
 // Re-lay every stream's rings out at a larger capacity, keeping the logical contents (deque order).
-int32_t regrow(sdrg_pulse_bank *b, int new_cap) {
+// every stream the bank's kernels may still run on
+int32_t sync_streams(sdrg_pulse_bank *b) {
     if (b->last_stream) PB_TRY(hipStreamSynchronize(b->last_stream));
+    if (b->detect_stream && b->detect_stream != b->last_stream) PB_TRY(hipStreamSynchronize(b->detect_stream));
+    return SDRG_OK;
+}
+
+int32_t regrow(sdrg_pulse_bank *b, int new_cap) {
+    if (int32_t rc = sync_streams(b)) return rc;
     if (b->reset_pending) return alloc_rings(b, new_cap);  // nothing to keep
     const int S = b->n_streams, oc = b->cap, om = oc - 1;
     const bool spectral = b->kind == SDRG_PULSE_SPECTRAL;
@@ -180,7 +187,8 @@ int32_t pulse_bank_init(sdrg_pulse_bank *b, int kind, const sdrg_pulse_config *c
     PB_TRY(dscope_.error());
     if ((rc = dev_alloc(&b->d_state, (size_t)n_streams)) || (rc = dev_alloc(&b->d_out, (size_t)n_streams))) return rc;
     if (kind == SDRG_PULSE_SPECTRAL && (rc = dev_alloc(&b->d_fh, (size_t)n_streams * 2 * PULSE_FH_SLOTS))) return rc;
-    if (kind == SDRG_PULSE_AUDIO && (rc = dev_alloc(&b->d_new_count, (size_t)n_streams))) return rc;
+    if (kind == SDRG_PULSE_AUDIO && (rc = dev_alloc(&b->d_new_count, (size_t)n_streams * sdrg_pulse_bank::NEW_SETS)))
+        return rc;
     if ((rc = alloc_rings(b, cap_for(*cfg)))) return rc;
     // (the null stream's fill, waited for: the bank's kernels run on non-blocking streams)
     PB_TRY(hipMemset(b->d_out, 0, sizeof(sdrg_pulse_output) * (size_t)n_streams));
@@ -191,7 +199,7 @@ int32_t pulse_bank_init(sdrg_pulse_bank *b, int kind, const sdrg_pulse_config *c
 
 void pulse_bank_release(sdrg_pulse_bank *b) {
     DeviceScope dscope_(b->device);
-    if (b->last_stream) (void)hipStreamSynchronize(b->last_stream);
+    (void)sync_streams(b);
     void *bufs[] = {b->d_state, b->d_e, b->d_f, b->d_rt, b->d_re, b->d_fh, b->d_out, b->d_in, b->d_new, b->d_new_count};
     for (void *p : bufs)
         if (p) (void)hipFree(p);
@@ -224,33 +232,39 @@ int32_t pulse_bank_spectral(sdrg_pulse_bank *b, const float *snr_sigma, const fl
     return SDRG_OK;
 }
 
-int32_t pulse_bank_audio_front(sdrg_pulse_bank *b, int n, AudioFront *af, hipStream_t stream) {
+int32_t pulse_bank_audio_front(sdrg_pulse_bank *b, int n, AudioFront *af, hipStream_t stream, int set) {
     DeviceScope dscope_(b->device);
     PB_TRY(dscope_.error());
     if (b->kind != SDRG_PULSE_AUDIO) return fail(SDRG_E_INVALID, "not an audio pulse bank");
+    if (set < 0 || set >= sdrg_pulse_bank::NEW_SETS) return fail(SDRG_E_INVALID, "energy-frame set %d", set);
     const PulseParams p = params_of(b);
     const size_t max_new = (size_t)std::max(n, 0) / (size_t)p.frame_samples + 2;  // (frameCount_ + n) / frameSamples_ < this
     if (max_new > b->new_slots || !b->d_new) {
-        if (b->last_stream) PB_TRY(hipStreamSynchronize(b->last_stream));  // the old buffer may be in use
-        int32_t rc = dev_alloc(&b->d_new, (size_t)b->n_streams * max_new);
+        if (int32_t rc = sync_streams(b)) return rc;  // the old buffer may be in use
+        int32_t rc = dev_alloc(&b->d_new, (size_t)sdrg_pulse_bank::NEW_SETS * b->n_streams * max_new);
         if (rc) return rc;
         b->new_slots = max_new;
     }
-    int32_t rc = before_launch(b, stream);  // a pending reset runs before the front end reads the state
+    // a pending reset runs before the front end reads the state, and after every detector that still uses it
+    if (b->reset_pending && b->detect_stream && b->detect_stream != stream) PB_TRY(hipStreamSynchronize(b->detect_stream));
+    int32_t rc = before_launch(b, stream);
     if (rc) return rc;
     memcpy(af->band, p.band, sizeof(af->band));
     memcpy(af->low, p.low, sizeof(af->low));
     af->frame_samples = p.frame_samples;
     af->max_new = (int)b->new_slots;
     af->state = b->d_state;
-    af->new_e = b->d_new;
-    af->new_count = b->d_new_count;
+    af->new_e = b->d_new + (size_t)set * b->n_streams * b->new_slots;
+    af->new_count = b->d_new_count + (size_t)set * b->n_streams;
     return SDRG_OK;
 }
 
-int32_t pulse_bank_audio_detect(sdrg_pulse_bank *b, sdrg_pulse_output *out, hipStream_t stream) {
-    PB_TRY(launch_audio_detect(params_of(b), b->n_streams, b->d_state, b->d_e, b->d_rt, b->d_re, b->d_new,
-                               (int)b->new_slots, b->d_new_count, out, stream));
+int32_t pulse_bank_audio_detect(sdrg_pulse_bank *b, sdrg_pulse_output *out, hipStream_t stream, int set) {
+    if (set < 0 || set >= sdrg_pulse_bank::NEW_SETS) return fail(SDRG_E_INVALID, "energy-frame set %d", set);
+    if (stream != b->last_stream) b->detect_stream = stream;
+    PB_TRY(launch_audio_detect(params_of(b), b->n_streams, b->d_state, b->d_e, b->d_rt, b->d_re,
+                               b->d_new + (size_t)set * b->n_streams * b->new_slots, (int)b->new_slots,
+                               b->d_new_count + (size_t)set * b->n_streams, out, stream));
     return SDRG_OK;
 }
 

@@ -881,7 +881,6 @@ __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restr
     extern __shared__ __attribute__((aligned(16))) float stage[];
     __shared__ int sh_woff[12];
     __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
-    __shared__ unsigned sh_hw[4];                   // wide_role
     __shared__ __attribute__((aligned(16))) int hist[256];
     __shared__ uint32_t sh_xch[2];
     __shared__ float w_mean_db[10], w_best1k_db[10];
