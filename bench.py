@@ -695,8 +695,9 @@ def main() -> int:
             "ssb_ms_coresident": round(ts["ssb_ms"], 4),
             "frac_coresident": round(floor_ms / ts["ssb_ms"], 4) if ts["ssb_ms"] > 0 else None,
             "coresident_basis": ("every timed step: the SSB stream's time per step in the pipelined timed region, from "
-                                 "one step's SSB end marker to the next (the SSB pipeline kernel + the audio pulse "
-                                 "detector + their launch gaps; the first step from its own start marker)"
+                                 "one step's SSB end marker to the next (the SSB pipeline kernels and their launch "
+                                 "gaps; the audio pulse detector runs on a stream of its own; the first step from its "
+                                 "own start marker)"
                                  if pipelined else "every timed step: the SSB stream's start to end marker")}
         # the same kernel against HBM: the step's longest kernel by GPU time, and latency-bound (the floor above)
         ssb_bytes = streams * n * in_bps + streams * 2 * plen
