@@ -137,14 +137,14 @@ typedef struct sdrg_callbacks {
  * kernel was launched on (only filled while profiling is enabled).  Pipelined, the SSB chain's start marker
  * would sit on the SSB stream, the step's critical path, so only the first call after a reset of the timing
  * statistics carries one; every later pipelined call's ssb_ms is its SSB stream time, from the previous call's
- * SSB end marker to its own (the chain's kernels + the audio pulse detector + the launch gaps between them;
- * the stream idles in between only if the host falls behind). */
+ * SSB end marker to its own (the chain's kernels + the launch gaps between them; the stream idles in between only
+ * if the host falls behind).  The audio pulse detector runs after the chain on a stream of its own. */
 typedef struct sdrg_timings {
     float spectrum_ms;   /* unpack + FFT + |X|^2 + fftshift kernel */
     float stats_ms;      /* end of the spectrum -> end of the signal-strength kernel (+ spectral pulse detector when
                             requested), on the statistics' stream; never includes the SSB stream's work */
-    float ssb_ms;        /* whole SSB chain (all its kernels, + audio pulse detector when requested); pipelined:
-                            the SSB stream's time per call, above */
+    float ssb_ms;        /* whole SSB chain (all its kernels; not the audio pulse detector, which runs on a stream
+                            of its own after it); pipelined: the SSB stream's time per call, above */
     float total_ms;      /* call start -> end of the main stream's work; joined calls include the SSB stream */
 } sdrg_timings;
 

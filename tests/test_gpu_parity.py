@@ -329,7 +329,7 @@ def test_pipelined_calls_equal_joined_calls(S, O):
     pipelined mode (the SSB stage forked from the main stream, the inputs-ready mode with no fork, and both with the
     statistics on a stream of their own, SDRG_PIPELINE_STATS_ASYNC)."""
     import torch
-    n, fs, B, F = 16384, 2_000_000, 256, 4
+    n, fs, B, F = 16384, 2_000_000, 256, 7  # 7 calls: the audio detector's energy-frame sets (3) wrap twice
     dev = torch.device("cuda:0")
     raws = [torch.from_numpy(np.stack([O.synth_frames(1, n, O.CS8, tone_hz=300.0 * (b % 13) - 1800.0, fs=fs,
                                                       seed=100 * f + b)[0] for b in range(B)])).to(dev)
