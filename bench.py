@@ -264,9 +264,11 @@ def main() -> int:
                     help="1: pipelined calls run their statistics on a stream of their own beside the next call's spectrum "
                          "(SDRG_PIPELINE_STATS_ASYNC; every stage of every call still runs); 0: after the spectrum on the "
                          "main stream; auto (default): 1 for the 65536-point configs[4] lines, whose four-step FFT leaves "
-                         "room beside it (measured 8 %% / 2 %% faster at 5 / 200 kHz), 0 for 16384 points, whose persistent "
-                         "spectrum kernel loses more to co-resident statistics than they gain (c2 0.18 vs 0.13 ms/step) "
-                         "and for N > 1 (the per-step gathers read the records on the main stream)")
+                         "room beside it (measured 8 %% / 2 %% faster at 5 / 200 kHz), and for the c3 step with the SSB "
+                         "stage, whose statistics then run beside the SSB pipeline and the next spectrum (1.2 %% faster); "
+                         "0 for FFT + statistics alone at 16384 points (configs[1]), whose persistent spectrum kernel "
+                         "loses more to co-resident statistics than they gain (0.148 vs 0.128 ms/step), and for N > 1 "
+                         "(the per-step gathers read the records on the main stream)")
     ap.add_argument("--process-group", action="store_true",
                     help="N = 1: start a one-rank torch.distributed group anyway (nccl = RCCL, or gloo with "
                          "--rehearse-gloo) and run the N > 1 code path -- per-step gathers on the engine's stream, "
@@ -427,7 +429,8 @@ def main() -> int:
     # the inputs are generated before the timed region and synchronised, so they are complete at every call
     pipelined = args.pipelined if not (gather_pcm and dist_on) else 0
     async_ok = bool(pipelined and not dist_on)
-    stats_async = async_ok and (args.stats_async == "1" or (args.stats_async == "auto" and c5))
+    with_ssb = args.stages == "all"
+    stats_async = async_ok and (args.stats_async == "1" or (args.stats_async == "auto" and (c5 or with_ssb)))
     pipe_mode = pipelined | (sdrg.PIPELINE_STATS_ASYNC if stats_async else 0)
     c5_mode = pipelined | (sdrg.PIPELINE_STATS_ASYNC if async_ok and args.stats_async != "0" else 0)
     if pipelined:
@@ -509,11 +512,11 @@ def main() -> int:
         ssb_iso_ms = eng.timing_stats()["ssb_ms"]
     d2d = d2d_copy_gbs(torch, dev)
 
-    def labelled_rate(st, k_steps, variant_on=False):
+    def labelled_rate(st, k_steps, variant_on=False, mode=None):
         """A separately labelled line measured in this same run: k_steps pipelined steps of stages st."""
         if variant_on:
             eng.set_ssb_variant(NCO_HZ, 127)
-        eng.set_pipelining(pipe_mode)
+        eng.set_pipelining(pipe_mode if mode is None else mode)
         for _ in range(3):
             step(st)
         eng.synchronize()
@@ -573,7 +576,11 @@ def main() -> int:
     labelled = {}
     if not dist_on and args.config == "c3" and args.stages == "all" and not variant and not args.no_labelled:
         eng.set_profiling(False)
-        labelled["configs1_fft_stats"] = dict(labelled_rate(sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS, args.steps),
+        # FFT + statistics alone: the statistics after the spectrum on one stream (--stats-async auto) unless forced
+        c1_mode = pipelined | (sdrg.PIPELINE_STATS_ASYNC if async_ok and args.stats_async == "1" else 0)
+        labelled["configs1_fft_stats"] = dict(labelled_rate(sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS, args.steps,
+                                                            mode=c1_mode),
+                                              stats_async=bool(c1_mode & sdrg.PIPELINE_STATS_ASYNC),
                                               workload="BASELINE configs[1]: same batch, FFT + |X|^2 + fftshift + "
                                                        "log-mag/peak/signal-strength stats, no SSB")
         labelled["configs2_nco127"] = dict(labelled_rate(sdrg.STAGE_ALL, args.steps, variant_on=True),

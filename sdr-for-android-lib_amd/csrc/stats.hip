@@ -874,10 +874,17 @@ __device__ float kth_smallest_wave(Visit visit, int k, int *hist, uint32_t *xch)
 // order once the scans are done (R > 0: pool values <= R per lane, held in registers for the select), or, for
 // pools beyond 24 x 64 values (R == 0), a pool region after them.  Small on purpose: beside the SSB pipeline
 // (84.5 KiB of LDS per CU) the frames that fit at once set the kernel's time.
+// Registers for eight waves per SIMD (<= 64 VGPRs; the 24-register pool variant six): the statistics of a pipelined
+// call then fit beside the next call's spectrum on every SIMD (its four waves hold 112 VGPRs each) instead of waiting
+// for its workgroups to retire.  The staging copy keeps NARROW_BATCH loads per lane in flight (16 needed 12 VGPRs
+// more than 64 allow and spilled).
+// Measured (tools/gpu_r4n.sh, alternating, one box): alone 27.2 vs 26.7 us per 4096 frames; the c3 step with the
+// statistics on their own stream 0.3077-0.3088 ms against 0.3121-0.3124 (76 VGPRs) and 0.3141 on the main stream.
+constexpr int NARROW_BATCH = 8;
 template <int R>
-__global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restrict__ spectra, StatsGeometry g,
-                                                            int64_t now_ms, StatsState *__restrict__ state,
-                                                            sdrg_frame_record *__restrict__ records) {
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(R > 8 ? 6 : 8))) void stats_narrow_kernel(
+    const float *__restrict__ spectra, StatsGeometry g, int64_t now_ms, StatsState *__restrict__ state,
+    sdrg_frame_record *__restrict__ records) {
     extern __shared__ __attribute__((aligned(16))) float stage[];
     __shared__ int sh_woff[12];
     __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
@@ -933,10 +940,10 @@ __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restr
 #pragma unroll
             for (int k = 0; k < 10; k++) wo[k] = (k < n_ref) ? sh_woff[k + 1] : 0x7fffffff;
             const int foff = sh_woff[n_ref];
-            for (int base = lane; base < stage_total; base += 16 * WAVE) {
-                float v[16];
+            for (int base = lane; base < stage_total; base += NARROW_BATCH * WAVE) {
+                float v[NARROW_BATCH];
 #pragma unroll
-                for (int u = 0; u < 16; u++) {
+                for (int u = 0; u < NARROW_BATCH; u++) {
                     const int i = base + WAVE * u;
                     int d = dl[0];
 #pragma unroll
@@ -944,7 +951,7 @@ __global__ __launch_bounds__(WAVE) void stats_narrow_kernel(const float *__restr
                     v[u] = (i < stage_total) ? P[i + d] : 0.0f;
                 }
 #pragma unroll
-                for (int u = 0; u < 16; u++) {
+                for (int u = 0; u < NARROW_BATCH; u++) {
                     const int i = base + WAVE * u;
                     if (i < stage_total) stage[i] = v[u];
                     // the focus window is the last: a lane sees its bins in increasing order, strict > keeps
