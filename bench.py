@@ -41,6 +41,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 ALG_BYTES_PER_SAMPLE = {"spectrum": 6.0}  # CS8: 2 B in + 4 B fftshifted float32 power out
 ISO_LAUNCHES = 30  # launches of the spectrum stage alone behind roofline_isolated
 N_INPUTS = 3  # distinct input batches rotated per step: 3 x 128 MiB > the 256 MiB Infinity Cache
+SSB_ISO_CALLS = 20  # joined SSB-only calls timed for ssb_latency_floor.ssb_ms_alone
 N_OUTPUTS = 3  # spectra / records buffers rotated per step (asynchronous statistics read a call's spectra late)
 # SSB floor: the sample-serial low-pass wave's own instruction issue.  Per sample it issues 6 VALU instructions
 # (the packed product of the previous output, 4 dependent adds, the packed product of the output before it) and
@@ -505,8 +506,10 @@ def main() -> int:
     spec_iso_ms = eng.timing_stats()["spectrum_ms"]
     ssb_iso_ms = None
     if args.stages == "all":  # the SSB stage alone (nothing else on the chip), for its latency-floor fraction
-        eng.reset_timing_stats()
-        for k in range(10):
+        for k in range(5 + SSB_ISO_CALLS):  # 5 untimed calls, then SSB_ISO_CALLS timed ones
+            if k == 5:
+                eng.synchronize()
+                eng.reset_timing_stats()
             eng.process_device(iqs[k % N_INPUTS].data_ptr(), fmt, sdrg.STAGE_SSB, None, None, pcm.data_ptr(), now[0])
         eng.synchronize()
         ssb_iso_ms = eng.timing_stats()["ssb_ms"]
