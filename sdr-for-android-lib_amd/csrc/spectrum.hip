@@ -402,9 +402,6 @@ template <int FMT>
 __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restrict__ iq, float *__restrict__ spectra,
                                                            const float *__restrict__ tabs, int n_frames) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-#ifdef SDRG_K16_PRIO  // lab: issue priority of the spectrum waves
-    __builtin_amdgcn_s_setprio(SDRG_K16_PRIO);
-#endif
     f2 *xch = reinterpret_cast<f2 *>(smem);
     f2 *p1 = reinterpret_cast<f2 *>(smem + XCH_F2 * 8);
     float4 *a2 = reinterpret_cast<float4 *>(smem + XCH_F2 * 8 + P1_F2 * 8);
