@@ -643,11 +643,12 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             int32_t rc = pulse_bank_audio_front(&e->audio_bank, sp.pcm_len, &af, e->s_ssb, ap_set);
             if (rc) return rc;
         }
-        HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_chunk_table, e->d_ssb, e->d_ssb_scratch, pcm,
-                           do_ap ? &af : nullptr, e->s_ssb));
         // the SSB stream's end marker: input release (the SSB pipeline, an iq reader, is done), join, timing, and
-        // the audio detector's start
-        HIP_TRY(hipEventRecord(mk_ssb_end, e->s_ssb));
+        // the audio detector's start -- completed by the pipeline kernel's own launch where launch_ssb can
+        bool end_recorded = false;
+        HIP_TRY(launch_ssb(iq, fmt, B, sp, e->d_taps, e->d_chunk_table, e->d_ssb, e->d_ssb_scratch, pcm,
+                           do_ap ? &af : nullptr, e->s_ssb, mk_ssb_end, &end_recorded));
+        if (!end_recorded) HIP_TRY(hipEventRecord(mk_ssb_end, e->s_ssb));
         if (do_ap) {
             HIP_TRY(hipStreamWaitEvent(e->s_ap, mk_ssb_end, 0));
             int32_t rc = pulse_bank_audio_detect(&e->audio_bank, e->audio_bank.d_out, e->s_ap, ap_set);

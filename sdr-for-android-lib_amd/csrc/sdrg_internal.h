@@ -95,9 +95,11 @@ void ssb_report_stamps();  // diagnostic (SDRG_PIPE_STAMPS=1)
 // completed in it} (host-computed, see engine.cpp); may be null (reference kernels).
 int ssb_pipe_chunk(void);
 // audio (nullable): run the audio pulse detector's front end on the PCM as it is produced
+// stop: an event the pipeline kernel may complete itself (*stop_recorded = true); otherwise the caller records it
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,
-                      const AudioFront *audio, hipStream_t stream);
+                      const AudioFront *audio, hipStream_t stream, hipEvent_t stop = nullptr,
+                      bool *stop_recorded = nullptr);
 
 // Pulse detectors (pulse.hip): one wavefront per stream.  Rings are [n_streams][cap] (cap = cap_mask + 1),
 // fh [n_streams][2][PULSE_FH_SLOTS].
