@@ -1197,7 +1197,11 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         if (audio) af = *audio;
         static const int prio_mask = [] {  // diagnostic override: SDRG_PIPE_PRIO = bit mask of high-priority waves
             const char *e = lab_getenv("SDRG_PIPE_PRIO");
-            return e ? (int)strtol(e, nullptr, 0) : 0x7;
+            // default: the three recurrences and the desired-level roles DES0-DES2 (one beside each recurrence's wave
+            // on its SIMD under DEFAULT_ROLE_MAP): c3 0.3061-0.3079 vs 0.3086-0.3104 ms per step with the recurrences
+            // alone (tools/gpu_r4v.sh, 4 alternating rounds, one box); all four DES roles 0.3066-0.3084, DES3 alone or
+            // the EQ role on top no better
+            return e ? (int)strtol(e, nullptr, 0) : 0x707;
         }();
         // role of hardware wave w = nibble w (wave w runs on SIMD w % 4); SDRG_PIPE_MAP overrides (diagnostic)
         static const unsigned long long role_map = [] {
