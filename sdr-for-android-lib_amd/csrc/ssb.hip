@@ -571,8 +571,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     const int ser_s = SDRG_SERIAL_LANES ? (((lane >> 4) << 2) | (lane & 3)) : my_s;
     const float demod_k = p.upper ? 2.0f : 0.0f;  // demodSSB(y, y) = y + y or y - y (:89-94) as y * k
     const bool serial_live = (wave < 3 || wave == W_EQ) && (lane < PG) && (s0 + lane < n_frames);
-    const bool high = (prio_mask >> wave) & 1;  // masks are per role  // default: the recurrences (waves 0-2) own their SIMD's issue slots
-    if (high) __builtin_amdgcn_s_setprio(2);
+    // issue priority per role: a bit mask of roles at priority 2, or (bit 31 set) two bits of priority level per role
+    const int prio_lvl = prio_mask < 0 ? (prio_mask >> (2 * wave)) & 3 : ((prio_mask >> wave) & 1) * 2;
+    const bool high = prio_lvl != 0;
+    if (prio_lvl == 1) __builtin_amdgcn_s_setprio(1);
+    else if (prio_lvl == 2) __builtin_amdgcn_s_setprio(2);
+    else if (prio_lvl == 3) __builtin_amdgcn_s_setprio(3);
     const size_t bps = bytes_per_sample<FMT>();
     const int n_live = min(p.n_in, S);
 
@@ -1197,11 +1201,11 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         if (audio) af = *audio;
         static const int prio_mask = [] {  // diagnostic override: SDRG_PIPE_PRIO = bit mask of high-priority waves
             const char *e = lab_getenv("SDRG_PIPE_PRIO");
-            // default: the three recurrences and the desired-level roles DES0-DES2 (one beside each recurrence's wave
-            // on its SIMD under DEFAULT_ROLE_MAP): c3 0.3061-0.3079 vs 0.3086-0.3104 ms per step with the recurrences
-            // alone (tools/gpu_r4v.sh, 4 alternating rounds, one box); all four DES roles 0.3066-0.3084, DES3 alone or
-            // the EQ role on top no better
-            return e ? (int)strtol(e, nullptr, 0) : 0x707;
+            // default: the three recurrences at priority 3 and the desired-level roles DES0-DES2 (one beside each
+            // recurrence's wave on its SIMD under DEFAULT_ROLE_MAP) at 2.  c3 per step (tools/gpu_r4v.sh, alternating
+            // rounds, one box): recurrences alone at 2 (0x7) 0.3086-0.3104 ms, + DES0-DES2 at 2 (0x707) 0.3049-0.3079,
+            // recurrences at 3 (0x802A003F) 0.3040-0.3059; all four DES roles as three; the other helpers at 1 0.319-0.326
+            return e ? (int)strtoul(e, nullptr, 0) : (int)0x802A003Fu;
         }();
         // role of hardware wave w = nibble w (wave w runs on SIMD w % 4); SDRG_PIPE_MAP overrides (diagnostic)
         static const unsigned long long role_map = [] {
