@@ -1201,11 +1201,12 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         if (audio) af = *audio;
         static const int prio_mask = [] {  // diagnostic override: SDRG_PIPE_PRIO = bit mask of high-priority waves
             const char *e = lab_getenv("SDRG_PIPE_PRIO");
-            // default: the three recurrences at priority 3 and the desired-level roles DES0-DES2 (one beside each
-            // recurrence's wave on its SIMD under DEFAULT_ROLE_MAP) at 2.  c3 per step (tools/gpu_r4v.sh, alternating
-            // rounds, one box): recurrences alone at 2 (0x7) 0.3086-0.3104 ms, + DES0-DES2 at 2 (0x707) 0.3049-0.3079,
-            // recurrences at 3 (0x802A003F) 0.3040-0.3059; all four DES roles as three; the other helpers at 1 0.319-0.326
-            return e ? (int)strtoul(e, nullptr, 0) : (int)0x802A003Fu;
+            // default: the three recurrences at priority 3, the desired-level roles DES0-DES2 (one beside each
+            // recurrence's wave on its SIMD under DEFAULT_ROLE_MAP) and the loader at 2.  c3 per step (tools/gpu_r4v.sh,
+            // alternating rounds, one box): recurrences alone at 2 (0x7) 0.3086-0.3104 ms, + DES0-DES2 at 2 (0x707)
+            // 0.3049-0.3079, recurrences at 3 (0x802A003F) 0.3031-0.3059, + the loader at 2 (0x802A00BF) 0.3018-0.3022
+            // (at 1 or 3: 0.3019-0.3039); all four DES roles as three; the other helpers at 1 0.319-0.326
+            return e ? (int)strtoul(e, nullptr, 0) : (int)0x802A00BFu;
         }();
         // role of hardware wave w = nibble w (wave w runs on SIMD w % 4); SDRG_PIPE_MAP overrides (diagnostic)
         static const unsigned long long role_map = [] {
