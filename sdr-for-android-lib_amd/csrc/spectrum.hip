@@ -661,7 +661,8 @@ __device__ __forceinline__ void tile_pass(f2 *lds, const f2 *t_hi, const f2 *t_l
 
 template <int LOG2N1, int LOG2N2, int FMT>
 __global__ __launch_bounds__(TILE_A) void four_step_a(const void *__restrict__ iq, f2 *__restrict__ Y,
-                                                       const f2 *__restrict__ tw) {
+                                                       const f2 *__restrict__ tw, int hi) {
+    if (hi) __builtin_amdgcn_s_setprio(1);  // see launch_four_step
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
     using TP = TilePlan<N1, TILE_A>;
     __shared__ __attribute__((aligned(16))) f2 lds[TP::C * TP::LP];
@@ -685,7 +686,8 @@ __global__ __launch_bounds__(TILE_A) void four_step_a(const void *__restrict__ i
 
 template <int LOG2N1, int LOG2N2>
 __global__ __launch_bounds__(TILE_B) void four_step_b(const f2 *__restrict__ Y, float *__restrict__ spectra,
-                                                       const f2 *__restrict__ tw) {
+                                                       const f2 *__restrict__ tw, int hi) {
+    if (hi) __builtin_amdgcn_s_setprio(1);
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
     using TP = TilePlan<N2, TILE_B>;
     __shared__ __attribute__((aligned(16))) f2 lds[TP::C * TP::LP];
@@ -732,7 +734,8 @@ __device__ __forceinline__ f2 convert_scaled(uint32_t v) {  // load_sample's val
 
 template <int LOG2N1, int LOG2N2, int FMT>
 __global__ __launch_bounds__(TILE_A) void four_step_a_p(const void *__restrict__ iq, f2 *__restrict__ Y,
-                                                         const f2 *__restrict__ tw, int n_frames) {
+                                                         const f2 *__restrict__ tw, int n_frames, int hi) {
+    if (hi) __builtin_amdgcn_s_setprio(1);
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
     using TP = TilePlan<N1, TILE_A>;
     constexpr int C = TP::C, R = TP::RA, TPF = N2 / C, NB = (C * N1 / R) / TILE_A, JS = TILE_A / C;
@@ -795,7 +798,8 @@ __global__ __launch_bounds__(TILE_A) void four_step_a_p(const void *__restrict__
 
 template <int LOG2N1, int LOG2N2>
 __global__ __launch_bounds__(TILE_B) void four_step_b_p(const f2 *__restrict__ Y, float *__restrict__ spectra,
-                                                         const f2 *__restrict__ tw, int n_frames) {
+                                                         const f2 *__restrict__ tw, int n_frames, int hi) {
+    if (hi) __builtin_amdgcn_s_setprio(1);
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
     using TP = TilePlan<N2, TILE_B>;
     constexpr int C = TP::C, TPF = N1 / C, S = C * N2 / TILE_B;
@@ -833,9 +837,13 @@ __global__ __launch_bounds__(TILE_B) void four_step_b_p(const f2 *__restrict__ Y
     }
 }
 
+// hi: the waves run at issue priority 1, above statistics that run beside them on a stream of their own (configs[4]
+// at 5 kHz: 0.3096-0.3113 vs 0.3127-0.3130 ms per step, 200 kHz unchanged, tools/gpu_r4y.sh); not beside the SSB
+// pipeline, whose helper roles at priority 0 would yield to them
 template <int LOG2N1, int LOG2N2, int FMT>
 hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, float *spectra, float *scratch,
-                            int wave, hipStream_t s, bool persistent) {
+                            int wave, hipStream_t s, bool persistent, bool hi_prio) {
+    const int hi = hi_prio ? 1 : 0;
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
     const f2 *tw = reinterpret_cast<const f2 *>(twf);
     f2 *Y = reinterpret_cast<f2 *>(scratch);
@@ -846,27 +854,27 @@ hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, floa
             const int cus = k16::device_cus();
             const int ta = nf * (N2 / TilePlan<N1, TILE_A>::C), tb = nf * (N1 / TilePlan<N2, TILE_B>::C);
             const int ga = ta < 2 * cus ? ta : 2 * cus, gb = tb < 4 * cus ? tb : 4 * cus;
-            hipLaunchKernelGGL((four_step_a_p<LOG2N1, LOG2N2, FMT>), dim3(ga), dim3(TILE_A), 0, s, src, Y, tw, nf);
+            hipLaunchKernelGGL((four_step_a_p<LOG2N1, LOG2N2, FMT>), dim3(ga), dim3(TILE_A), 0, s, src, Y, tw, nf, hi);
             hipLaunchKernelGGL((four_step_b_p<LOG2N1, LOG2N2>), dim3(gb), dim3(TILE_B), 0, s, Y, spectra + (size_t)f0 * N,
-                               tw, nf);
+                               tw, nf, hi);
             continue;
         }
         hipLaunchKernelGGL((four_step_a<LOG2N1, LOG2N2, FMT>), dim3(N2 / TilePlan<N1, TILE_A>::C, nf), dim3(TILE_A), 0,
-                           s, src, Y, tw);
+                           s, src, Y, tw, hi);
         hipLaunchKernelGGL((four_step_b<LOG2N1, LOG2N2>), dim3(N1 / TilePlan<N2, TILE_B>::C, nf), dim3(TILE_B), 0, s, Y,
-                           spectra + (size_t)f0 * N, tw);
+                           spectra + (size_t)f0 * N, tw, hi);
     }
     return hipGetLastError();
 }
 
 template <int LOG2N1, int LOG2N2>
 hipError_t launch_four_step_fmt(const void *iq, int fmt, int n_frames, const float *tw, float *spectra,
-                                float *scratch, int wave, hipStream_t s, bool pe) {
+                                float *scratch, int wave, hipStream_t s, bool pe, bool hi) {
     switch (fmt) {
-    case SDRG_IQ_CS8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS8>(iq, n_frames, tw, spectra, scratch, wave, s, pe);
-    case SDRG_IQ_CU8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CU8>(iq, n_frames, tw, spectra, scratch, wave, s, pe);
-    case SDRG_IQ_CS16: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS16>(iq, n_frames, tw, spectra, scratch, wave, s, pe);
-    case SDRG_IQ_CF32: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CF32>(iq, n_frames, tw, spectra, scratch, wave, s, pe);
+    case SDRG_IQ_CS8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS8>(iq, n_frames, tw, spectra, scratch, wave, s, pe, hi);
+    case SDRG_IQ_CU8: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CU8>(iq, n_frames, tw, spectra, scratch, wave, s, pe, hi);
+    case SDRG_IQ_CS16: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CS16>(iq, n_frames, tw, spectra, scratch, wave, s, pe, hi);
+    case SDRG_IQ_CF32: return launch_four_step<LOG2N1, LOG2N2, SDRG_IQ_CF32>(iq, n_frames, tw, spectra, scratch, wave, s, pe, hi);
     default: return hipErrorInvalidValue;
     }
 }
@@ -958,10 +966,10 @@ hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const f
     switch (n) {
     case 32768:
         return launch_four_step_fmt<7, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream,
-                                          !beside_wide_stats);
+                                          !beside_wide_stats, !beside_ssb);
     case 65536:
         return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream,
-                                          !beside_wide_stats);
+                                          !beside_wide_stats, !beside_ssb);
     case 16384: return k16::launch_fmt(iq, fmt, n_frames, twiddles + spectrum_k16_tables_offset(), spectra, stream,
                                       beside_ssb ? 1 : 2, n_cus);
     case 64: return launch_n<6>(iq, fmt, n_frames, twiddles, spectra, stream);
