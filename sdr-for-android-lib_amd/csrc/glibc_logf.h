@@ -165,6 +165,52 @@ SDRG_HD float log10f_posnormal(float x, const LogfEntry *tab) {
     return zz + c;
 }
 
+// The table folded with e_logf.c's k: for m in [0.5, 2), (int32)(bits(m) - OFF) >> 19 = kk * 16 + i with kk in
+// {-1, 0, 1}, so one 48-entry table indexed by that value + 16 holds 1/c and y0 = fma(kk, Ln2, log c) -- the same
+// double that log10f_posnormal computes per call, so the same bits, one conversion and one f64 fma fewer per log
+// (the wide statistics kernels, whose producers evaluate a log per reference-window bin).
+struct LogfFold {
+    double invc, y0;
+};
+constexpr int LOGF_FOLD_N = 48;
+SDRG_HD LogfFold logf_fold_entry(int idx, const LogfEntry *tab) {
+    const double Ln2 = 0x1.62e42fefa39efp-1;
+    const int j = idx - 16;
+    const LogfEntry e = tab[j & 15];
+    return LogfFold{e.invc, fma_d((double)(j >> 4), Ln2, e.logc)};
+}
+
+SDRG_HD float log10f_posnormal_fold(float x, const LogfFold *fold) {
+    const float ivln10 = 4.3429449201e-01f, log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
+    const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+    const int32_t hx = (int32_t)f2u(x);
+    const int32_t k = (hx >> 23) - 127;
+    const int32_t i = (int32_t)((uint32_t)k >> 31);
+    const uint32_t ix = (uint32_t)((hx & 0x007fffff) | ((0x7f - i) << 23));
+    const float y = (float)(k + i);
+    const uint32_t tmp = ix - 0x3f330000u;
+    const LogfFold f = fold[((int32_t)tmp >> 19) + 16];
+    const uint32_t iz = ix - (tmp & 0xff800000u);
+    const double z = (double)u2f(iz);
+    const double r = fma_d(z, f.invc, -1.0);
+    const double r2 = r * r;
+    double yy = fma_d(A1, r, A2);
+    yy = fma_d(A0, r2, yy);
+    yy = fma_d(yy, r2, f.y0 + r);
+    const float lnm = (float)yy;
+    const float a = y * log10_2lo;
+    const float b = ivln10 * lnm;
+    const float zz = a + b;
+    const float c = y * log10_2hi;
+    return zz + c;
+}
+
+SDRG_HD float log10f_fast_fold(float x, const LogfFold *fold) {
+    const uint32_t u = f2u(x);
+    if (__builtin_expect(u - 0x00800000u < 0x7f000000u, 1)) return log10f_posnormal_fold(x, fold);
+    return log10f_with(x, logf_table());
+}
+
 // log10f_with, branch-free for positive normal finite x (the common case), the general path otherwise
 SDRG_HD float log10f_fast(float x, const LogfEntry *tab) {
     const uint32_t u = f2u(x);

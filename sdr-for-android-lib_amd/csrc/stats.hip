@@ -54,6 +54,18 @@ __device__ __forceinline__ float db_of(float p) {  // refPower = 1
     return 10.0f * glibc::log10f_fast(p / 1.0f + 1e-20f, s_logf_tab);
 }
 
+// The same dB through the folded table (glibc_logf.h, log10f_posnormal_fold: the same bits, one conversion and one
+// f64 fma fewer per log): the wide kernels' per-bin logs (their producers and pooled gaps).  Loaded beside s_logf_tab
+// by load_logf_fold in those kernels only (the narrow kernel's LDS stays as it was: it shares CUs with the SSB
+// pipeline and the spectrum).
+__shared__ glibc::LogfFold s_logf_fold[glibc::LOGF_FOLD_N];
+__device__ __forceinline__ void load_logf_fold() {
+    if (threadIdx.x < glibc::LOGF_FOLD_N) s_logf_fold[threadIdx.x] = glibc::logf_fold_entry(threadIdx.x, glibc::logf_table());
+}
+__device__ __forceinline__ float db_fold(float p) {  // refPower = 1
+    return 10.0f * glibc::log10f_fast_fold(p / 1.0f + 1e-20f, s_logf_fold);
+}
+
 struct WinScan {
     float sum;       // sequential sum over [lo, hi]
     float best1k;    // best1kHzMean(lo, hi)
@@ -332,7 +344,7 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
                 const float v = va[k];
                 row[t] = v;
                 row[RS + t] = (e >= w) ? v - vb[k] : v;
-                const float d = db_of(v);
+                const float d = db_fold(v);
                 if (want_db) row[2 * RS + t] = in ? d : 0.0f;
                 // SDRG_WIDE_DBPOOL: the reference windows' dB values also go to the frame's pool scratch, where the
                 // pooled-gap pass reads the bottom window's instead of evaluating its logs again
@@ -1153,6 +1165,7 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
     const size_t frame = blockIdx.x;
     const int n_ref = g.n_ref;
     load_logf_tab();
+    load_logf_fold();
     // the window bounds are indexed by thread below: copy them out of the kernel arguments with constant
     // indices (a thread-indexed kernarg array would be copied to scratch)
 #pragma unroll
@@ -1276,7 +1289,7 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
                         }
 #pragma unroll
                         for (int r = 0; r < REG_POOL; r++) {
-                            v[r] = fabsf(db_of(v[r]) - m);
+                            v[r] = fabsf(db_fold(v[r]) - m);
                             __builtin_amdgcn_sched_barrier(0);  // one log10 at a time (register pressure)
                         }
                     }
@@ -1290,7 +1303,7 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
                         cnt / 2, hist, sh_xch);
                 } else {
 #pragma unroll 4
-                    for (int i = lo + lane; i <= hi; i += WG) pool[i - lo] = fabsf(db_of(P[i]) - m);
+                    for (int i = lo + lane; i <= hi; i += WG) pool[i - lo] = fabsf(db_fold(P[i]) - m);
                     __syncthreads();
                     STATS_STAMP(3);
                     med = kth_smallest_of<WG>(pool, cnt, cnt / 2, hist, sh_xch);
@@ -1303,7 +1316,7 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
 #pragma unroll 8
                     for (int i = lane; i < len; i += WG) {
                         const int q = cnt + i;
-                        if (q < g.max_pool) pool[q] = db_of(src[i]);
+                        if (q < g.max_pool) pool[q] = db_fold(src[i]);
                     }
                     cnt += len;
                 }
@@ -1451,6 +1464,7 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
     const int n_ref = g.n_ref, nwin = n_ref + 1, fq = n_ref;
     const int f0 = blockIdx.x * F;
     load_logf_tab();
+    load_logf_fold();
 #pragma unroll
     for (int i = 0; i < 10; i++) {
         if (tid == i) {
@@ -1575,7 +1589,7 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
                         }
                     }
                 } else if (want_db) {
-                    row[2 * RS + t] = in ? db_of(v) : 0.0f;
+                    row[2 * RS + t] = in ? db_fold(v) : 0.0f;
                 }
             }
             if (!SDRG_MW_ILP) __builtin_amdgcn_sched_barrier(0);  // one bin's log10 at a time
@@ -1784,7 +1798,7 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
         // differing bit of the real values and the select's prefix never matches them (no per-slot masks to keep)
 #pragma unroll
         for (int r = 0; r < REG; r++) {
-            v[r] = stid + GT * r < cnt ? fabsf(db_of(v[r]) - m) : __uint_as_float(0xffffffffu);
+            v[r] = stid + GT * r < cnt ? fabsf(db_fold(v[r]) - m) : __uint_as_float(0xffffffffu);
             if (!SDRG_MW_ILP) __builtin_amdgcn_sched_barrier(0);  // one log10 at a time
         }
         MW_STAMP(4);

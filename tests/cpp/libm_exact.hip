@@ -23,7 +23,10 @@ using sdrg::glibc::LogfEntry;
 
 __global__ void eval(uint32_t base, uint32_t count, float *out_ln, float *out_lg, unsigned long long *lds_bad) {
     __shared__ LogfEntry tab[16];
+    __shared__ sdrg::glibc::LogfFold fold[sdrg::glibc::LOGF_FOLD_N];
     if (threadIdx.x < 16) tab[threadIdx.x] = sdrg::glibc::logf_table()[threadIdx.x];
+    if (threadIdx.x < sdrg::glibc::LOGF_FOLD_N)
+        fold[threadIdx.x] = sdrg::glibc::logf_fold_entry(threadIdx.x, sdrg::glibc::logf_table());
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
@@ -34,7 +37,8 @@ __global__ void eval(uint32_t base, uint32_t count, float *out_ln, float *out_lg
     // the LDS-table instantiation must agree with the constant-table one bit for bit
     const int bad = (__float_as_uint(sdrg::glibc::logf_with(x, tab)) != __float_as_uint(ln)) +
                     (__float_as_uint(sdrg::glibc::log10f_with(x, tab)) != __float_as_uint(lg)) +
-                    (__float_as_uint(sdrg::glibc::log10f_fast(x, tab)) != __float_as_uint(lg));  // the stats' path
+                    (__float_as_uint(sdrg::glibc::log10f_fast(x, tab)) != __float_as_uint(lg)) +  // the stats' path
+                    (__float_as_uint(sdrg::glibc::log10f_fast_fold(x, fold)) != __float_as_uint(lg));  // wide stats
     if (bad) atomicAdd(lds_bad, (unsigned long long)bad);
 }
 
