@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 4: the wide multi-frame kernel's producer logs without a branch per bin (nb: a temporary patch, not kept -- every
+# slot's positive-normal log first, then one fix-up per chunk for negative / infinite / NaN powers)
+# against the product (base): the wide statistics GPU tests on nb, then stats alone (1024 x 65536, 200 kHz)
+# and the configs[4] 200 kHz line, alternating
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+D=sdr-for-android-lib_amd/lib
+SDRG_LIB_PATH=$D/libsdrg_nb.so timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+  tests/test_gpu_stats_exact.py tests/test_gpu_stats_geometry.py tests/test_gpu_libm_exact.py > gpurun_out/r4ze_tests.log 2>&1 || { tail -30 gpurun_out/r4ze_tests.log; exit 1; }
+tail -2 gpurun_out/r4ze_tests.log
+for i in 1 2 3; do
+  for v in base nb; do
+    echo "$v stats alone: $(SDRG_LIB_PATH=$D/libsdrg_$v.so timeout -k 10 120 python tools/lab/stats_time.py 65536 200 1024 30 2>/dev/null | tail -1)"
+    SDRG_LIB_PATH=$D/libsdrg_$v.so timeout -k 10 200 python bench.py --config c5 --focus 200 --steps 100 --warmup 20 --no-cpu-baseline > gpurun_out/r4ze.json 2>/dev/null || exit 1
+    echo "$v 200 kHz $(python3 -c "import json; d=json.load(open('gpurun_out/r4ze.json')); print(d['value'], d['ms_per_step'], d['kernel_ms'])")"
+  done
+done
