@@ -14,8 +14,11 @@ work (the per-stream filter state advances from step to step like a live receive
 `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts the N rank processes itself
 (torch.distributed.run as a child process, before anything touches a GPU) and exits with their status.
 With N > 1 every rank runs its own 4096 streams (weak scaling) and the per-frame records (+ focus-window
-spectra) of each step are gathered to rank 0 over RCCL; value = all ranks' samples / max-over-ranks time.  The
-full-spectra gather (the fftCallback payload) is timed after the timed region and reported separately.
+spectra) of each step are gathered to rank 0 by libsdrg.so's own RCCL ncclGather (sdrg_dist_create +
+sdrg_engine_gather, the C ABI a C/C++ host behind JNI calls; torch.distributed only carries the control plane:
+the communicator id, barriers and the max-over-ranks time, over gloo); value = all ranks' samples /
+max-over-ranks time.  The full-spectra gather (the fftCallback payload) is timed after the timed region and
+reported separately.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -248,9 +251,9 @@ def main() -> int:
                          "mixer at +250 kHz + 127-tap FIR (sdrg_engine_set_ssb_variant); a separately labelled line")
     ap.add_argument("--gather", default="records+focus", choices=["records", "records+pcm", "records+focus",
                                                                   "records+pcm+focus"],
-                    help="N > 1: what each step gathers to rank 0 over RCCL: the 72-B frame records (peak indices and "
-                         "statistics) and, by default, each frame's focus-window spectrum slice (sdrg.shard.gather_focus; "
-                         "BASELINE configs[3] gathers spectra + peak indices), optionally each frame's PCM (SURVEY 8e)")
+                    help="N > 1: what each step gathers to rank 0 over RCCL (sdrg_engine_gather): the 72-B frame records "
+                         "(peak indices and statistics) and, by default, each frame's focus-window spectrum slice "
+                         "(BASELINE configs[3] gathers spectra + peak indices), optionally each frame's PCM (SURVEY 8e)")
     ap.add_argument("--rehearse-gloo", action="store_true",
                     help="rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0, gloo backend, the gathers "
                          "staged through host memory (not a measurement)")
@@ -271,13 +274,9 @@ def main() -> int:
                          "loses more to co-resident statistics than they gain (0.148 vs 0.128 ms/step), and for N > 1 "
                          "(the per-step gathers read the records on the main stream)")
     ap.add_argument("--process-group", action="store_true",
-                    help="N = 1: start a one-rank torch.distributed group anyway (nccl = RCCL, or gloo with "
-                         "--rehearse-gloo) and run the N > 1 code path -- per-step gathers on the engine's stream, "
-                         "barriers, max-over-ranks timing, the full-spectra gather -- on the one GPU (a rehearsal line)")
-    ap.add_argument("--gather-mode", default="sync", choices=["sync", "async"],
-                    help="N > 1 (or --process-group): sync (default) makes the engine's stream wait for each step's "
-                         "gathers; async leaves them on RCCL's stream, overlapping the next step's kernels (rotated "
-                         "buffers, all complete inside the timed region)")
+                    help="N = 1: run the N > 1 code path anyway on the one GPU -- a one-rank RCCL communicator from the "
+                         "C ABI with the per-step gathers on the engine's stream, barriers, max-over-ranks timing, the "
+                         "full-spectra gather (a rehearsal line)")
     ap.add_argument("--launch-dry-run", action="store_true", help=argparse.SUPPRESS)
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
@@ -300,6 +299,10 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist_on = world > 1 or args.process_group  # a process group (one rank included): the N > 1 code path
     rehearse = args.rehearse_gloo and dist_on
+    # the data path of a real N > 1 run: libsdrg.so's own RCCL communicator and gathers (C ABI); torch.distributed
+    # (gloo) carries the control plane only.  --rehearse-gloo (every rank on cuda:0, where RCCL refuses two ranks on
+    # one device) gathers through sdrg.shard over gloo instead
+    capi = dist_on and not rehearse
     if dist_on and world == 1:  # a one-rank group started without torch.distributed.run
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
@@ -313,10 +316,8 @@ def main() -> int:
         return 3
     if rehearse:
         local = 0
+    if dist_on:
         dist.init_process_group("gloo")
-    elif dist_on:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     ranks_info = None
@@ -330,8 +331,9 @@ def main() -> int:
         every = [None] * world
         dist.all_gather_object(every, mine)
         distinct = len({e["uuid"] or (e["pci_bus_id"], e["device"]) for e in every}) == world
-        ranks_info = {"ranks_seen": dist.get_world_size(), "backend": dist.get_backend(),
-                      "distinct_devices": distinct,
+        ranks_info = {"ranks_seen": dist.get_world_size(),
+                      "backend": "rccl (sdrg_engine_gather, C ABI)" if capi else "gloo (sdrg.shard, host-staged)",
+                      "control_backend": dist.get_backend(), "distinct_devices": distinct,
                       "devices": [{k: v for k, v in e.items() if v not in (None, "")} for e in every]}
         if not rehearse and not distinct:
             log(f"bench: warning: ranks may share a GPU: {every}")
@@ -372,49 +374,45 @@ def main() -> int:
     # PCM travels as bytes: neither RCCL nor gloo has a 16-bit integer type
     p_out = torch.empty((world * streams, 2 * plen), dtype=torch.uint8, device=gdev) if gather_pcm and rank == 0 else None
     f_lo, f_n = sdrg.focus_window(FS, n, focus_khz)
-    # one focus staging buffer per rotated output buffer: an asynchronous gather may still read the last ones
-    f_stages = [torch.empty((streams, f_n), dtype=torch.float32, device=dev) for _ in range(N_OUTPUTS)] if focus else None
-    f_stage = f_stages[0] if focus else None
+    # host-staged focus slices of the gloo rehearsal (the C ABI packs them on the device itself)
+    f_stages = ([torch.empty((streams, f_n), dtype=torch.float32, device=dev) for _ in range(N_OUTPUTS)]
+                if focus and rehearse else None)
+    f_stage = f_stages[0] if f_stages else None
     f_out = torch.empty((world * streams, f_n), dtype=torch.float32, device=gdev) if focus and rank == 0 else None
     host = (lambda t: t.cpu()) if rehearse else (lambda t: t)
-    if dist_on:
-        # the engine enqueues on a torch stream that is current for the collectives too, so the RCCL gather is
-        # ordered after each step on the GPU without a host synchronisation, and the next step's kernels
-        # follow the gather (a real stream: the legacy default stream has no handle to pass)
+    dcomm = None
+    if capi:
+        # the communicator: rank 0's ncclGetUniqueId bytes to every rank over the control plane, then
+        # ncclCommInitRank inside libsdrg.so on this rank's GPU
+        uid = [sdrg.dist_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        dcomm = sdrg.Dist(uid[0], world, rank, device=local)
+        ranks_info["rccl_version"] = dcomm.info()["rccl_version"]
+    elif rehearse:
+        # the engine enqueues on a torch stream, so the host-staged gathers' copies follow each step's kernels
         work_stream = torch.cuda.Stream(dev)
         torch.cuda.set_stream(work_stream)
         eng.set_stream(work_stream.cuda_stream)
 
     calls = [0]
-    # RCCL gathers run asynchronously on RCCL's stream (after this step's kernels on the engine's stream): the next
-    # step's kernels do not wait for them.  A step's buffers (records, focus staging) are rotated over N_OUTPUTS, so
-    # before a step rewrites them it waits (on the GPU) for the gathers of the step that last used them
-    async_gather = dist_on and not rehearse and not gather_pcm and args.gather_mode == "async"
-    pending = []
 
-    def drain_gathers(keep: int) -> None:
-        while len(pending) > keep:
-            for w in pending.pop(0):
-                w.wait()
+    def ptr(t):
+        return t.data_ptr() if t is not None else None
 
     def step(st=None):
         nonlocal spec, rec, f_stage
-        if async_gather:
-            drain_gathers(N_OUTPUTS - 1)
         iq = iqs[calls[0] % N_INPUTS]
         spec, rec = specs[calls[0] % N_OUTPUTS], recs[calls[0] % N_OUTPUTS]
-        if focus:
+        if focus and f_stages is not None:
             f_stage = f_stages[calls[0] % N_OUTPUTS]
         calls[0] += 1
         eng.process_device(iq.data_ptr(), fmt, stages if st is None else st, spec.data_ptr(), rec.data_ptr(),
                            pcm.data_ptr(), now[0])
         now[0] += n // 2000  # frame duration in ms at 2 Msps (8 ms for 16384)
-        if async_gather:
-            ws = [shard.gather_records(rec, world, rank, dst=0, out=gathered, async_op=True)[1]]
-            if focus:
-                ws.append(shard.gather_focus(spec, f_lo, f_n, world, rank, dst=0, out=f_out, staging=f_stage,
-                                             async_op=True)[1])
-            pending.append([w for w in ws if w is not None])
+        if capi:  # one RCCL group on the engine's main stream, after this step's outputs
+            eng.gather(dcomm, 0, records=rec.data_ptr(), records_out=ptr(gathered),
+                       focus_spectra=spec.data_ptr() if focus else None, focus_out=ptr(f_out),
+                       pcm=pcm.data_ptr() if gather_pcm else None, pcm_out=ptr(p_out))
         elif dist_on:
             shard.gather_records(host(rec), world, rank, dst=0, out=gathered)  # records (peaks, stats) to rank 0
             if gather_pcm:
@@ -426,9 +424,10 @@ def main() -> int:
                 else:
                     shard.gather_focus(spec, f_lo, f_n, world, rank, dst=0, out=f_out, staging=f_stage)
 
-    # a pipelined call leaves its SSB stream running past the call, so a per-step PCM gather needs the joined schedule
-    # the inputs are generated before the timed region and synchronised, so they are complete at every call
-    pipelined = args.pipelined if not (gather_pcm and dist_on) else 0
+    # the inputs are generated before the timed region and synchronised, so they are complete at every call.  The
+    # host-staged rehearsal copies the PCM on the main stream, so its per-step PCM gather needs the joined schedule
+    # (sdrg_engine_gather orders a pipelined call's PCM itself)
+    pipelined = args.pipelined if not (gather_pcm and rehearse) else 0
     async_ok = bool(pipelined and not dist_on)
     with_ssb = args.stages == "all"
     stats_async = async_ok and (args.stats_async == "1" or (args.stats_async == "auto" and (c5 or with_ssb)))
@@ -445,12 +444,10 @@ def main() -> int:
         for _ in range(25):
             step()
         prewarm_steps += 25
-        drain_gathers(0)
         eng.synchronize()
     prewarm_ms = (time.perf_counter() - t_pre) * 1e3
     for _ in range(args.warmup):
         step()
-    drain_gathers(0)
     eng.synchronize()
     torch.cuda.synchronize()
     eng.reset_timing_stats()
@@ -460,8 +457,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    drain_gathers(0)  # every step's gathers complete inside the timed region
-    eng.synchronize()
+    eng.synchronize()  # every step's gathers (on the engine's main stream) complete inside the timed region
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -472,15 +468,24 @@ def main() -> int:
         eng.synchronize()
         s_out = torch.empty((world * streams, n), dtype=torch.float32, device=gdev) if rank == 0 else None
         s_src = host(spec)
-        shard.gather_spectra(s_src, world, rank, dst=0, out=s_out)  # untimed first gather
+
+        def gather_spectra():
+            if capi:
+                eng.gather(dcomm, 0, spectra=s_src.data_ptr(), spectra_out=ptr(s_out))
+            else:
+                shard.gather_spectra(s_src, world, rank, dst=0, out=s_out)
+
+        gather_spectra()  # untimed first gather
+        eng.synchronize()
         torch.cuda.synchronize()
         dist.barrier()
         tg = time.perf_counter()
         for _ in range(args.spectra_gather_steps):
-            shard.gather_spectra(s_src, world, rank, dst=0, out=s_out)
+            gather_spectra()
+        eng.synchronize()
         torch.cuda.synchronize()
         dist.barrier()
-        tgt = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=gdev)
+        tgt = torch.tensor([time.perf_counter() - tg], dtype=torch.float64)
         dist.all_reduce(tgt, op=dist.ReduceOp.MAX)
         g_ms = float(tgt.item()) / args.spectra_gather_steps * 1e3
         into0 = (world - 1) * streams * n * 4
@@ -491,8 +496,13 @@ def main() -> int:
                                   "payload, SURVEY 8e), after the timed region; not part of value"}
         del s_out
     # every rank hashes what it contributed to the last step's gathers; rank 0 checks its gathered blocks (any backend)
-    rehearsal_check = rehearsal_verify(torch, dist, world, rank, streams, rec, f_stage, pcm, gather_pcm, gathered, f_out,
-                                       p_out) if dist_on else None
+    if dist_on:
+        eng.synchronize()
+        f_mine = (f_stage if rehearse else spec[:, f_lo:f_lo + f_n].contiguous()) if focus else None
+        rehearsal_check = rehearsal_verify(torch, dist, world, rank, streams, rec, f_mine, pcm, gather_pcm, gathered,
+                                           f_out, p_out)
+    else:
+        rehearsal_check = None
     ts = eng.timing_stats()
     # the spectrum kernel alone (no SSB sharing the chip), a few launches after the timed region: its
     # isolated HBM rate, reported beside the timed-region one
@@ -516,21 +526,31 @@ def main() -> int:
     d2d = d2d_copy_gbs(torch, dev)
 
     def labelled_rate(st, k_steps, variant_on=False, mode=None):
-        """A separately labelled line measured in this same run: k_steps pipelined steps of stages st."""
+        """A separately labelled line measured in this same run: k_steps pipelined steps of stages st, with the
+        per-kernel times of those steps (HIP events on each kernel's stream, as kernel_ms), so a change of the line
+        between two records can be attributed to a kernel."""
         if variant_on:
             eng.set_ssb_variant(NCO_HZ, 127)
         eng.set_pipelining(pipe_mode if mode is None else mode)
+        eng.set_profiling(True)
         for _ in range(3):
             step(st)
         eng.synchronize()
+        eng.reset_timing_stats()
         t1 = time.perf_counter()
         for _ in range(k_steps):
             step(st)
         eng.synchronize()
         dt = time.perf_counter() - t1
+        tm = eng.timing_stats()
+        eng.set_profiling(False)
         if variant_on:
             eng.set_ssb_variant(0.0, 0)
-        return {"value": round(k_steps * streams * n / dt / 1e6, 2), "ms_per_step": round(dt / k_steps * 1e3, 4)}
+        r = {"value": round(k_steps * streams * n / dt / 1e6, 2), "ms_per_step": round(dt / k_steps * 1e3, 4),
+             "spectrum_ms": round(tm["spectrum_ms"], 4), "stats_ms": round(tm["stats_ms"], 4)}
+        if st & sdrg.STAGE_SSB:
+            r["ssb_ms"] = round(tm["ssb_ms"], 4)
+        return r
 
     def c5_line(focus_c5: int, k_steps: int) -> dict:
         """BASELINE configs[4] in this same run: 1024 streams x 65536-pt CS16 frames, FFT + |X|^2 + fftshift + stats
@@ -586,6 +606,12 @@ def main() -> int:
                                               stats_async=bool(c1_mode & sdrg.PIPELINE_STATS_ASYNC),
                                               workload="BASELINE configs[1]: same batch, FFT + |X|^2 + fftshift + "
                                                        "log-mag/peak/signal-strength stats, no SSB")
+        if async_ok:  # the other statistics schedule of the same line, measured right after it (an A/B in the record)
+            alt = pipelined | (0 if c1_mode & sdrg.PIPELINE_STATS_ASYNC else sdrg.PIPELINE_STATS_ASYNC)
+            labelled["configs1_fft_stats_other_schedule"] = dict(
+                labelled_rate(sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS, args.steps, mode=alt),
+                stats_async=bool(alt & sdrg.PIPELINE_STATS_ASYNC),
+                note="configs1_fft_stats with the statistics schedule flipped (--stats-async), not the line's choice")
         labelled["configs2_nco127"] = dict(labelled_rate(sdrg.STAGE_ALL, args.steps, variant_on=True),
                                            workload="BASELINE configs[2] as written (a build extension, not the "
                                                     f"reference chain): SSB with an NCO mixer at +{NCO_HZ / 1e3:g} kHz "
@@ -593,7 +619,7 @@ def main() -> int:
         labelled["configs4_c5_5khz"] = c5_line(5, args.steps)
         labelled["configs4_c5_200khz"] = c5_line(200, args.steps)
     if dist_on:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -639,8 +665,8 @@ def main() -> int:
                    "streams_per_gpu": streams, "samples_per_frame": n, "sample_rate": FS, "format": fmt_name,
                    "focus_khz": focus_khz,
                    "parallelism": f"streams sharded {streams}/GPU x {world} GPU(s)" + (
-                       (", RCCL gather of records" + (" + PCM" if gather_pcm else "")
-                        + (f" + {f_n}-bin focus spectra" if focus else ""))
+                       ((", RCCL gather (sdrg_engine_gather) of records" if capi else ", gloo gather of records")
+                        + (" + PCM" if gather_pcm else "") + (f" + {f_n}-bin focus spectra" if focus else ""))
                        if dist_on else "")},
         "kernel_ms": {k: round(v, 4) for k, v in ts.items() if k != "count"},
         "roofline": {"kernel": f"{kname} (unpack+FFT+|X|^2+fftshift)", "bound": "hbm",
@@ -689,9 +715,9 @@ def main() -> int:
     if ranks_info:
         out.update(ranks_info)
     if dist_on:
-        out["gather_mode"] = ("asynchronous: each step's RCCL gathers run on RCCL's stream after that step's kernels, "
-                              f"{N_OUTPUTS} rotated record / focus buffers, all complete inside the timed region"
-                              if async_gather else "synchronous: the engine's stream waits for each step's gathers")
+        out["gather_mode"] = ("sdrg_engine_gather: one RCCL group per step on the engine's main stream after the step's "
+                              "outputs (no host synchronisation); the next step's kernels follow it" if capi else
+                              "host-staged gloo gathers (rehearsal)")
     if spectra_gather:
         out["spectra_gather"] = spectra_gather
     if ssb_iso_ms:
@@ -722,8 +748,9 @@ def main() -> int:
                 "note": "the longest kernel by GPU time, measured co-resident in the timed region; it is bound by the "
                         "sample-serial recurrences (ssb_latency_floor), not by HBM: IQ in (I used) + PCM out"}
     if args.stages == "all" and ts["ssb_ms"] > 0:
-        # the kernel with the most GPU time per step, against HBM: pipelined, the SSB stream (the pipeline kernel and
-        # the audio detector) and the main stream (spectrum, statistics, spectral detector) each fill the step
+        # the kernel with the most GPU time per step, against HBM: pipelined, the SSB stream (the pipeline kernel; the
+        # audio detector runs on a stream of its own, s_ap) and the main stream (spectrum, statistics, spectral
+        # detector) each fill the step
         cand = {"ssb_pipe_kernel": (ts["ssb_ms"], streams * n * in_bps + streams * 2 * plen),
                 "spectrum16k_kernel" if not c5 else "four_step_a + four_step_b": (spec_ms, alg_bytes),
                 "stats_kernel": (ts["stats_ms"], None)}
@@ -759,6 +786,8 @@ def main() -> int:
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)
     eng.close()
+    if dcomm is not None:
+        dcomm.close()
     if dist_on:
         dist.destroy_process_group()
     return 0

@@ -25,6 +25,7 @@
 #ifndef SDRG_H
 #define SDRG_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -135,10 +136,14 @@ typedef struct sdrg_callbacks {
 
 /* Per-kernel device times of the last process call, from hipEvents recorded on the stream each
  * kernel was launched on (only filled while profiling is enabled).  Pipelined, the SSB chain's start marker
- * would sit on the SSB stream, the step's critical path, so only the first call after a reset of the timing
- * statistics carries one; every later pipelined call's ssb_ms is its SSB stream time, from the previous call's
- * SSB end marker to its own (the chain's kernels + the launch gaps between them; the stream idles in between only
- * if the host falls behind).  The audio pulse detector runs after the chain on a stream of its own. */
+ * would sit on the SSB stream, the step's critical path, so a pipelined call carries one only when the call before
+ * it was not a profiled SSB call (the first call after a reset of the timing statistics, after profiling was
+ * re-enabled, or after an unprofiled call); every other pipelined call's ssb_ms is the interval from the previous
+ * call's SSB end marker to its own.  That interval is the SSB chain's own time (its kernels + the launch gaps
+ * between them) in SDRG_PIPELINE_INPUTS_READY mode with the host keeping ahead of the GPU.  In SDRG_PIPELINE_ON
+ * mode each call's SSB stream first waits for the call's start marker on the main stream, so the interval also
+ * holds that wait (the step period rather than the chain), and in any mode it holds the time the host spends
+ * blocked between two calls.  The audio pulse detector runs after the chain on a stream of its own. */
 typedef struct sdrg_timings {
     float spectrum_ms;   /* unpack + FFT + |X|^2 + fftshift kernel */
     float stats_ms;      /* end of the spectrum -> end of the signal-strength kernel (+ spectral pulse detector when
@@ -474,6 +479,65 @@ int32_t sdrg_engine_get_timings(const sdrg_engine *eng, sdrg_timings *out);
 /* Mean timings over every profiled call since the last reset (waits for them); *count = calls averaged. */
 int32_t sdrg_engine_get_timing_stats(const sdrg_engine *eng, sdrg_timings *mean, int32_t *count);
 int32_t sdrg_engine_reset_timing_stats(sdrg_engine *eng);
+
+/* ------------------------------------------------------------------------------------------------
+ * Multi-GPU: one process per GPU (rank), each with its own engine for its block of streams (rank r owns the
+ * global streams [r*B, (r+1)*B): frames and per-stream state are independent, so nothing else is exchanged), and
+ * the per-frame results gathered to a root rank with RCCL (ncclGather over xGMI).  The reference is one receiver
+ * in one process; what is gathered is what its soapyCallback hands to Kotlin per frame
+ * (sdr-bridge-java-soapy.cpp:456-466: the fftCallback spectrum, the getters' values with the peak) and the SSB
+ * worker's PCM (ssb_processor.cpp:103-108).  RCCL is loaded at run time (librccl.so.1) by the first call below;
+ * without it they return SDRG_E_UNSUPPORTED and nothing else is affected.
+ * ---------------------------------------------------------------------------------------------- */
+#define SDRG_DIST_ID_BYTES 128
+typedef struct sdrg_dist sdrg_dist;
+/* ncclGetUniqueId, on one rank: the caller hands these bytes to every rank (a file, a socket, MPI, ...). */
+int32_t sdrg_dist_unique_id(void *id, int32_t bytes);
+/* ncclCommInitRank on `device` (collective: every rank of the job calls it with the same id). */
+int32_t sdrg_dist_create(const void *id, int32_t world_size, int32_t rank, int32_t device, sdrg_dist **out);
+int32_t sdrg_dist_destroy(sdrg_dist *d);
+/* Rank, world size and the RCCL version in use (any pointer may be NULL). */
+int32_t sdrg_dist_info(const sdrg_dist *d, int32_t *rank, int32_t *world_size, int32_t *rccl_version);
+
+/* What one gather moves.  Each selected pair gathers this rank's n_streams rows to the root's output, which
+ * holds world_size x n_streams rows in rank order (= global stream order); the *_out pointers are read on the
+ * root only (NULL elsewhere).  A NULL source skips the pair; every rank selects the same pairs.  All device memory
+ * of the engine's device.
+ *   records       [n_streams] sdrg_frame_record  -> records_out [world][n_streams]
+ *   focus_spectra [n_streams][N] (a call's spectra) -> focus_out [world][n_streams][n_bins]: each frame's focus
+ *                 window (sdrg_focus_window of the statistics' configuration), packed on the device first
+ *   spectra       [n_streams][N]                 -> spectra_out [world][n_streams][N]: the whole fftshifted spectra
+ *                 (268 MB per rank at 4096 x 16384)
+ *   pcm           [n_streams][pcm_len] int16     -> pcm_out [world][n_streams][pcm_len] */
+typedef struct sdrg_gather_buffers {
+    const sdrg_frame_record *records;
+    sdrg_frame_record *records_out;
+    const float *focus_spectra;  /* the focus-window slices of these spectra */
+    float *focus_out;
+    const float *spectra;        /* the whole spectra */
+    float *spectra_out;
+    const int16_t *pcm;
+    int16_t *pcm_out;
+} sdrg_gather_buffers;
+/* Enqueue the gathers (one RCCL group) on the engine's main stream after the last process call's outputs they read
+ * (records of asynchronous statistics and the PCM of a pipelined call included): no host synchronisation, and the
+ * engine's next call cannot overwrite a gathered buffer before the gather has read it.  Every rank calls it with the
+ * same selection.  Complete after sdrg_engine_synchronize (or on a stream after sdrg_engine_wait_outputs). */
+int32_t sdrg_engine_gather(sdrg_engine *eng, sdrg_dist *d, int32_t root, const sdrg_gather_buffers *bufs);
+/* Single-pair forms of sdrg_engine_gather. */
+int32_t sdrg_engine_gather_records(sdrg_engine *eng, sdrg_dist *d, int32_t root, const sdrg_frame_record *records,
+                                   sdrg_frame_record *records_out);
+int32_t sdrg_engine_gather_focus(sdrg_engine *eng, sdrg_dist *d, int32_t root, const float *spectra, float *focus_out);
+int32_t sdrg_engine_gather_spectra(sdrg_engine *eng, sdrg_dist *d, int32_t root, const float *spectra,
+                                   float *spectra_out);
+int32_t sdrg_engine_gather_pcm(sdrg_engine *eng, sdrg_dist *d, int32_t root, const int16_t *pcm, int16_t *pcm_out);
+
+/* Device memory for a host that has no other GPU allocator (the C/C++ side of the JNI boundary): hipMalloc /
+ * hipFree on `device`, and a synchronous copy in any direction (hipMemcpyDefault; it is not ordered with the
+ * engine's streams -- call sdrg_engine_synchronize before reading an engine output back). */
+int32_t sdrg_device_alloc(int32_t device, size_t bytes, void **out);
+int32_t sdrg_device_free(int32_t device, void *p);
+int32_t sdrg_memcpy(int32_t device, void *dst, const void *src, size_t bytes);
 
 #ifdef __cplusplus
 }

@@ -124,7 +124,7 @@ struct EvSet {
     hipEvent_t t0 = nullptr, spec = nullptr, stats = nullptr, ssb0 = nullptr, ssb1 = nullptr, end = nullptr;
     bool has_spec = false, has_stats = false, has_ssb = false, pending = false;
     bool ssb_timed = false;  // ssb0 recorded: this call's SSB duration is measured from its own start marker
-    int64_t seq = -1;        // the call's number among profiled calls (pipelined SSB: interval to call seq - 1)
+    int64_t seq = -1;        // the call's number among ALL calls (pipelined SSB: interval to call seq - 1, if profiled)
     bool stats_marked = false;  // `stats` recorded after the statistics (joined calls, whose `end` follows the join)
 };
 
@@ -162,8 +162,8 @@ struct sdrg_engine {
     sdrg_timings last_timings{};
     double sum_spec = 0, sum_stats = 0, sum_ssb = 0, sum_total = 0;
     int n_acc = 0, n_ssb = 0;
-    int64_t calls_profiled = 0;
-    int64_t seq_reset = 0;  // seq of the first profiled call after the last reset of the timing statistics
+    int64_t calls_total = 0;  // every enqueue, profiled or not: two calls are consecutive only if their seqs are
+    int64_t seq_reset = 0;    // seq of the first call after the last reset of the timing statistics
 
     // device state / buffers
     StatsState *d_stats = nullptr;
@@ -177,6 +177,12 @@ struct sdrg_engine {
     size_t ssb_scratch_elems = 0;
     float *d_spec_scratch = nullptr;
     size_t spec_scratch_elems = 0;
+    float *d_focus_stage = nullptr;   // sdrg_engine_gather: the focus-window slices, packed for ncclGather
+    size_t focus_stage_elems = 0;
+    // sdrg_engine_gather of a call's PCM: the next call's SSB stage (which does not follow the main stream when
+    // pipelined) waits for the gather before it overwrites the buffer
+    hipEvent_t ev_gather = nullptr;
+    bool gather_pending_ssb = false;
     float *d_fft_scratch = nullptr;   // four-step intermediate (N > 16384)
     size_t fft_scratch_elems = 0;
     sdrg_frame_record *d_rec_scratch = nullptr;
@@ -556,6 +562,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     }
 
     const bool prof = e->profiling;
+    const int64_t seq = e->calls_total++;
     EvSet *ev = nullptr;
     if (prof) {
         const int slot = e->ring_next;
@@ -574,14 +581,16 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         ev->has_stats = do_stats;
         ev->has_ssb = do_ssb;
         // the SSB start marker sits on the SSB stream between the fork and the pipeline; pipelined, that stream is
-        // the step's critical path, so only the first call of a timing window carries one: every later call's SSB
-        // time is measured from the previous call's SSB end marker to its own (fold_slot)
-        ev->ssb_timed = do_ssb && (!(e->pipelined && !join) || e->calls_profiled == e->seq_reset);
-        ev->seq = e->calls_profiled;
+        // the step's critical path, so a call carries one only when its SSB time cannot be measured from the previous
+        // call's SSB end marker to its own (fold_slot): the previous call (seq - 1, every enqueue counts) was not a
+        // profiled SSB call of this timing window
+        const EvSet &pv = e->ring[(slot + sdrg_engine::RING - 1) % sdrg_engine::RING];
+        const bool chained = pv.seq == seq - 1 && pv.has_ssb && seq > e->seq_reset;
+        ev->ssb_timed = do_ssb && (!(e->pipelined && !join) || !chained);
+        ev->seq = seq;
         // a joined call's end marker follows the wait for the SSB stream, and asynchronous statistics end on a
         // stream of their own: the statistics get a marker of their own
         ev->stats_marked = do_stats && (!(e->pipelined && !join) || e->stats_async);
-        e->calls_profiled++;
     }
     // Markers: every event recorded between two kernels of a stream costs that stream a gap (several us
     // measured), so a call records at most one at its start on the main stream (the SSB fork and the timing
@@ -632,7 +641,10 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         if (!early_fork) {
             HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
             HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
+        } else if (e->gather_pending_ssb) {  // the last call's PCM is being gathered on the main stream
+            HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_gather, 0));
         }
+        e->gather_pending_ssb = false;
         if (prof && ev->ssb_timed) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
         // AudioPulseDetector::process(pcm) after processSSB_opt (ssb_processor.cpp:109): its per-sample front
         // end runs inside the SSB kernel on the PCM it produces, the detector right after
@@ -885,15 +897,16 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (e->s_ap) (void)hipStreamSynchronize(e->s_ap);
     e->spec_bank.last_stream = e->audio_bank.last_stream = nullptr;  // drained above
     e->spec_bank.detect_stream = e->audio_bank.detect_stream = nullptr;
-    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_nco_tab, e->d_chunk_table, e->d_ssb_scratch, e->d_spec_scratch, e->d_fft_scratch, e->d_pool,
-                    e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage, e->d_ss_stage, e->d_rec_stage, e->d_pcm_stage};
+    void *bufs[] = {e->d_stats, e->d_ssb, e->d_twiddles, e->d_taps, e->d_nco_tab, e->d_chunk_table, e->d_ssb_scratch,
+                    e->d_spec_scratch, e->d_fft_scratch, e->d_pool, e->d_rec_scratch, e->d_iq_stage, e->d_spec_stage,
+                    e->d_ss_stage, e->d_rec_stage, e->d_pcm_stage, e->d_focus_stage};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (e->s_spec) (void)hipStreamSynchronize(e->s_spec);
     for (hipEvent_t ev : e->ev_stats_end)
         if (ev) (void)hipEventDestroy(ev);
     hipEvent_t evs[] = {e->ev_fork, e->ev_join, e->ev_in_main, e->ev_in_ssb, e->ev_fork_spec, e->ev_join_spec,
-                        e->ev_spec_done, e->ev_ap_end[0], e->ev_ap_end[1], e->ev_ap_end[2]};
+                        e->ev_spec_done, e->ev_ap_end[0], e->ev_ap_end[1], e->ev_ap_end[2], e->ev_gather};
     for (hipEvent_t ev : evs)
         if (ev) (void)hipEventDestroy(ev);
     for (auto &r : e->ring) {
@@ -1317,6 +1330,8 @@ int32_t sdrg_engine_set_profiling(sdrg_engine *e, int32_t enabled) {
         }
         e->ring_created = true;
     }
+    // calls made while profiling was off break the chain of SSB end markers (their seqs are not profiled), so the first
+    // profiled call after re-enabling takes a start marker of its own (enqueue's `chained`)
     e->profiling = enabled != 0;
     return SDRG_OK;
 }
@@ -1345,6 +1360,93 @@ int32_t sdrg_engine_get_timing_stats(const sdrg_engine *ce, sdrg_timings *mean, 
     return SDRG_OK;
 }
 
+// Multi-GPU gather (include/sdrg.h; dist.cpp holds RCCL): the gathers go on the main stream after the outputs they
+// read -- the statistics' stream's last event for records of asynchronous statistics, the SSB stream's end marker for
+// PCM -- so the next call's spectrum and statistics (main stream, or forked from it) follow them; the next call's
+// SSB stage, which a pipelined call does not fork from the main stream, waits for ev_gather when PCM was gathered.
+int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdrg_gather_buffers *b) {
+    if (!e || !d || !b) return fail(SDRG_E_INVALID, "null argument");
+    if (dist_device(d) != e->device)
+        return fail(SDRG_E_INVALID, "communicator on device %d, engine on device %d", dist_device(d), e->device);
+    if (root < 0 || root >= dist_world(d)) return fail(SDRG_E_INVALID, "root %d outside [0, %d)", root, dist_world(d));
+    DeviceScope dscope(e->device);
+    HIP_TRY(dscope.error());
+    const bool at_root = dist_rank(d) == root;
+    const size_t B = (size_t)e->n_streams;
+    const int n = e->cfg.samples_per_reading;
+    hipStream_t s = e->s_main;
+    GatherItem items[4];
+    int k = 0;
+    if (b->records) {
+        if (at_root && !b->records_out) return fail(SDRG_E_INVALID, "null records_out on the root");
+        if (e->stats_async && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));
+        items[k++] = {b->records, b->records_out, B * sizeof(sdrg_frame_record)};
+    }
+    if (b->focus_spectra) {
+        if (at_root && !b->focus_out) return fail(SDRG_E_INVALID, "null focus_out on the root");
+        const StatsGeometry g = stats_geometry(e->fft_fs, e->fft_fc, n, e->fft_focus);
+        if (g.focus_len <= 0) return fail(SDRG_E_INVALID, "the focus window is empty (focus wider than the band)");
+        int32_t rc = ensure_device(&e->d_focus_stage, &e->focus_stage_elems, B * (size_t)g.focus_len);
+        if (rc) return rc;
+        HIP_TRY(launch_focus_pack(b->focus_spectra, (int)B, n, g.focus_lo, g.focus_len, e->d_focus_stage, s));
+        items[k++] = {e->d_focus_stage, b->focus_out, B * (size_t)g.focus_len * sizeof(float)};
+    }
+    if (b->spectra) {
+        if (at_root && !b->spectra_out) return fail(SDRG_E_INVALID, "null spectra_out on the root");
+        items[k++] = {b->spectra, b->spectra_out, B * (size_t)n * sizeof(float)};
+    }
+    const int plen = ssb_pcm_len(ssb_frozen_or(e), (uint32_t)e->cfg.sample_rate, e->fir_taps);
+    if (b->pcm && plen > 0) {
+        if (at_root && !b->pcm_out) return fail(SDRG_E_INVALID, "null pcm_out on the root");
+        if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
+        items[k++] = {b->pcm, b->pcm_out, B * (size_t)plen * sizeof(int16_t)};
+    }
+    if (k == 0) return SDRG_OK;
+    int32_t rc = dist_gather(d, items, k, root, s);
+    if (rc) return rc;
+    if (b->pcm && plen > 0) {
+        if (!e->ev_gather)
+            HIP_TRY(hipEventCreateWithFlags(&e->ev_gather, hipEventDisableTiming | hipEventDisableSystemFence));
+        HIP_TRY(hipEventRecord(e->ev_gather, s));
+        e->gather_pending_ssb = true;
+    }
+    return SDRG_OK;
+}
+
+int32_t sdrg_engine_gather_records(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdrg_frame_record *records,
+                                   sdrg_frame_record *records_out) {
+    if (!records) return fail(SDRG_E_INVALID, "null records");
+    sdrg_gather_buffers b{};
+    b.records = records;
+    b.records_out = records_out;
+    return sdrg_engine_gather(e, d, root, &b);
+}
+
+int32_t sdrg_engine_gather_focus(sdrg_engine *e, sdrg_dist *d, int32_t root, const float *spectra, float *focus_out) {
+    if (!spectra) return fail(SDRG_E_INVALID, "null spectra");
+    sdrg_gather_buffers b{};
+    b.focus_spectra = spectra;
+    b.focus_out = focus_out;
+    return sdrg_engine_gather(e, d, root, &b);
+}
+
+int32_t sdrg_engine_gather_spectra(sdrg_engine *e, sdrg_dist *d, int32_t root, const float *spectra,
+                                   float *spectra_out) {
+    if (!spectra) return fail(SDRG_E_INVALID, "null spectra");
+    sdrg_gather_buffers b{};
+    b.spectra = spectra;
+    b.spectra_out = spectra_out;
+    return sdrg_engine_gather(e, d, root, &b);
+}
+
+int32_t sdrg_engine_gather_pcm(sdrg_engine *e, sdrg_dist *d, int32_t root, const int16_t *pcm, int16_t *pcm_out) {
+    if (!pcm) return fail(SDRG_E_INVALID, "null pcm");
+    sdrg_gather_buffers b{};
+    b.pcm = pcm;
+    b.pcm_out = pcm_out;
+    return sdrg_engine_gather(e, d, root, &b);
+}
+
 int32_t sdrg_engine_reset_timing_stats(sdrg_engine *e) {
     if (!e) return fail(SDRG_E_INVALID, "null engine");
     int32_t rc = fold_all(e);
@@ -1352,7 +1454,7 @@ int32_t sdrg_engine_reset_timing_stats(sdrg_engine *e) {
     e->sum_spec = e->sum_stats = e->sum_ssb = e->sum_total = 0;
     e->n_acc = e->n_ssb = 0;
     // a pipelined call's SSB interval starts at the previous call's end marker: the window's first call has none
-    e->seq_reset = e->calls_profiled;
+    e->seq_reset = e->calls_total;
     return SDRG_OK;
 }
 

@@ -116,4 +116,21 @@ hipError_t launch_audio_detect(const PulseParams &p, int n_streams, PulseStreamS
                                int *roi_etat, const float *new_e, int max_new, const int *new_count,
                                sdrg_pulse_output *out, hipStream_t stream);
 
+// Sets the thread's sdrg_last_error message and returns code (engine.cpp).
+int32_t fail(int32_t code, const char *fmt, ...);
+
+// Multi-GPU (dist.cpp, gather.hip).  One gather per item, all in one RCCL group on `stream`: every rank sends
+// items[i].bytes from items[i].send; the root receives world x bytes at items[i].recv in rank order.
+struct GatherItem {
+    const void *send;
+    void *recv;
+    size_t bytes;
+};
+int32_t dist_gather(sdrg_dist *d, const GatherItem *items, int n_items, int root, hipStream_t stream);
+int dist_device(const sdrg_dist *d);
+int dist_world(const sdrg_dist *d);
+int dist_rank(const sdrg_dist *d);
+// out[s][j] = spectra[s][lo + j], j < nb: each stream's focus-window slice, contiguous for the gather
+hipError_t launch_focus_pack(const float *spectra, int n_streams, int n, int lo, int nb, float *out, hipStream_t stream);
+
 }  // namespace sdrg

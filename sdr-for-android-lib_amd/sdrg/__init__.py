@@ -99,7 +99,11 @@ EXPORTS = [
     "sdrg_ssb_processor_enqueue", "sdrg_ssb_processor_set_sound_mode", "sdrg_ssb_processor_set_pulse_config",
     "sdrg_ssb_processor_get_ambient_energy", "sdrg_ssb_processor_get_current_ratio", "sdrg_ssb_processor_drain",
     "sdrg_ssb_processor_counters",
+    "sdrg_dist_unique_id", "sdrg_dist_create", "sdrg_dist_destroy", "sdrg_dist_info", "sdrg_engine_gather",
+    "sdrg_engine_gather_records", "sdrg_engine_gather_focus", "sdrg_engine_gather_spectra", "sdrg_engine_gather_pcm",
+    "sdrg_device_alloc", "sdrg_device_free", "sdrg_memcpy",
 ]
+DIST_ID_BYTES = 128  # SDRG_DIST_ID_BYTES (ncclUniqueId)
 
 
 class SdrgError(RuntimeError):
@@ -178,6 +182,11 @@ CB_SSB_PULSE = ctypes.CFUNCTYPE(None, _V, _F, _I32)
 
 class _SsbCallbacks(ctypes.Structure):
     _fields_ = [("user", _V), ("pcm", CB_SSB_PCM), ("pulse", CB_SSB_PULSE)]
+
+
+class _GatherBuffers(ctypes.Structure):
+    _fields_ = [(k, _V) for k in ("records", "records_out", "focus_spectra", "focus_out", "spectra", "spectra_out",
+                                  "pcm", "pcm_out")]
 
 
 _lib = None
@@ -271,6 +280,18 @@ def load() -> ctypes.CDLL:
         "sdrg_ssb_processor_drain": (_I32, [P]),
         "sdrg_ssb_processor_counters": (_I32, [P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
                                               ctypes.POINTER(_I32)]),
+        "sdrg_dist_unique_id": (_I32, [P, _I32]),
+        "sdrg_dist_create": (_I32, [P, _I32, _I32, _I32, ctypes.POINTER(P)]),
+        "sdrg_dist_destroy": (_I32, [P]),
+        "sdrg_dist_info": (_I32, [P, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
+        "sdrg_engine_gather": (_I32, [P, P, _I32, ctypes.POINTER(_GatherBuffers)]),
+        "sdrg_engine_gather_records": (_I32, [P, P, _I32, P, P]),
+        "sdrg_engine_gather_focus": (_I32, [P, P, _I32, P, P]),
+        "sdrg_engine_gather_spectra": (_I32, [P, P, _I32, P, P]),
+        "sdrg_engine_gather_pcm": (_I32, [P, P, _I32, P, P]),
+        "sdrg_device_alloc": (_I32, [_I32, ctypes.c_size_t, ctypes.POINTER(P)]),
+        "sdrg_device_free": (_I32, [_I32, P]),
+        "sdrg_memcpy": (_I32, [_I32, P, P, ctypes.c_size_t]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -308,6 +329,81 @@ class HostBuffer:
             self.array = None
             load().sdrg_host_free(self._p)
             self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceBuffer:
+    """Device memory through the C ABI (sdrg_device_alloc): a torch-free host can feed the engine and the gathers.
+    upload / download are synchronous copies (not ordered with the engine's streams: synchronize the engine first)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        self.device, self.nbytes = device, int(nbytes)
+        p = ctypes.c_void_p()
+        _check(load().sdrg_device_alloc(device, max(self.nbytes, 1), ctypes.byref(p)), "sdrg_device_alloc")
+        self._p = p
+
+    @property
+    def ptr(self) -> int:
+        return self._p.value
+
+    def upload(self, a: np.ndarray) -> None:
+        a = np.ascontiguousarray(a)
+        if a.nbytes > self.nbytes:
+            raise ValueError(f"{a.nbytes} bytes into a {self.nbytes}-byte device buffer")
+        _check(load().sdrg_memcpy(self.device, self._p, a.ctypes.data_as(ctypes.c_void_p), a.nbytes), "sdrg_memcpy")
+
+    def download(self, shape, dtype) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        if out.nbytes > self.nbytes:
+            raise ValueError(f"{out.nbytes} bytes from a {self.nbytes}-byte device buffer")
+        _check(load().sdrg_memcpy(self.device, out.ctypes.data_as(ctypes.c_void_p), self._p, out.nbytes), "sdrg_memcpy")
+        return out
+
+    def close(self) -> None:
+        if getattr(self, "_p", None) is not None and self._p.value:
+            load().sdrg_device_free(self.device, self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def dist_unique_id() -> bytes:
+    """ncclGetUniqueId (sdrg_dist_unique_id) on one rank; hand the bytes to every rank of the job."""
+    buf = ctypes.create_string_buffer(DIST_ID_BYTES)
+    _check(load().sdrg_dist_unique_id(buf, DIST_ID_BYTES), "sdrg_dist_unique_id")
+    return buf.raw
+
+
+class Dist:
+    """An RCCL communicator over the job's ranks (sdrg_dist_create: one process per GPU).  Engine.gather moves the
+    per-frame outputs of every rank's engine to a root rank with it."""
+
+    def __init__(self, unique_id: bytes, world_size: int, rank: int, device: int = 0):
+        if len(unique_id) != DIST_ID_BYTES:
+            raise ValueError(f"unique id must be {DIST_ID_BYTES} bytes")
+        h = ctypes.c_void_p()
+        _check(load().sdrg_dist_create(ctypes.c_char_p(unique_id), world_size, rank, device, ctypes.byref(h)),
+               "sdrg_dist_create")
+        self._h, self.world_size, self.rank, self.device = h, world_size, rank, device
+
+    def info(self) -> dict:
+        r, w, v = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _check(load().sdrg_dist_info(self._h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(v)), "sdrg_dist_info")
+        return {"rank": r.value, "world_size": w.value, "rccl_version": v.value}
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            load().sdrg_dist_destroy(self._h)
+            self._h = None
 
     def __del__(self):
         try:
@@ -542,6 +638,13 @@ class Engine:
         _check(load().sdrg_engine_get_ssb_variant(self._h, ctypes.byref(hz), ctypes.byref(taps), ctypes.byref(inc),
                                                   ctypes.byref(ph)), "get_ssb_variant")
         return {"nco_hz": hz.value, "fir_taps": taps.value, "nco_increment": inc.value, "nco_phase": ph.value}
+
+    def gather(self, dist: "Dist", root: int = 0, records=None, records_out=None, focus_spectra=None, focus_out=None,
+               spectra=None, spectra_out=None, pcm=None, pcm_out=None) -> None:
+        """sdrg_engine_gather: RCCL gathers of this rank's per-frame outputs (device pointers, ints) to `root`, one
+        RCCL group on the engine's main stream after the last call's outputs; *_out only on the root."""
+        b = _GatherBuffers(records, records_out, focus_spectra, focus_out, spectra, spectra_out, pcm, pcm_out)
+        _check(load().sdrg_engine_gather(self._h, dist._h, root, ctypes.byref(b)), "sdrg_engine_gather")
 
     def set_stream(self, hip_stream: int | None) -> None:
         """Enqueue on the caller's HIP stream (e.g. torch.cuda.current_stream().cuda_stream); None = own."""

@@ -1,0 +1,29 @@
+"""BASELINE configs[3]'s collective behind the C ABI: RCCL's ncclGather driven by libsdrg.so
+itself (sdrg_dist_create + sdrg_engine_gather), in an interpreter that never imports torch, so a C/C++ host behind
+the JNI boundary can shard and gather without PyTorch.  One rank (the box has one GPU; RCCL refuses two ranks on one
+device), a pipelined engine with asynchronous statistics, four calls with their gathers and no host synchronisation
+between them: the gathered records, focus slices, full spectra and PCM equal a joined engine's outputs bit for bit.
+The per-frame payload is soapyCallback's (sdr-bridge-java-soapy.cpp:456-466) and the SSB worker's
+(ssb_processor.cpp:103-108)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def test_capi_rccl_gathers_equal_engine_outputs_without_torch():
+    worker = os.path.join(ROOT, "tests", "dist_capi_worker.py")
+    env = dict(os.environ, PYTHONPATH="")
+    r = subprocess.run([sys.executable, "-u", worker], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["torch_loaded"] is False
+    assert res["world"] == 1 and res["rccl_version"] > 0
+    assert res["ok"] and all(res["ok"].values()), res["ok"]

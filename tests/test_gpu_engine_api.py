@@ -123,6 +123,51 @@ def test_timings_right_after_pipelined_call_and_ring_wrap(S, O):
     eng.close()
 
 
+def test_ssb_ms_after_profiling_pause(S, O):
+    """a pipelined call's ssb_ms is measured from the previous call's SSB end marker only when that call
+    was profiled and came right before it.  Turning profiling off for some calls (and idling) and on again without
+    resetting the statistics must not hand the first profiled call an interval spanning the pause."""
+    import time
+
+    import torch
+    B = 256
+    dev = torch.device("cuda:0")
+    eng = engine(S, N, FS, B)
+    eng.set_pipelining(S.PIPELINE_INPUTS_READY)
+    iq = torch.from_numpy(frames(O, B, 1)[0]).to(dev)
+    spec = torch.empty((B, N), dtype=torch.float32, device=dev)
+    rec = torch.zeros((B, S.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    pcm = torch.empty((B, eng.pcm_len), dtype=torch.int16, device=dev)
+    torch.cuda.synchronize()
+    now = [1000]
+
+    def call():
+        eng.process_device(iq.data_ptr(), S.CS8, S.STAGE_ALL, spec.data_ptr(), rec.data_ptr(), pcm.data_ptr(), now[0])
+        now[0] += 8
+
+    eng.set_profiling(True)
+    for _ in range(12):
+        call()
+    per_call = eng.timing_stats()["ssb_ms"]
+    assert per_call > 0
+    eng.set_profiling(False)
+    for _ in range(10):
+        call()
+    eng.synchronize()
+    time.sleep(0.05)  # 50 ms idle: far above a call's SSB time
+    eng.set_profiling(True)
+    call()
+    t = eng.timings()
+    assert 0 < t["ssb_ms"] < 3 * per_call + 0.5, (t, per_call)
+    for _ in range(3):  # the calls after it chain from its end marker again
+        call()
+    t = eng.timings()
+    assert 0 < t["ssb_ms"] < 3 * per_call + 0.5, (t, per_call)
+    st = eng.timing_stats()  # the window's mean holds no pause either
+    assert st["ssb_ms"] < 3 * per_call + 0.5, (st, per_call)
+    eng.close()
+
+
 def test_rejected_call_freezes_nothing(S, O):
     """a call rejected after the SSB statics would have been set (null pcm) must not freeze the SSB
     frame size: the first SUCCESSFUL call freezes it (processSSB_opt's static sampCount, :224-227)."""

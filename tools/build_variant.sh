@@ -13,7 +13,9 @@ $HIP -c $D/csrc/fftany.hip -o $B/fftany.o
 $HIP -I$D/csrc -Iinclude -ffp-contract=off -fno-slp-vectorize -c ${STATS_SRC:-$D/csrc/stats.hip} -o $B/stats.o
 $HIP -I$D/csrc -Iinclude -ffp-contract=off -fno-slp-vectorize -c ${SSB_SRC:-$D/csrc/ssb.hip} -o $B/ssb.o
 $HIP -ffp-contract=off -c $D/csrc/pulse.hip -o $B/pulse.o
-for f in design engine pulse_bank ingest compat ssb_processor; do $CXX -c $D/csrc/$f.cpp -o $B/$f.o; done
+$HIP -c $D/csrc/gather.hip -o $B/gather.o
+for f in design engine pulse_bank ingest compat ssb_processor dist; do $CXX -c $D/csrc/$f.cpp -o $B/$f.o; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/lib/libsdrg_$NAME.so $B/spectrum.o $B/fftany.o $B/stats.o \
-    $B/ssb.o $B/pulse.o $B/design.o $B/engine.o $B/pulse_bank.o $B/ingest.o $B/compat.o $B/ssb_processor.o -lm -lpthread
+    $B/ssb.o $B/pulse.o $B/gather.o $B/design.o $B/engine.o $B/pulse_bank.o $B/ingest.o $B/compat.o $B/ssb_processor.o \
+    $B/dist.o -lm -lpthread -ldl
 echo built $D/lib/libsdrg_$NAME.so
