@@ -519,10 +519,12 @@ typedef struct sdrg_gather_buffers {
     const int16_t *pcm;
     int16_t *pcm_out;
 } sdrg_gather_buffers;
-/* Enqueue the gathers (one RCCL group) on the engine's main stream after the last process call's outputs they read
- * (records of asynchronous statistics and the PCM of a pipelined call included): no host synchronisation, and the
- * engine's next call cannot overwrite a gathered buffer before the gather has read it.  Every rank calls it with the
- * same selection.  Complete after sdrg_engine_synchronize (or on a stream after sdrg_engine_wait_outputs). */
+/* Enqueue the gathers (one RCCL group) on a gather stream of the engine, after the last process call's outputs they
+ * read (records of asynchronous statistics and the PCM of a pipelined call included): no host synchronisation, and
+ * none of the engine's own streams waits for them -- a later call that writes a buffer still being gathered (the
+ * same pointer) waits for the gather on the GPU first, so a caller rotating its output buffers overlaps the gathers
+ * with its next calls.  Every rank calls it with the same selection.  Complete after sdrg_engine_synchronize (or on
+ * a stream after sdrg_engine_wait_outputs). */
 int32_t sdrg_engine_gather(sdrg_engine *eng, sdrg_dist *d, int32_t root, const sdrg_gather_buffers *bufs);
 /* Single-pair forms of sdrg_engine_gather. */
 int32_t sdrg_engine_gather_records(sdrg_engine *eng, sdrg_dist *d, int32_t root, const sdrg_frame_record *records,

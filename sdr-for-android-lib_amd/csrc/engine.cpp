@@ -179,10 +179,13 @@ struct sdrg_engine {
     size_t spec_scratch_elems = 0;
     float *d_focus_stage = nullptr;   // sdrg_engine_gather: the focus-window slices, packed for ncclGather
     size_t focus_stage_elems = 0;
-    // sdrg_engine_gather of a call's PCM: the next call's SSB stage (which does not follow the main stream when
-    // pipelined) waits for the gather before it overwrites the buffer
+    // sdrg_engine_gather runs on a stream of its own after the outputs it reads; a later call that writes a buffer
+    // still being gathered (same pointer) waits for the gather on the GPU first, so a caller rotating its output
+    // buffers never delays its next call's kernels behind a gather
+    hipStream_t s_gather = nullptr;
     hipEvent_t ev_gather = nullptr;
-    bool gather_pending_ssb = false;
+    std::vector<const void *> g_bufs;  // buffers the gathers since the last wait on ev_gather read
+    bool gathering(const void *p) const { return p && std::find(g_bufs.begin(), g_bufs.end(), p) != g_bufs.end(); }
     float *d_fft_scratch = nullptr;   // four-step intermediate (N > 16384)
     size_t fft_scratch_elems = 0;
     sdrg_frame_record *d_rec_scratch = nullptr;
@@ -632,6 +635,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         if (c >= 1 && e->sa_live[pv] && (e->sa_spec[pv] == spec || !async))
             HIP_TRY(hipStreamWaitEvent(sm, e->ev_stats_end[pv], 0));
     }
+    if (do_spec && e->gathering(spec)) HIP_TRY(hipStreamWaitEvent(sm, e->ev_gather, 0));  // still being gathered
     if (do_spec) {
         HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, sm, do_ssb && early_fork && !split,
                                 split ? e->spec_cus : 0, do_stats && stats_uses_wide(geo)));
@@ -641,10 +645,8 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         if (!early_fork) {
             HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
             HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
-        } else if (e->gather_pending_ssb) {  // the last call's PCM is being gathered on the main stream
-            HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_gather, 0));
         }
-        e->gather_pending_ssb = false;
+        if (e->gathering(pcm)) HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_gather, 0));  // still being gathered
         if (prof && ev->ssb_timed) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
         // AudioPulseDetector::process(pcm) after processSSB_opt (ssb_processor.cpp:109): its per-sample front
         // end runs inside the SSB kernel on the PCM it produces, the detector right after
@@ -678,6 +680,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             HIP_TRY(hipStreamWaitEvent(e->s_stats, e->ev_spec_done, 0));
             st = e->s_stats;
         }
+        if (e->gathering(recs)) HIP_TRY(hipStreamWaitEvent(st, e->ev_gather, 0));  // still being gathered
         HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->d_pool, st));
         if (do_sp) {  // spectralPulseDetector.process(best1kHzSnrSigma, best1kHzCenterFreqHz) (:477-479)
             int32_t rc = pulse_bank_spectral(&e->spec_bank, &recs->best1khz_snr_sigma, &recs->best1khz_center_freq_hz,
@@ -716,6 +719,12 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         e->nco_phase = nco_next;
     }
     if (do_stats) e->cf_changed_pending = false;
+    // a buffer this call waited for is rewritten on a stream ordered after the gathers: no longer pending (the other
+    // gathered buffers stay pending until a call writes them)
+    const void *written[] = {do_spec ? (const void *)spec : nullptr, do_stats ? (const void *)recs : nullptr,
+                             do_ssb ? (const void *)pcm : nullptr};
+    for (const void *w : written)
+        if (w) e->g_bufs.erase(std::remove(e->g_bufs.begin(), e->g_bufs.end(), w), e->g_bufs.end());
     if (do_spec) e->last_in_main = mk_main_end;
     if (do_ssb) e->last_in_ssb = mk_ssb_end;
     return SDRG_OK;
@@ -905,6 +914,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (e->s_spec) (void)hipStreamSynchronize(e->s_spec);
     for (hipEvent_t ev : e->ev_stats_end)
         if (ev) (void)hipEventDestroy(ev);
+    if (e->s_gather) (void)hipStreamSynchronize(e->s_gather);
     hipEvent_t evs[] = {e->ev_fork, e->ev_join, e->ev_in_main, e->ev_in_ssb, e->ev_fork_spec, e->ev_join_spec,
                         e->ev_spec_done, e->ev_ap_end[0], e->ev_ap_end[1], e->ev_ap_end[2], e->ev_gather};
     for (hipEvent_t ev : evs)
@@ -921,6 +931,7 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
     if (e->s_spec) (void)hipStreamDestroy(e->s_spec);
     if (e->s_stats) (void)hipStreamDestroy(e->s_stats);
     if (e->s_ap) (void)hipStreamDestroy(e->s_ap);
+    if (e->s_gather) (void)hipStreamDestroy(e->s_gather);
     delete e;
     return SDRG_OK;
 }
@@ -993,6 +1004,7 @@ int32_t sdrg_engine_wait_outputs(sdrg_engine *e, void *hip_stream) {
     if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));                    // PCM
     if (e->last_ap_end) HIP_TRY(hipStreamWaitEvent(s, e->last_ap_end, 0));                    // audio pulse
     if (e->stats_async && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));  // records
+    if (e->ev_gather) HIP_TRY(hipStreamWaitEvent(s, e->ev_gather, 0));  // the gathered outputs on the root
     return SDRG_OK;
 }
 
@@ -1219,6 +1231,7 @@ int32_t sdrg_engine_synchronize(sdrg_engine *e) {
     HIP_TRY(hipStreamSynchronize(e->s_ssb));  // not joined into s_main when pipelined
     if (e->s_stats) HIP_TRY(hipStreamSynchronize(e->s_stats));  // SDRG_PIPELINE_STATS_ASYNC
     HIP_TRY(hipStreamSynchronize(e->s_ap));                      // the audio pulse detector
+    if (e->s_gather) HIP_TRY(hipStreamSynchronize(e->s_gather));  // sdrg_engine_gather
     static const bool stamps = [] {
         const char *v = lab_getenv("SDRG_PIPE_STAMPS");
         return v && v[0] == '1';
@@ -1360,10 +1373,10 @@ int32_t sdrg_engine_get_timing_stats(const sdrg_engine *ce, sdrg_timings *mean, 
     return SDRG_OK;
 }
 
-// Multi-GPU gather (include/sdrg.h; dist.cpp holds RCCL): the gathers go on the main stream after the outputs they
-// read -- the statistics' stream's last event for records of asynchronous statistics, the SSB stream's end marker for
-// PCM -- so the next call's spectrum and statistics (main stream, or forked from it) follow them; the next call's
-// SSB stage, which a pipelined call does not fork from the main stream, waits for ev_gather when PCM was gathered.
+// Multi-GPU gather (include/sdrg.h; dist.cpp holds RCCL).  The gathers run on s_gather after the outputs they read --
+// the main stream's end marker (spectra; records of statistics on the main stream), the statistics' stream's last
+// event (records of asynchronous statistics), the SSB stream's end marker (PCM) -- so they delay none of the engine's
+// streams; a later call that writes a buffer still being gathered waits for ev_gather first (enqueue).
 int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdrg_gather_buffers *b) {
     if (!e || !d || !b) return fail(SDRG_E_INVALID, "null argument");
     if (dist_device(d) != e->device)
@@ -1374,42 +1387,43 @@ int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdr
     const bool at_root = dist_rank(d) == root;
     const size_t B = (size_t)e->n_streams;
     const int n = e->cfg.samples_per_reading;
-    hipStream_t s = e->s_main;
+    const int plen = ssb_pcm_len(ssb_frozen_or(e), (uint32_t)e->cfg.sample_rate, e->fir_taps);
+    const bool g_rec = b->records, g_foc = b->focus_spectra, g_spec = b->spectra, g_pcm = b->pcm && plen > 0;
+    if ((g_rec && at_root && !b->records_out) || (g_foc && at_root && !b->focus_out) ||
+        (g_spec && at_root && !b->spectra_out) || (g_pcm && at_root && !b->pcm_out))
+        return fail(SDRG_E_INVALID, "null output buffer on the root");
+    StatsGeometry geo{};
+    if (g_foc) {
+        geo = stats_geometry(e->fft_fs, e->fft_fc, n, e->fft_focus);
+        if (geo.focus_len <= 0) return fail(SDRG_E_INVALID, "the focus window is empty (focus wider than the band)");
+        int32_t rc = ensure_device(&e->d_focus_stage, &e->focus_stage_elems, B * (size_t)geo.focus_len);
+        if (rc) return rc;
+    }
+    if (!(g_rec || g_foc || g_spec || g_pcm)) return SDRG_OK;
+    if (!e->s_gather) HIP_TRY(hipStreamCreateWithFlags(&e->s_gather, hipStreamNonBlocking));
+    if (!e->ev_gather) HIP_TRY(hipEventCreateWithFlags(&e->ev_gather, hipEventDisableTiming | hipEventDisableSystemFence));
+    hipStream_t s = e->s_gather;
+    if ((g_rec || g_foc || g_spec) && e->last_in_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));
+    if (g_rec && e->stats_async && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));
+    if (g_pcm && e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
     GatherItem items[4];
     int k = 0;
-    if (b->records) {
-        if (at_root && !b->records_out) return fail(SDRG_E_INVALID, "null records_out on the root");
-        if (e->stats_async && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));
-        items[k++] = {b->records, b->records_out, B * sizeof(sdrg_frame_record)};
+    if (g_rec) items[k++] = {b->records, b->records_out, B * sizeof(sdrg_frame_record)};
+    if (g_foc) {
+        HIP_TRY(launch_focus_pack(b->focus_spectra, (int)B, n, geo.focus_lo, geo.focus_len, e->d_focus_stage, s));
+        items[k++] = {e->d_focus_stage, b->focus_out, B * (size_t)geo.focus_len * sizeof(float)};
     }
-    if (b->focus_spectra) {
-        if (at_root && !b->focus_out) return fail(SDRG_E_INVALID, "null focus_out on the root");
-        const StatsGeometry g = stats_geometry(e->fft_fs, e->fft_fc, n, e->fft_focus);
-        if (g.focus_len <= 0) return fail(SDRG_E_INVALID, "the focus window is empty (focus wider than the band)");
-        int32_t rc = ensure_device(&e->d_focus_stage, &e->focus_stage_elems, B * (size_t)g.focus_len);
-        if (rc) return rc;
-        HIP_TRY(launch_focus_pack(b->focus_spectra, (int)B, n, g.focus_lo, g.focus_len, e->d_focus_stage, s));
-        items[k++] = {e->d_focus_stage, b->focus_out, B * (size_t)g.focus_len * sizeof(float)};
-    }
-    if (b->spectra) {
-        if (at_root && !b->spectra_out) return fail(SDRG_E_INVALID, "null spectra_out on the root");
-        items[k++] = {b->spectra, b->spectra_out, B * (size_t)n * sizeof(float)};
-    }
-    const int plen = ssb_pcm_len(ssb_frozen_or(e), (uint32_t)e->cfg.sample_rate, e->fir_taps);
-    if (b->pcm && plen > 0) {
-        if (at_root && !b->pcm_out) return fail(SDRG_E_INVALID, "null pcm_out on the root");
-        if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
-        items[k++] = {b->pcm, b->pcm_out, B * (size_t)plen * sizeof(int16_t)};
-    }
-    if (k == 0) return SDRG_OK;
+    if (g_spec) items[k++] = {b->spectra, b->spectra_out, B * (size_t)n * sizeof(float)};
+    if (g_pcm) items[k++] = {b->pcm, b->pcm_out, B * (size_t)plen * sizeof(int16_t)};
     int32_t rc = dist_gather(d, items, k, root, s);
     if (rc) return rc;
-    if (b->pcm && plen > 0) {
-        if (!e->ev_gather)
-            HIP_TRY(hipEventCreateWithFlags(&e->ev_gather, hipEventDisableTiming | hipEventDisableSystemFence));
-        HIP_TRY(hipEventRecord(e->ev_gather, s));
-        e->gather_pending_ssb = true;
-    }
+    HIP_TRY(hipEventRecord(e->ev_gather, s));
+    // the buffers the gathers in flight read (a gather's own focus staging is reused only by the next gather, which
+    // follows it on s_gather); ev_gather covers every earlier gather too
+    const void *read[] = {g_rec ? (const void *)b->records : nullptr, g_foc ? (const void *)b->focus_spectra : nullptr,
+                          g_spec ? (const void *)b->spectra : nullptr, g_pcm ? (const void *)b->pcm : nullptr};
+    for (const void *r : read)
+        if (r && !e->gathering(r)) e->g_bufs.push_back(r);
     return SDRG_OK;
 }
 

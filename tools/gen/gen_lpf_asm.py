@@ -140,6 +140,7 @@ def chunk(role, lds=True, split=False, il=False):
 
 
 SLOT = 16 * 68 * 4  # bytes per [stream][sample] chunk buffer (PG x ROW floats)
+SLOT64 = 64 * 68 * 4  # the same for ssb64.hip's 64-stream rows
 
 
 def lpf_loop():
@@ -236,7 +237,7 @@ def lpf_loop():
     return out
 
 
-def lpf_loop_interleaved(spread=False):
+def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3):
     """lpf_loop() with the LDS traffic spread through the VALU stream: sub-blocks are numbered g = 4c + sb across
     chunks and live in buffer g mod 3; while sub-block g runs, after each 4-sample quad t its output quad is written
     and quad t of sub-block g + 2 is read (for sb = 2, 3 that is the next chunk's sub-block 0, 1, complete in its
@@ -245,8 +246,10 @@ def lpf_loop_interleaved(spread=False):
     ring slot and are never used; the block drains them (lgkmcnt(0)) before it ends."""
     out = []
     u = "%="
-    # the 16 stream lanes: 0-15, or (spread) lanes {0-3, 16-19, 32-35, 48-51}
-    lanes = ["s_mov_b32 exec_lo, 0xf000f", "s_mov_b32 exec_hi, 0xf000f"] if spread else ["s_mov_b64 exec, 0xffff"]
+    # the 16 stream lanes: 0-15, or (spread) lanes {0-3, 16-19, 32-35, 48-51}; all_lanes: 64 streams, one per lane
+    # (ssb64.hip), with `slot` bytes per ring slot and the output ring's slot = chunk & ymask
+    lanes = (["s_mov_b64 exec, -1"] if all_lanes else
+             ["s_mov_b32 exec_lo, 0xf000f", "s_mov_b32 exec_hi, 0xf000f"] if spread else ["s_mov_b64 exec, 0xffff"])
     out += ["s_mov_b64 %[sv], exec"] + lanes + [
         "s_nop 4",
         "v_pk_mov_b32 v[46:47], %[z], %[z] op_sel:[1,0]",
@@ -259,8 +262,8 @@ def lpf_loop_interleaved(spread=False):
         f"s_cbranch_scc1 L_pre_{u}",
         "s_cmp_ge_i32 %[cc], %[nch]",
         f"s_cbranch_scc1 L_drain_{u}",
-        "s_and_b32 %[yo], %[cc], 3",
-        f"s_mul_i32 %[yo], %[yo], {SLOT}",
+        f"s_and_b32 %[yo], %[cc], {ymask}",
+        f"s_mul_i32 %[yo], %[yo], {slot}",
         "v_add_u32 v54, %[yo], %[ybase]",
         "s_cmp_eq_u32 %[r], 0",
         f"s_cbranch_scc1 L_r0_{u}",
@@ -283,7 +286,7 @@ def lpf_loop_interleaved(spread=False):
                 if q % 4 == 3:
                     t = q // 4
                     out.append(f"ds_write_b128 v54, v[{b + 4 * t}:{b + 4 * t + 3}] offset:{(16 * sb + 4 * t) * 4}")
-                    out.append(f"ds_read_b128 v[{rb + 4 * t}:{rb + 4 * t + 3}], %[abase] offset:{rslot * SLOT + (16 * rsb + 4 * t) * 4}")
+                    out.append(f"ds_read_b128 v[{rb + 4 * t}:{rb + 4 * t + 3}], %[abase] offset:{rslot * slot + (16 * rsb + 4 * t) * 4}")
         last = BUFS[(r + 3) % 3] + 15
         out.append(f"v_pk_mov_b32 v[52:53], v[{last - 1}:{last}], v[{last - 1}:{last}] op_sel:[1,0]")
         out.append(f"s_branch L_bar1_{u}")
@@ -351,6 +354,8 @@ def main():
     emit("SDRG_LPF_LOOP_IL_ASM", lpf_loop_interleaved())
     print("// the same on the lanes {0-3, 16-19, 32-35, 48-51} (SDRG_SERIAL_LANES=1)")
     emit("SDRG_LPF_LOOP_IL_SPREAD_ASM", lpf_loop_interleaved(spread=True))
+    print("// the same on all 64 lanes, one stream each (ssb64.hip: 64-stream rows, a 2-slot output ring)")
+    emit("SDRG_LPF64_LOOP_IL_ASM", lpf_loop_interleaved(all_lanes=True, slot=SLOT64, ymask=1))
     print("// the low-pass chunk with its VALU on all 64 lanes and the LDS operations on the caller's lanes; extra operand")
     print("// %[sv] (=&s, 64-bit): the caller's EXEC (lab option SDRG_LPF_ASM=2)")
     emit("SDRG_LPF_CHUNK_SPLIT_ASM", chunk("lpf", split=True))
@@ -364,6 +369,7 @@ def main():
         print("    " + ", ".join(regs[i:i + 16]) + (", \\" if i + 16 < len(regs) else ""))
     print("#define SDRG_LPF_CHUNK_CLOBBERS SDRG_CHUNK_CLOBBERS")
     print(f"#define SDRG_LPF_LOOP_SLOT_BYTES {SLOT}")
+    print(f"#define SDRG_LPF64_LOOP_SLOT_BYTES {SLOT64}")
 
 
 if __name__ == "__main__":

@@ -1,22 +1,30 @@
 #!/bin/bash
-# The current GPU session's steps (overwritten per session; git history keeps each one).  Run: gpurun -- bash tools/session.sh
-# r5a: the C-ABI RCCL gather, the profiling-pause timing fix, the labelled lines'
-# per-kernel times, then the default bench line and the one-rank --process-group line through the C ABI.
+# r5d: (1) wide statistics with the pooled dB sum's reads pipelined: tests, alone vs round 4, stamps per phase;
+# (2) ssb64 with the front's LDS-DMA raw ring: SSB parity tests, per-role stamps, per-kernel times
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-T=r5a
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_dist_capi.py \
-  tests/test_gpu_engine_api.py tests/test_gpu_rccl.py > gpurun_out/${T}_tests.log 2>&1 || { tail -40 gpurun_out/${T}_tests.log; exit 1; }
-tail -3 gpurun_out/${T}_tests.log
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { tail -20 gpurun_out/${T}_bench.err; exit 1; }
-python3 tools/bench_summary.py gpurun_out/${T}_bench.json
+T=r5d
+D=sdr-for-android-lib_amd/lib
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_stats_exact.py \
+  tests/test_gpu_stats_geometry.py > gpurun_out/${T}_tests.log 2>&1 || { tail -40 gpurun_out/${T}_tests.log; exit 1; }
+tail -1 gpurun_out/${T}_tests.log
 for i in 1 2; do
-  timeout -k 10 200 python bench.py --process-group --steps 200 --warmup 100 --no-cpu-baseline --no-labelled > gpurun_out/${T}_pg$i.json 2> gpurun_out/${T}_pg$i.err || { tail -20 gpurun_out/${T}_pg$i.err; exit 1; }
-  timeout -k 10 200 python bench.py --steps 200 --warmup 100 --no-cpu-baseline --no-labelled > gpurun_out/${T}_nopg$i.json 2> gpurun_out/${T}_nopg$i.err || { tail -20 gpurun_out/${T}_nopg$i.err; exit 1; }
-  python3 -c "
-import json
-a=json.load(open('gpurun_out/${T}_pg$i.json')); b=json.load(open('gpurun_out/${T}_nopg$i.json'))
-print('pg', a['value'], a['ms_per_step'], a.get('backend'), a.get('gather_check'), a.get('rccl_version'), '| no pg', b['value'], b['ms_per_step'])"
+  for v in r4stats base; do
+    L=$D/libsdrg_$v.so; [ $v == base ] && L=$D/libsdrg.so
+    echo "$v stats alone: $(SDRG_LIB_PATH=$L timeout -k 10 120 python tools/lab/stats_time.py 65536 200 1024 30 2>/dev/null | tail -1)"
+  done
 done
-bash tools/gpu_rehearse.sh > gpurun_out/${T}_rehearse.log 2>&1; echo "rehearse exit $?"; tail -5 gpurun_out/${T}_rehearse.log
+SDRG_LIB_PATH=$D/libsdrg_mwst.so timeout -k 10 120 python tools/lab/stats_time.py 65536 200 1024 3 2>&1 | grep "mw stamps" | tail -1
+SDRG_LIB_PATH=$D/libsdrg_ssb64.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+  tests/test_gpu_parity.py tests/test_gpu_pulse.py tests/test_gpu_ssb_schedule.py > gpurun_out/${T}_ssb64_tests.log 2>&1 || { tail -40 gpurun_out/${T}_ssb64_tests.log; exit 1; }
+tail -1 gpurun_out/${T}_ssb64_tests.log
+SDRG_SSB64_STAMPS=1 SDRG_LIB_PATH=$D/libsdrg_ssb64.so timeout -k 10 200 python bench.py --stages ssb --steps 40 --warmup 5 --no-cpu-baseline --no-labelled --prewarm-ms 0 > gpurun_out/${T}_st.json 2> gpurun_out/${T}_st.err || { tail -5 gpurun_out/${T}_st.err; exit 1; }
+grep "ssb64 stamps" gpurun_out/${T}_st.err | tail -2
+SDRG_LIB_PATH=$D/libsdrg_ssb64.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof64 -o run --output-format csv -- python3 bench.py --stages ssb --steps 20 --warmup 10 --no-cpu-baseline --no-labelled > gpurun_out/${T}_prof64.log 2>&1 || { echo "prof failed"; tail -5 gpurun_out/${T}_prof64.log; exit 1; }
+python3 - <<'PY'
+import csv, glob
+for f in glob.glob("gpurun_out/r5d_prof64/**/run_kernel_stats.csv", recursive=True):
+    for r in list(csv.DictReader(open(f)))[:4]:
+        print(f"{r['Name'][:70]:70s} {r['Calls']:>5} {float(r['AverageNs'])/1e3:9.1f} us")
+PY
