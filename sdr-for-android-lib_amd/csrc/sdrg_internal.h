@@ -102,7 +102,7 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
                       bool *stop_recorded = nullptr);
 // ssb64.hip: the chain with 64 streams per serial wave (a front and a back workgroup per 64 streams); launch_ssb takes
 // it when ssb64_supported (scratch: [n_frames][samp_count] floats for the front -> back hand-off)
-bool ssb64_supported(const SsbParams &p, const void *iq, int fmt, int nsl_mask, bool have_scratch);
+bool ssb64_supported(const SsbParams &p, const void *iq, int fmt, int n_frames, int nsl_mask, bool have_scratch);
 hipError_t launch_ssb64(const void *iq, int fmt, int n_frames, const SsbParams &p, int nsl_mask, const int *chunk_table,
                         const float *taps, SsbStreamState *state, float *scratch, int16_t *pcm, const AudioFront *audio,
                         hipStream_t stream, hipEvent_t stop, bool *stop_recorded);

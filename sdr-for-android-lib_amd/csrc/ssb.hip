@@ -1024,14 +1024,16 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
     const int4 *chunk_out = reinterpret_cast<const int4 *>(chunk_table);
     // the 64-stream front/back split (ssb64.hip), where it applies (SDRG_SSB64; lab builds: the environment knob of the
     // same name overrides)
+#if SDRG_SSB64  // lab builds only (profiles/r5_ssb64_stamps.md): not faster than this pipeline, see DESIGN.md 3.3
     static const int use64 = [] {
         const char *v = lab_getenv("SDRG_SSB64");
         return v ? atoi(v) : SDRG_SSB64;
     }();
     if (use64 && chunk_out && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels() &&
-        ssb64_supported(p, iq, fmt, nsl_mask, scratch != nullptr))
+        ssb64_supported(p, iq, fmt, n_frames, nsl_mask, scratch != nullptr))
         return launch_ssb64(iq, fmt, n_frames, p, nsl_mask, chunk_table, taps, state, scratch, pcm, audio, stream, stop,
                             stop_recorded);
+#endif
     if (chunk_out && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels()) {
         const dim3 grid((n_frames + PG - 1) / PG);
         size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
