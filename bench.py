@@ -45,6 +45,7 @@ ALG_BYTES_PER_SAMPLE = {"spectrum": 6.0}  # CS8: 2 B in + 4 B fftshifted float32
 ISO_LAUNCHES = 30  # launches of the spectrum stage alone behind roofline_isolated
 N_INPUTS = 3  # distinct input batches rotated per step: 3 x 128 MiB > the 256 MiB Infinity Cache
 SSB_ISO_CALLS = 20  # joined SSB-only calls timed for ssb_latency_floor.ssb_ms_alone
+LAB_NO_STEP_GATHER = os.environ.get("SDRG_BENCH_NO_STEP_GATHER") == "1"  # lab: the N > 1 path without its per-step gathers
 N_OUTPUTS = 3  # spectra / records buffers rotated per step (asynchronous statistics read a call's spectra late)
 # SSB floor: the sample-serial low-pass wave's own instruction issue.  Per sample it issues 6 VALU instructions
 # (the packed product of the previous output, 4 dependent adds, the packed product of the output before it) and
@@ -409,7 +410,7 @@ def main() -> int:
         eng.process_device(iq.data_ptr(), fmt, stages if st is None else st, spec.data_ptr(), rec.data_ptr(),
                            pcm.data_ptr(), now[0])
         now[0] += n // 2000  # frame duration in ms at 2 Msps (8 ms for 16384)
-        if capi:  # one RCCL group on the engine's main stream, after this step's outputs
+        if capi and not LAB_NO_STEP_GATHER:  # one RCCL group on the engine's gather stream, after this step's outputs
             eng.gather(dcomm, 0, records=rec.data_ptr(), records_out=ptr(gathered),
                        focus_spectra=spec.data_ptr() if focus else None, focus_out=ptr(f_out),
                        pcm=pcm.data_ptr() if gather_pcm else None, pcm_out=ptr(p_out))
@@ -428,7 +429,9 @@ def main() -> int:
     # host-staged rehearsal copies the PCM on the main stream, so its per-step PCM gather needs the joined schedule
     # (sdrg_engine_gather orders a pipelined call's PCM itself)
     pipelined = args.pipelined if not (gather_pcm and rehearse) else 0
-    async_ok = bool(pipelined and not dist_on)
+    # asynchronous statistics need gathers ordered after the statistics' own stream: sdrg_engine_gather does that (it
+    # waits for them on the GPU); the host-staged rehearsal gathers on a torch stream and keeps them on the main stream
+    async_ok = bool(pipelined and (capi or not dist_on))
     with_ssb = args.stages == "all"
     stats_async = async_ok and (args.stats_async == "1" or (args.stats_async == "auto" and (c5 or with_ssb)))
     pipe_mode = pipelined | (sdrg.PIPELINE_STATS_ASYNC if stats_async else 0)

@@ -183,9 +183,24 @@ struct sdrg_engine {
     // still being gathered (same pointer) waits for the gather on the GPU first, so a caller rotating its output
     // buffers never delays its next call's kernels behind a gather
     hipStream_t s_gather = nullptr;
-    hipEvent_t ev_gather = nullptr;
-    std::vector<const void *> g_bufs;  // buffers the gathers since the last wait on ev_gather read
-    bool gathering(const void *p) const { return p && std::find(g_bufs.begin(), g_bufs.end(), p) != g_bufs.end(); }
+    hipEvent_t ev_gather = nullptr;  // the last gather's end (wait_outputs, synchronize)
+    // each gather's end in a ring; a buffer a gather read maps to that gather's slot, so a call that rewrites it waits
+    // for that gather only (waiting on the last gather instead made call k + 3's spectrum wait for gather k + 2, and
+    // with it for call k + 2's asynchronous statistics)
+    static constexpr int GRING = 8;
+    hipEvent_t ev_g[GRING] = {};
+    int64_t g_calls = 0;
+    struct GBuf {
+        const void *p;
+        int slot;
+    };
+    std::vector<GBuf> g_bufs;  // buffers read by gathers no later call has yet waited for
+    hipEvent_t gathering(const void *p) const {
+        if (p)
+            for (const GBuf &g : g_bufs)
+                if (g.p == p) return ev_g[g.slot];
+        return nullptr;
+    }
     float *d_fft_scratch = nullptr;   // four-step intermediate (N > 16384)
     size_t fft_scratch_elems = 0;
     sdrg_frame_record *d_rec_scratch = nullptr;
@@ -635,7 +650,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         if (c >= 1 && e->sa_live[pv] && (e->sa_spec[pv] == spec || !async))
             HIP_TRY(hipStreamWaitEvent(sm, e->ev_stats_end[pv], 0));
     }
-    if (do_spec && e->gathering(spec)) HIP_TRY(hipStreamWaitEvent(sm, e->ev_gather, 0));  // still being gathered
+    if (hipEvent_t g = do_spec ? e->gathering(spec) : nullptr) HIP_TRY(hipStreamWaitEvent(sm, g, 0));  // being gathered
     if (do_spec) {
         HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, sm, do_ssb && early_fork && !split,
                                 split ? e->spec_cus : 0, do_stats && stats_uses_wide(geo)));
@@ -646,7 +661,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
             HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
         }
-        if (e->gathering(pcm)) HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_gather, 0));  // still being gathered
+        if (hipEvent_t g = e->gathering(pcm)) HIP_TRY(hipStreamWaitEvent(e->s_ssb, g, 0));  // still being gathered
         if (prof && ev->ssb_timed) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
         // AudioPulseDetector::process(pcm) after processSSB_opt (ssb_processor.cpp:109): its per-sample front
         // end runs inside the SSB kernel on the PCM it produces, the detector right after
@@ -680,7 +695,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             HIP_TRY(hipStreamWaitEvent(e->s_stats, e->ev_spec_done, 0));
             st = e->s_stats;
         }
-        if (e->gathering(recs)) HIP_TRY(hipStreamWaitEvent(st, e->ev_gather, 0));  // still being gathered
+        if (hipEvent_t g = e->gathering(recs)) HIP_TRY(hipStreamWaitEvent(st, g, 0));  // still being gathered
         HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->d_pool, st));
         if (do_sp) {  // spectralPulseDetector.process(best1kHzSnrSigma, best1kHzCenterFreqHz) (:477-479)
             int32_t rc = pulse_bank_spectral(&e->spec_bank, &recs->best1khz_snr_sigma, &recs->best1khz_center_freq_hz,
@@ -724,7 +739,9 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     const void *written[] = {do_spec ? (const void *)spec : nullptr, do_stats ? (const void *)recs : nullptr,
                              do_ssb ? (const void *)pcm : nullptr};
     for (const void *w : written)
-        if (w) e->g_bufs.erase(std::remove(e->g_bufs.begin(), e->g_bufs.end(), w), e->g_bufs.end());
+        if (w)
+            e->g_bufs.erase(std::remove_if(e->g_bufs.begin(), e->g_bufs.end(), [w](const sdrg_engine::GBuf &g) { return g.p == w; }),
+                            e->g_bufs.end());
     if (do_spec) e->last_in_main = mk_main_end;
     if (do_ssb) e->last_in_ssb = mk_ssb_end;
     return SDRG_OK;
@@ -817,6 +834,38 @@ int32_t sdrg_ssb_design(int32_t samp_count, int64_t sample_rate, int32_t sound_m
     return SDRG_OK;
 }
 
+// Lab (SDRG_QUEUES = "dedicated_mask[,eager]"): HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues, shared
+// round-robin by creation order, so streams another library creates (RCCL's, at communicator init) change which engine
+// streams share a queue.  dedicated_mask bit 1 main, 2 SSB, 4 statistics, 8 audio detector, 16 gathers: that stream is
+// created with a full CU mask, which gives it a hardware queue of its own; eager: the statistics and gather streams are
+// created with the engine instead of at first use.
+struct QueuePlan {
+    int dedicated = 0;
+    bool eager = false;
+};
+static QueuePlan queue_plan() {
+    static const QueuePlan q = [] {
+        QueuePlan r;
+        if (const char *v = lab_getenv("SDRG_QUEUES")) {
+            int eg = 0;
+            if (sscanf(v, "%d,%d", &r.dedicated, &eg) >= 1) r.eager = eg != 0;
+        }
+        return r;
+    }();
+    return q;
+}
+static hipError_t create_engine_stream(hipStream_t *s, int role_bit, int device, int prio = 0) {
+    if (queue_plan().dedicated & role_bit) {
+        int ncu = 0;
+        hipError_t e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+        if (e != hipSuccess) return e;
+        std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; i++) m[i / 32] |= 1u << (i % 32);
+        return hipExtStreamCreateWithCUMask(s, (uint32_t)m.size(), m.data());
+    }
+    return prio ? hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio) : hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t device, sdrg_engine **out) {
     if (!out) return fail(SDRG_E_INVALID, "null out");
     *out = nullptr;
@@ -848,8 +897,8 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
     if (const char *v = lab_getenv("SDRG_STREAM_PRIO")) {
         if (sscanf(v, "%d,%d", &prio_main, &prio_ssb) != 2) prio_main = prio_ssb = 0;
     }
-    if (hipStreamCreateWithPriority(&e->s_own, hipStreamNonBlocking, prio_main) != hipSuccess ||
-        hipStreamCreateWithPriority(&e->s_ssb, hipStreamNonBlocking, prio_ssb) != hipSuccess)
+    if (create_engine_stream(&e->s_own, 1, device, prio_main) != hipSuccess ||
+        create_engine_stream(&e->s_ssb, 2, device, prio_ssb) != hipSuccess)
         return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
     e->s_main = e->s_own;
     // lab: SDRG_CU_SPLIT = 1 (SSB on even CU-mask bits, spectrum/statistics on odd) or 2 (low / high half): the
@@ -882,7 +931,10 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         return (v && atoi(v) == 1) ? (unsigned)hipEventDisableTiming
                                    : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
     }();
-    if (hipStreamCreateWithFlags(&e->s_ap, hipStreamNonBlocking) != hipSuccess)
+    if (create_engine_stream(&e->s_ap, 8, device) != hipSuccess)
+        return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
+    if (queue_plan().eager &&
+        (create_engine_stream(&e->s_stats, 4, device) != hipSuccess || create_engine_stream(&e->s_gather, 16, device) != hipSuccess))
         return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
     hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join, &e->ev_in_main, &e->ev_in_ssb, &e->ev_ap_end[0], &e->ev_ap_end[1],
                          &e->ev_ap_end[2]};
@@ -916,8 +968,10 @@ int32_t sdrg_engine_destroy(sdrg_engine *e) {
         if (ev) (void)hipEventDestroy(ev);
     if (e->s_gather) (void)hipStreamSynchronize(e->s_gather);
     hipEvent_t evs[] = {e->ev_fork, e->ev_join, e->ev_in_main, e->ev_in_ssb, e->ev_fork_spec, e->ev_join_spec,
-                        e->ev_spec_done, e->ev_ap_end[0], e->ev_ap_end[1], e->ev_ap_end[2], e->ev_gather};
+                        e->ev_spec_done, e->ev_ap_end[0], e->ev_ap_end[1], e->ev_ap_end[2]};
     for (hipEvent_t ev : evs)
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : e->ev_g)  // ev_gather is one of these
         if (ev) (void)hipEventDestroy(ev);
     for (auto &r : e->ring) {
         hipEvent_t rev[] = {r.t0, r.spec, r.stats, r.ssb0, r.ssb1, r.end};
@@ -1102,7 +1156,7 @@ int32_t sdrg_engine_set_pipelining(sdrg_engine *e, int32_t on) {
         HIP_TRY(hipStreamWaitEvent(e->s_main, e->last_stats_end, 0));
     if (async) {  // created lazily, each handle on its own: a failed earlier attempt leaves no null behind in use
         const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
-        if (!e->s_stats) HIP_TRY(hipStreamCreateWithFlags(&e->s_stats, hipStreamNonBlocking));
+        if (!e->s_stats) HIP_TRY(create_engine_stream(&e->s_stats, 4, e->device));
         if (!e->ev_spec_done) HIP_TRY(hipEventCreateWithFlags(&e->ev_spec_done, fl));
         for (hipEvent_t &ev : e->ev_stats_end)
             if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, fl));
@@ -1400,8 +1454,9 @@ int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdr
         if (rc) return rc;
     }
     if (!(g_rec || g_foc || g_spec || g_pcm)) return SDRG_OK;
-    if (!e->s_gather) HIP_TRY(hipStreamCreateWithFlags(&e->s_gather, hipStreamNonBlocking));
-    if (!e->ev_gather) HIP_TRY(hipEventCreateWithFlags(&e->ev_gather, hipEventDisableTiming | hipEventDisableSystemFence));
+    if (!e->s_gather) HIP_TRY(create_engine_stream(&e->s_gather, 16, e->device));
+    const int slot = (int)(e->g_calls % sdrg_engine::GRING);
+    if (!e->ev_g[slot]) HIP_TRY(hipEventCreateWithFlags(&e->ev_g[slot], hipEventDisableTiming | hipEventDisableSystemFence));
     hipStream_t s = e->s_gather;
     if ((g_rec || g_foc || g_spec) && e->last_in_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));
     if (g_rec && e->stats_async && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));
@@ -1417,13 +1472,20 @@ int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdr
     if (g_pcm) items[k++] = {b->pcm, b->pcm_out, B * (size_t)plen * sizeof(int16_t)};
     int32_t rc = dist_gather(d, items, k, root, s);
     if (rc) return rc;
-    HIP_TRY(hipEventRecord(e->ev_gather, s));
-    // the buffers the gathers in flight read (a gather's own focus staging is reused only by the next gather, which
-    // follows it on s_gather); ev_gather covers every earlier gather too
+    HIP_TRY(hipEventRecord(e->ev_g[slot], s));
+    e->ev_gather = e->ev_g[slot];
+    e->g_calls++;
+    // the buffers this gather reads (its own focus staging is reused only by the next gather, which follows it on
+    // s_gather), mapped to its slot; a slot re-recorded by a later gather still covers this one (same stream)
     const void *read[] = {g_rec ? (const void *)b->records : nullptr, g_foc ? (const void *)b->focus_spectra : nullptr,
                           g_spec ? (const void *)b->spectra : nullptr, g_pcm ? (const void *)b->pcm : nullptr};
-    for (const void *r : read)
-        if (r && !e->gathering(r)) e->g_bufs.push_back(r);
+    for (const void *r : read) {
+        if (!r) continue;
+        bool found = false;
+        for (sdrg_engine::GBuf &g : e->g_bufs)
+            if (g.p == r) g.slot = slot, found = true;
+        if (!found) e->g_bufs.push_back({r, slot});
+    }
     return SDRG_OK;
 }
 

@@ -314,6 +314,10 @@ namespace k16 {
 #define SDRG_K16_ABLATE 0
 #endif
 constexpr int ABL = SDRG_K16_ABLATE;
+#ifndef SDRG_K16_ALONE_X1  // lab: the alone kernel with the cross-wave first exchange (isolates the occupancy)
+#define SDRG_K16_ALONE_X1 0
+#endif
+constexpr bool K16_ALONE_X1 = SDRG_K16_ALONE_X1;
 
 constexpr int LOG2N = 14, N = 1 << LOG2N, T = N / E, HALF = N / 2;
 constexpr int XCH_F2 = HALF;              // half-frame exchange buffer, f2 slots (XOR-swizzled, no padding)
@@ -386,6 +390,67 @@ __device__ __forceinline__ void exch2(f2 *lds, f2 (&v)[E]) {
     for (int i = 0; i < E; ++i) v[i] = nxt[i];
 }
 
+// ---- the spectrum-alone layout (spectrum16k_alone_kernel): pass 0 on half-waves ----
+// Pass 0 thread 32 h + a (half-wave h, lane a) holds x[16 a + h + 512 r]: the inputs of the current kernel's thread
+// 16 a + h, so the same radix-32 codelet gives the same values.  Pass 1 needs, in lane c of half-wave h, the pass-0
+// outputs c of the 32 lanes a of the SAME half-wave: the first exchange becomes a 32 x 32 transpose inside a wave,
+// through the wave's own 16 KiB of the (full-frame) exchange buffer, with no workgroup barrier.  The block of
+// half-wave h is the buffer's row h of the second exchange, which half-wave h writes itself, so the two uses of
+// the buffer never overlap between waves.  Same exch1 swizzle: slot 32 a + c at 32 a + (c ^ 2 (a mod 16)).
+__device__ __forceinline__ void transpose_local(f2 *lds, f2 (&v)[E]) {
+    const int t = threadIdx.x, l = t & 31;
+    f2 *blk = lds + 1024 * (t >> 5);
+    char *lb = reinterpret_cast<char *>(blk);
+    int row = 256 * l + ((l & 15) << 4);
+    asm volatile("" : "+v"(row));
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        *reinterpret_cast<float4 *>(lb + (row ^ (q << 4))) = pair4(v[2 * q], v[2 * q + 1]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // one wave writes and reads its block: LDS executes a wave's instructions in order, so no barrier; the
+    // compiler keeps the reads behind the writes (they alias the same block)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = blk[32 * r + (l ^ (2 * (r & 15)))];
+}
+
+// lab (SDRG_K16_ALONE_X1=1): the first exchange over the whole frame, cross-wave as in exch1 (two barriers)
+__device__ __forceinline__ void exch1_full(f2 *lds, f2 (&v)[E]) {
+    const int t = threadIdx.x;
+    char *lb = reinterpret_cast<char *>(lds);
+    int row = 256 * t + ((t & 15) << 4);
+    asm volatile("" : "+v"(row));
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        *reinterpret_cast<float4 *>(lb + (row ^ (q << 4))) = pair4(v[2 * q], v[2 * q + 1]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    const f2 *rb = lds + (t ^ (2 * ((t >> 5) & 15)));
+#pragma unroll
+    for (int r = 0; r < 32; ++r) v[r] = rb[512 * r];
+    __syncthreads();
+}
+
+// the second exchange over the whole frame (exch2 with both halves at once): two barriers per frame
+__device__ __forceinline__ void exch2_full(f2 *lds, f2 (&v)[E]) {
+    const int t = threadIdx.x;
+    int row = (t >> 5) * 1024 + (t & 31);
+    asm volatile("" : "+v"(row));
+#pragma unroll
+    for (int r = 0; r < 32; ++r) lds[(row ^ (2 * (r & 15))) + 32 * r] = v[r];
+    __syncthreads();
+    const float4 *rb = reinterpret_cast<const float4 *>(lds + ((2 * t) ^ (2 * ((t >> 4) & 15))));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const float4 p = rb[512 * r];  // slots 2t, 2t + 1 of row 1024 r
+        v[r] = f2{p.x, p.y};
+        v[16 + r] = f2{p.z, p.w};
+    }
+    __syncthreads();
+}
+
 // raw samples x[t + 512 r] of frame f into registers (zero-extended 16/32-bit words); live = false gives a
 // zero-sized resource, so the loads return 0 without touching memory
 template <int FMT>
@@ -397,15 +462,17 @@ __device__ __forceinline__ void issue_raw(const void *iq, int f, int t, uint32_t
     for (int r = 0; r < E; ++r) raw[r] = load_raw_word<FMT>(rs, t * BPS, r * (N / 32) * BPS);
 }
 
-// __launch_bounds__(512, 4): four waves per SIMD = two workgroups per CU, so at most 128 VGPRs
-template <int FMT>
-__global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restrict__ iq, float *__restrict__ spectra,
-                                                           const float *__restrict__ tabs, int n_frames) {
+// ALONE: the spectrum-alone layout (full-frame exchange buffer, pass 0 on half-waves, see transpose_local)
+template <int FMT, bool ALONE>
+__device__ __forceinline__ void spectrum16k_body(const void *__restrict__ iq, float *__restrict__ spectra,
+                                                 const float *__restrict__ tabs, int n_frames) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int XB = (ALONE ? N : XCH_F2) * 8;  // exchange buffer bytes
     f2 *xch = reinterpret_cast<f2 *>(smem);
-    f2 *p1 = reinterpret_cast<f2 *>(smem + XCH_F2 * 8);
-    float4 *a2 = reinterpret_cast<float4 *>(smem + XCH_F2 * 8 + P1_F2 * 8);
+    f2 *p1 = reinterpret_cast<f2 *>(smem + XB);
+    float4 *a2 = reinterpret_cast<float4 *>(smem + XB + P1_F2 * 8);
     const int t = threadIdx.x;
+    const int src = ALONE && !K16_ALONE_X1 ? 16 * (t & 31) + (t >> 5) : t;  // pass 0 reads x[src + 512 r]
     for (int i = t; i < P1_F2; i += T) p1[i] = reinterpret_cast<const f2 *>(tabs)[i];
     for (int i = t; i < A2_F4; i += T) a2[i] = reinterpret_cast<const float4 *>(tabs + 2 * P1_F2)[i];
     __syncthreads();
@@ -415,7 +482,7 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
     constexpr bool STAGE = FMT != SDRG_IQ_CF32;  // CF32 (8 B/sample) loads at the top of the iteration
     uint32_t raw[E];
     if constexpr (STAGE) {
-        issue_raw<FMT>(iq, (int)blockIdx.x < n_frames ? blockIdx.x : 0, t, raw, (int)blockIdx.x < n_frames);
+        issue_raw<FMT>(iq, (int)blockIdx.x < n_frames ? blockIdx.x : 0, src, raw, (int)blockIdx.x < n_frames);
         // opaque words into the frame loop: with the loop's own loads zero-extended too, the compiler would hoist the
         // zero-extension behind the loop's phi and spend a v_and per word per frame on it (once here, before the loop)
 #pragma unroll
@@ -431,18 +498,25 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
         } else {
             const __amdgpu_buffer_rsrc_t rs = frame_rsrc(reinterpret_cast<const char *>(iq) + (size_t)frame * N * BPS, N * BPS);
 #pragma unroll
-            for (int r = 0; r < E; ++r) v[r] = load_unscaled<FMT>(rs, t * BPS, r * (N / 32) * BPS);
+            for (int r = 0; r < E; ++r) v[r] = load_unscaled<FMT>(rs, src * BPS, r * (N / 32) * BPS);
         }
         const int next = frame + gridDim.x;
         if constexpr (!(ABL & 8)) dft<32>(v);
-        if constexpr (!(ABL & 4)) exch1(xch, v);
+        if constexpr (!(ABL & 4)) {
+            if constexpr (ALONE && K16_ALONE_X1) exch1_full(xch, v);
+            else if constexpr (ALONE) transpose_local(xch, v);
+            else exch1(xch, v);
+        }
         // ---- pass 1: radix 32, NS = 32 ----
         if constexpr (!(ABL & 1)) {
 #pragma unroll
             for (int r = 1; r < 32; ++r) v[r] = cmul_v(v[r], p1_row[r * 32]);
         }
         if constexpr (!(ABL & 8)) dft<32>(v);
-        if constexpr (!(ABL & 4)) exch2(xch, v);
+        if constexpr (!(ABL & 4)) {
+            if constexpr (ALONE) exch2_full(xch, v);
+            else exch2(xch, v);
+        }
         // ---- pass 2: radix 16, NS = 1024, butterflies j = 2t + b held as v[16 b + r] ----
         if constexpr (!(ABL & 2)) {
             f2 wa, wb;  // w_16384^j for j = 2t, 2t + 1
@@ -495,7 +569,7 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
             asm("v_fma_f32 %0, %1, %1, %2" : "=v"(p1) : "v"(x1[r].x), "v"(q1));
             pw[r] = f2s{p0, p1};
         }
-        if constexpr (STAGE) issue_raw<FMT>(iq, next < n_frames ? next : frame, t, raw, next < n_frames);
+        if constexpr (STAGE) issue_raw<FMT>(iq, next < n_frames ? next : frame, src, raw, next < n_frames);
         float *o = spectra + (size_t)frame * N + 2 * t;
         if constexpr (ABL & 16) {  // keep the values live without the stores
             float acc = 0.f;
@@ -512,6 +586,23 @@ __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restric
                                                       4 * ((r * 1024 + N / 2) & (N - 1)), 2 /* nt */);
         }
     }
+}
+
+// __launch_bounds__(512, 4): four waves per SIMD = two workgroups per CU, so at most 128 VGPRs
+template <int FMT>
+__global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restrict__ iq, float *__restrict__ spectra,
+                                                           const float *__restrict__ tabs, int n_frames) {
+    spectrum16k_body<FMT, false>(iq, spectra, tabs, n_frames);
+}
+
+// The spectrum-alone kernel (no SSB pipeline beside it): one workgroup per CU with the full-frame exchange buffer,
+// two barriers per frame instead of eight.  Same operations on the same values as spectrum16k_kernel: same bits.
+constexpr int LDS_ALONE_BYTES = N * 8 + P1_F2 * 8 + A2_F4 * 16;
+static_assert(LDS_ALONE_BYTES <= 160 * 1024, "one workgroup per CU");
+template <int FMT>
+__global__ __launch_bounds__(T, 2) void spectrum16k_alone_kernel(const void *__restrict__ iq, float *__restrict__ spectra,
+                                                                 const float *__restrict__ tabs, int n_frames) {
+    spectrum16k_body<FMT, true>(iq, spectra, tabs, n_frames);
 }
 
 // the two LDS tables, laid out as the kernel reads them (exp evaluated in double, rounded once)
@@ -541,21 +632,24 @@ int device_cus() {
     return cus;
 }
 
-// wg_per_cu: persistent workgroups per CU (2 alone; 1 when the SSB pipeline shares the CUs, see launch_spectrum)
+// wg_per_cu: persistent workgroups per CU (2 alone; 1 when the SSB pipeline shares the CUs, see launch_spectrum);
+// 0 = the spectrum-alone kernel (one workgroup per CU, full-frame exchange)
 template <int FMT>
 hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectra, hipStream_t s, int wg_per_cu = 2,
                   int n_cus = 0) {
-    auto k = spectrum16k_kernel<FMT>;
-    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(k), LDS_BYTES);
+    const bool alone = wg_per_cu == 0;
+    auto k = alone ? spectrum16k_alone_kernel<FMT> : spectrum16k_kernel<FMT>;
+    const int lds = alone ? LDS_ALONE_BYTES : LDS_BYTES;
+    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(k), lds);
     if (e != hipSuccess) return e;
     static const int max_grid = [] {  // lab override (SDRG_SPECTRUM_GRID): persistent workgroups
         const char *v = lab_getenv("SDRG_SPECTRUM_GRID");
         const int g = v ? atoi(v) : 0;
         return g > 0 ? g : 0;
     }();
-    const int cap = max_grid > 0 ? max_grid : (wg_per_cu == 1 ? 1 : 2) * (n_cus > 0 ? n_cus : device_cus());
+    const int cap = max_grid > 0 ? max_grid : (wg_per_cu == 2 ? 2 : 1) * (n_cus > 0 ? n_cus : device_cus());
     const int grid = n_frames < cap ? n_frames : cap;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(T), LDS_BYTES, s, iq, spectra, tabs, n_frames);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(T), lds, s, iq, spectra, tabs, n_frames);
     return hipGetLastError();
 }
 
@@ -959,6 +1053,18 @@ size_t spectrum_scratch_floats(int n, int n_frames) {
     return (size_t)wave * n * 2;
 }
 
+// N = 16384 with no SSB pipeline beside it: the two-workgroup kernel (2).  The spectrum-alone kernel (0: one
+// workgroup per CU, two barriers per frame, the same bits) measured 187 us per 4096 CS8 frames against 111 us (DESIGN
+// §3.1, round 5) and is a lab option only: SDRG_K16_ALONE=1 (lab builds).
+static int k16_alone_mode(int fmt) {
+    static const int forced = [] {
+        const char *v = lab_getenv("SDRG_K16_ALONE");
+        return v ? atoi(v) : -1;
+    }();
+    (void)fmt;
+    return forced > 0 ? 0 : 2;
+}
+
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles, float *spectra,
                            float *scratch, hipStream_t stream, bool beside_ssb, int n_cus, bool beside_wide_stats) {
     if (n_frames <= 0) return hipSuccess;
@@ -971,7 +1077,7 @@ hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const f
         return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream,
                                           !beside_wide_stats, !beside_ssb);
     case 16384: return k16::launch_fmt(iq, fmt, n_frames, twiddles + spectrum_k16_tables_offset(), spectra, stream,
-                                      beside_ssb ? 1 : 2, n_cus);
+                                      beside_ssb ? 1 : k16_alone_mode(fmt), n_cus);
     case 64: return launch_n<6>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 128: return launch_n<7>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 256: return launch_n<8>(iq, fmt, n_frames, twiddles, spectra, stream);

@@ -65,6 +65,9 @@ constexpr size_t front_lds_bytes() {
 
 // Lab (SDRG_SSB64_STAMPS): per wave, the cycles of its own work (body to its last LDS operation) and of its whole
 // loop, at stamps[(group * 16 + slot) * 2 + {0, 1}] (front roles in slots 0-3, back roles in 4-15); null: nothing runs
+#ifndef SSB64_SKIP_LOAD  // lab diagnostic (wrong results): the loader does no work, so the front's loop shows the
+#define SSB64_SKIP_LOAD 0  // serial roles' own rate
+#endif
 #define SSB64_WORK_BEGIN() const unsigned long long st_a_ = stamps ? __builtin_amdgcn_s_memtime() : 0
 #define SSB64_WORK_END()                                                                                       \
     do {                                                                                                       \
@@ -162,9 +165,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(FRONT_T, FRONT_T))) void s
             }
         };
         for (int c = 0; c < NRW - 1 && c < nch && !SSB64_SKIP_LOAD; c++) issue(c);
-#ifndef SSB64_SKIP_LOAD  // lab diagnostic (wrong results): the loader does no work, so the front's loop shows the
-#define SSB64_SKIP_LOAD 0  // serial roles' own rate
-#endif
         for (int it = 0; it < nit; ++it) {
             SSB64_WORK_BEGIN();
             if (it < nch && !SSB64_SKIP_LOAD) {
