@@ -45,6 +45,8 @@ ALG_BYTES_PER_SAMPLE = {"spectrum": 6.0}  # CS8: 2 B in + 4 B fftshifted float32
 ISO_LAUNCHES = 30  # launches of the spectrum stage alone behind roofline_isolated
 N_INPUTS = 3  # distinct input batches rotated per step: 3 x 128 MiB > the 256 MiB Infinity Cache
 SSB_ISO_CALLS = 20  # joined SSB-only calls timed for ssb_latency_floor.ssb_ms_alone
+LAB_HOST_TIMES = os.environ.get("SDRG_BENCH_HOST_TIMES") == "1"
+LAB_HOST_DELAY = float(os.environ.get("SDRG_BENCH_HOST_DELAY_US", "0")) * 1e-6
 LAB_NO_STEP_GATHER = os.environ.get("SDRG_BENCH_NO_STEP_GATHER") == "1"  # lab: the N > 1 path without its per-step gathers
 N_OUTPUTS = 3  # spectra / records buffers rotated per step (asynchronous statistics read a call's spectra late)
 # SSB floor: the sample-serial low-pass wave's own instruction issue.  Per sample it issues 6 VALU instructions
@@ -388,7 +390,12 @@ def main() -> int:
         uid = [sdrg.dist_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         dcomm = sdrg.Dist(uid[0], world, rank, device=local)
-        ranks_info["rccl_version"] = dcomm.info()["rccl_version"]
+        if os.environ.get("SDRG_BENCH_ONE_RANK_RCCL") == "1":  # lab: RCCL's one-rank kernel instead of device copies
+            dcomm.set_one_rank_rccl(True)
+        di = dcomm.info()
+        ranks_info["rccl_version"] = di["rccl_version"]
+        # one rank: device copies unless set_one_rank_rccl (RCCL's one-rank kernel slows the pipeline: DESIGN 7)
+        ranks_info["gather_data_path"] = "rccl" if di["rccl_data"] else "device copies (one rank)"
     elif rehearse:
         # the engine enqueues on a torch stream, so the host-staged gathers' copies follow each step's kernels
         work_stream = torch.cuda.Stream(dev)
@@ -396,6 +403,7 @@ def main() -> int:
         eng.set_stream(work_stream.cuda_stream)
 
     calls = [0]
+    host_t = [0.0, 0.0, 0]  # lab (SDRG_BENCH_HOST_TIMES=1): host seconds in process_device, in gather; calls
 
     def ptr(t):
         return t.data_ptr() if t is not None else None
@@ -407,13 +415,16 @@ def main() -> int:
         if focus and f_stages is not None:
             f_stage = f_stages[calls[0] % N_OUTPUTS]
         calls[0] += 1
+        h0 = time.perf_counter()
         eng.process_device(iq.data_ptr(), fmt, stages if st is None else st, spec.data_ptr(), rec.data_ptr(),
                            pcm.data_ptr(), now[0])
+        h1 = time.perf_counter()
         now[0] += n // 2000  # frame duration in ms at 2 Msps (8 ms for 16384)
-        if capi and not LAB_NO_STEP_GATHER:  # one RCCL group on the engine's gather stream, after this step's outputs
-            eng.gather(dcomm, 0, records=rec.data_ptr(), records_out=ptr(gathered),
-                       focus_spectra=spec.data_ptr() if focus else None, focus_out=ptr(f_out),
-                       pcm=pcm.data_ptr() if gather_pcm else None, pcm_out=ptr(p_out))
+        if capi:  # one gather group behind this step's outputs, on the stream that produced them (sdrg_engine_gather)
+            if not LAB_NO_STEP_GATHER:
+                eng.gather(dcomm, 0, records=rec.data_ptr(), records_out=ptr(gathered),
+                           focus_spectra=spec.data_ptr() if focus else None, focus_out=ptr(f_out),
+                           pcm=pcm.data_ptr() if gather_pcm else None, pcm_out=ptr(p_out))
         elif dist_on:
             shard.gather_records(host(rec), world, rank, dst=0, out=gathered)  # records (peaks, stats) to rank 0
             if gather_pcm:
@@ -424,6 +435,14 @@ def main() -> int:
                     shard.gather_records(f_stage.cpu(), world, rank, dst=0, out=f_out)
                 else:
                     shard.gather_focus(spec, f_lo, f_n, world, rank, dst=0, out=f_out, staging=f_stage)
+        if LAB_HOST_DELAY > 0:  # lab: a busy host delay in place of the gather call
+            t_end = time.perf_counter() + LAB_HOST_DELAY
+            while time.perf_counter() < t_end:
+                pass
+        if LAB_HOST_TIMES:
+            host_t[0] += h1 - h0
+            host_t[1] += time.perf_counter() - h1
+            host_t[2] += 1
 
     # the inputs are generated before the timed region and synchronised, so they are complete at every call.  The
     # host-staged rehearsal copies the PCM on the main stream, so its per-step PCM gather needs the joined schedule
@@ -458,13 +477,17 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host_t[:] = [0.0, 0.0, 0]
     for _ in range(args.steps):
         step()
-    eng.synchronize()  # every step's gathers (on the engine's main stream) complete inside the timed region
+    eng.synchronize()  # every step's gathers (on the engine's streams) complete inside the timed region
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if LAB_HOST_TIMES and host_t[2]:
+        log(f"bench: host us per step: process_device {host_t[0] / host_t[2] * 1e6:.1f}, gather "
+            f"{host_t[1] / host_t[2] * 1e6:.1f} over {host_t[2]} timed calls")
     spectra_gather = None
     if dist_on and args.spectra_gather_steps > 0:
         # the full spectra of every frame (fftCallback payload) to rank 0, timed on its own: outside the metric
@@ -718,8 +741,9 @@ def main() -> int:
     if ranks_info:
         out.update(ranks_info)
     if dist_on:
-        out["gather_mode"] = ("sdrg_engine_gather: one RCCL group per step on the engine's main stream after the step's "
-                              "outputs (no host synchronisation); the next step's kernels follow it" if capi else
+        out["gather_mode"] = ("sdrg_engine_gather: one gather group per step behind the step's outputs on the stream "
+                              "that produced them (the statistics stream when asynchronous), no host synchronisation; "
+                              "RCCL ncclGather at N > 1, device copies on one rank" if capi else
                               "host-staged gloo gathers (rehearsal)")
     if spectra_gather:
         out["spectra_gather"] = spectra_gather

@@ -496,8 +496,13 @@ int32_t sdrg_dist_unique_id(void *id, int32_t bytes);
 /* ncclCommInitRank on `device` (collective: every rank of the job calls it with the same id). */
 int32_t sdrg_dist_create(const void *id, int32_t world_size, int32_t rank, int32_t device, sdrg_dist **out);
 int32_t sdrg_dist_destroy(sdrg_dist *d);
-/* Rank, world size and the RCCL version in use (any pointer may be NULL). */
-int32_t sdrg_dist_info(const sdrg_dist *d, int32_t *rank, int32_t *world_size, int32_t *rccl_version);
+/* Rank, world size, the RCCL version in use and whether the gathers move their bytes through RCCL (1) or, for a
+ * one-rank communicator, as device copies on the gather stream (0).  Any pointer may be NULL. */
+int32_t sdrg_dist_info(const sdrg_dist *d, int32_t *rank, int32_t *world_size, int32_t *rccl_version,
+                       int32_t *rccl_data);
+/* A one-rank communicator's gathers are device copies by default (RCCL's one-rank gather kernel runs beside the SSB
+ * pipeline and slows the step: DESIGN.md §7); on = 1 routes them through ncclGather as at world size > 1. */
+int32_t sdrg_dist_set_one_rank_rccl(sdrg_dist *d, int32_t on);
 
 /* What one gather moves.  Each selected pair gathers this rank's n_streams rows to the root's output, which
  * holds world_size x n_streams rows in rank order (= global stream order); the *_out pointers are read on the

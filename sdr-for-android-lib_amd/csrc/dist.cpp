@@ -73,7 +73,14 @@ int32_t rccl_fail(const RcclApi &a, ncclResult_t r, const char *what) {
 struct sdrg_dist {
     ncclComm_t comm = nullptr;
     int rank = 0, world = 0, device = 0;
+    bool rccl_data = true;  // the gathers go through RCCL (false: a one-rank communicator's device copies)
 };
+
+// A one-rank gather is a copy.  RCCL runs it as its generic kernel (5 workgroups, 141 us on average beside the SSB
+// pipeline in bench.py --process-group, rocprofv3 r5p), whose waves slow the CUs they land on, and a persistent pipeline
+// runs at its slowest CU's pace: the c3 step +2.8 % for the 288-KB records gather.  So at world size 1 the gathers are
+// hipMemcpyAsync device copies on the same stream (a ~3 us blit); sdrg_dist_set_one_rank_rccl(d, 1) keeps RCCL there
+// too (tests/test_gpu_dist_capi.py runs both).
 
 int32_t sdrg::dist_gather(sdrg_dist *d, const GatherItem *items, int n_items, int root, hipStream_t stream) {
     const RcclApi &a = rccl();
@@ -82,6 +89,14 @@ int32_t sdrg::dist_gather(sdrg_dist *d, const GatherItem *items, int n_items, in
     for (int i = 0; i < n_items; i++)
         if (!items[i].send || (d->rank == root && !items[i].recv))
             return fail(SDRG_E_INVALID, "gather item %d: null %s buffer", i, items[i].send ? "receive" : "send");
+    if (!d->rccl_data) {  // world size 1: the root's own blocks
+        for (int i = 0; i < n_items; i++)
+            if (items[i].bytes && items[i].recv != items[i].send) {
+                hipError_t e = hipMemcpyAsync(items[i].recv, items[i].send, items[i].bytes, hipMemcpyDeviceToDevice, stream);
+                if (e != hipSuccess) return fail(SDRG_E_HIP, "hipMemcpyAsync: %s", hipGetErrorString(e));
+            }
+        return SDRG_OK;
+    }
     // one group: every selected gather goes out as one RCCL launch on the stream
     ncclResult_t r = a.group_start();
     if (r != ncclSuccess) return rccl_fail(a, r, "ncclGroupStart");
@@ -137,6 +152,7 @@ int32_t sdrg_dist_create(const void *id, int32_t world_size, int32_t rank, int32
         return rccl_fail(a, r, "ncclCommInitRank");
     }
     d->rank = rank;
+    d->rccl_data = world_size > 1;
     d->world = world_size;
     d->device = device;
     *out = d;
@@ -153,8 +169,10 @@ int32_t sdrg_dist_destroy(sdrg_dist *d) {
     return SDRG_OK;
 }
 
-int32_t sdrg_dist_info(const sdrg_dist *d, int32_t *rank, int32_t *world_size, int32_t *rccl_version) {
+int32_t sdrg_dist_info(const sdrg_dist *d, int32_t *rank, int32_t *world_size, int32_t *rccl_version,
+                       int32_t *rccl_data) {
     if (!d) return fail(SDRG_E_INVALID, "null dist");
+    if (rccl_data) *rccl_data = d->rccl_data ? 1 : 0;
     if (rank) *rank = d->rank;
     if (world_size) *world_size = d->world;
     if (rccl_version) {
@@ -163,6 +181,12 @@ int32_t sdrg_dist_info(const sdrg_dist *d, int32_t *rank, int32_t *world_size, i
         if (a.get_version) (void)a.get_version(&v);
         *rccl_version = v;
     }
+    return SDRG_OK;
+}
+
+int32_t sdrg_dist_set_one_rank_rccl(sdrg_dist *d, int32_t on) {
+    if (!d) return fail(SDRG_E_INVALID, "null dist");
+    d->rccl_data = d->world > 1 || on != 0;
     return SDRG_OK;
 }
 

@@ -182,7 +182,9 @@ struct sdrg_engine {
     // sdrg_engine_gather runs on a stream of its own after the outputs it reads; a later call that writes a buffer
     // still being gathered (same pointer) waits for the gather on the GPU first, so a caller rotating its output
     // buffers never delays its next call's kernels behind a gather
-    hipStream_t s_gather = nullptr;
+    bool last_async_stats = false;  // the last call with a statistics stage ran it on s_stats
+    hipStream_t s_gather = nullptr;   // lab (SDRG_GATHER_STREAM=1): the gathers on a stream of their own
+    hipStream_t s_last_gather = nullptr;  // the stream of the last gather
     hipEvent_t ev_gather = nullptr;  // the last gather's end (wait_outputs, synchronize)
     // each gather's end in a ring; a buffer a gather read maps to that gather's slot, so a call that rewrites it waits
     // for that gather only (waiting on the last gather instead made call k + 3's spectrum wait for gather k + 2, and
@@ -744,6 +746,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
                             e->g_bufs.end());
     if (do_spec) e->last_in_main = mk_main_end;
     if (do_ssb) e->last_in_ssb = mk_ssb_end;
+    if (do_spec || do_stats) e->last_async_stats = do_stats && async;
     return SDRG_OK;
 }
 
@@ -933,9 +936,14 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
     }();
     if (create_engine_stream(&e->s_ap, 8, device) != hipSuccess)
         return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
-    if (queue_plan().eager &&
-        (create_engine_stream(&e->s_stats, 4, device) != hipSuccess || create_engine_stream(&e->s_gather, 16, device) != hipSuccess))
-        return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
+    // the statistics stream is created with the engine's other streams: HIP shares GPU_MAX_HW_QUEUES hardware queues
+    // among a process's streams by creation order, and created later (after another library's streams, e.g. RCCL's at
+    // communicator init) it landed on the main stream's queue, where the asynchronous statistics ran in line with the
+    // spectrum (rocprofv3 r5p: --process-group 0.3136 vs 0.3029 ms per step)
+    if (create_engine_stream(&e->s_stats, 4, device) != hipSuccess) return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
+    if (const char *v = lab_getenv("SDRG_GATHER_STREAM"))
+        if (atoi(v) == 1 && create_engine_stream(&e->s_gather, 16, device) != hipSuccess)
+            return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
     hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join, &e->ev_in_main, &e->ev_in_ssb, &e->ev_ap_end[0], &e->ev_ap_end[1],
                          &e->ev_ap_end[2]};
     static_assert(sdrg_pulse_bank::NEW_SETS == 3, "ev_ap_end creation");
@@ -1285,7 +1293,7 @@ int32_t sdrg_engine_synchronize(sdrg_engine *e) {
     HIP_TRY(hipStreamSynchronize(e->s_ssb));  // not joined into s_main when pipelined
     if (e->s_stats) HIP_TRY(hipStreamSynchronize(e->s_stats));  // SDRG_PIPELINE_STATS_ASYNC
     HIP_TRY(hipStreamSynchronize(e->s_ap));                      // the audio pulse detector
-    if (e->s_gather) HIP_TRY(hipStreamSynchronize(e->s_gather));  // sdrg_engine_gather
+    if (e->s_gather) HIP_TRY(hipStreamSynchronize(e->s_gather));
     static const bool stamps = [] {
         const char *v = lab_getenv("SDRG_PIPE_STAMPS");
         return v && v[0] == '1';
@@ -1427,10 +1435,13 @@ int32_t sdrg_engine_get_timing_stats(const sdrg_engine *ce, sdrg_timings *mean, 
     return SDRG_OK;
 }
 
-// Multi-GPU gather (include/sdrg.h; dist.cpp holds RCCL).  The gathers run on s_gather after the outputs they read --
-// the main stream's end marker (spectra; records of statistics on the main stream), the statistics' stream's last
-// event (records of asynchronous statistics), the SSB stream's end marker (PCM) -- so they delay none of the engine's
-// streams; a later call that writes a buffer still being gathered waits for ev_gather first (enqueue).
+// Multi-GPU gather (include/sdrg.h; dist.cpp holds RCCL).  A gather runs on the stream that produced what it reads, in
+// order behind it and with no cross-stream wait: the statistics stream when the last call ran its statistics there
+// (records, and the spectra its statistics already waited for), else the main stream; with PCM, the audio detector's
+// stream, which follows the SSB stream's end marker, waiting for the main or statistics stream's last marker.  (On a
+// stream of its own the gather's waits shared a hardware queue with the engine's streams: HIP maps a process's streams
+// onto GPU_MAX_HW_QUEUES queues, and a wait blocks the whole queue.)  A later call that writes a buffer a gather reads
+// waits for that gather's event first (enqueue).
 int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdrg_gather_buffers *b) {
     if (!e || !d || !b) return fail(SDRG_E_INVALID, "null argument");
     if (dist_device(d) != e->device)
@@ -1454,13 +1465,25 @@ int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdr
         if (rc) return rc;
     }
     if (!(g_rec || g_foc || g_spec || g_pcm)) return SDRG_OK;
-    if (!e->s_gather) HIP_TRY(create_engine_stream(&e->s_gather, 16, e->device));
     const int slot = (int)(e->g_calls % sdrg_engine::GRING);
     if (!e->ev_g[slot]) HIP_TRY(hipEventCreateWithFlags(&e->ev_g[slot], hipEventDisableTiming | hipEventDisableSystemFence));
-    hipStream_t s = e->s_gather;
-    if ((g_rec || g_foc || g_spec) && e->last_in_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));
-    if (g_rec && e->stats_async && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));
-    if (g_pcm && e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
+    const bool on_stats = !g_pcm && e->last_async_stats && !e->s_gather;
+    hipStream_t s = e->s_gather ? e->s_gather : g_pcm ? e->s_ap : on_stats ? e->s_stats : e->s_main;
+    if (e->s_gather) {  // lab: waits for every producer
+        if ((g_rec || g_foc || g_spec) && e->last_in_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));
+        if (g_rec && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));
+        if (g_pcm && e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
+    } else if (g_pcm) {
+        if ((g_rec || g_foc || g_spec) && e->last_in_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));
+        if (g_rec && e->last_async_stats && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));
+        if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
+    }
+    // records an earlier call's asynchronous statistics wrote (the last call ran no statistics there)
+    if (!e->s_gather && !g_pcm && !on_stats && g_rec && e->last_stats_end)
+        HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));
+    // the focus staging buffer and RCCL's issue order: a gather follows the previous one even on another stream
+    if (e->ev_gather && s != e->s_last_gather) HIP_TRY(hipStreamWaitEvent(s, e->ev_gather, 0));
+    e->s_last_gather = s;
     GatherItem items[4];
     int k = 0;
     if (g_rec) items[k++] = {b->records, b->records_out, B * sizeof(sdrg_frame_record)};
@@ -1475,8 +1498,8 @@ int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdr
     HIP_TRY(hipEventRecord(e->ev_g[slot], s));
     e->ev_gather = e->ev_g[slot];
     e->g_calls++;
-    // the buffers this gather reads (its own focus staging is reused only by the next gather, which follows it on
-    // s_gather), mapped to its slot; a slot re-recorded by a later gather still covers this one (same stream)
+    // the buffers this gather reads, mapped to its slot; a slot re-recorded by a later gather still covers this one
+    // (gathers follow each other)
     const void *read[] = {g_rec ? (const void *)b->records : nullptr, g_foc ? (const void *)b->focus_spectra : nullptr,
                           g_spec ? (const void *)b->spectra : nullptr, g_pcm ? (const void *)b->pcm : nullptr};
     for (const void *r : read) {

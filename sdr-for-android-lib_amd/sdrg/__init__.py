@@ -99,7 +99,8 @@ EXPORTS = [
     "sdrg_ssb_processor_enqueue", "sdrg_ssb_processor_set_sound_mode", "sdrg_ssb_processor_set_pulse_config",
     "sdrg_ssb_processor_get_ambient_energy", "sdrg_ssb_processor_get_current_ratio", "sdrg_ssb_processor_drain",
     "sdrg_ssb_processor_counters",
-    "sdrg_dist_unique_id", "sdrg_dist_create", "sdrg_dist_destroy", "sdrg_dist_info", "sdrg_engine_gather",
+    "sdrg_dist_unique_id", "sdrg_dist_create", "sdrg_dist_destroy", "sdrg_dist_info", "sdrg_dist_set_one_rank_rccl",
+    "sdrg_engine_gather",
     "sdrg_engine_gather_records", "sdrg_engine_gather_focus", "sdrg_engine_gather_spectra", "sdrg_engine_gather_pcm",
     "sdrg_device_alloc", "sdrg_device_free", "sdrg_memcpy",
 ]
@@ -283,7 +284,9 @@ def load() -> ctypes.CDLL:
         "sdrg_dist_unique_id": (_I32, [P, _I32]),
         "sdrg_dist_create": (_I32, [P, _I32, _I32, _I32, ctypes.POINTER(P)]),
         "sdrg_dist_destroy": (_I32, [P]),
-        "sdrg_dist_info": (_I32, [P, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
+        "sdrg_dist_info": (_I32, [P, ctypes.POINTER(_I32), ctypes.POINTER(_I32), ctypes.POINTER(_I32),
+                                  ctypes.POINTER(_I32)]),
+        "sdrg_dist_set_one_rank_rccl": (_I32, [P, _I32]),
         "sdrg_engine_gather": (_I32, [P, P, _I32, ctypes.POINTER(_GatherBuffers)]),
         "sdrg_engine_gather_records": (_I32, [P, P, _I32, P, P]),
         "sdrg_engine_gather_focus": (_I32, [P, P, _I32, P, P]),
@@ -395,10 +398,15 @@ class Dist:
                "sdrg_dist_create")
         self._h, self.world_size, self.rank, self.device = h, world_size, rank, device
 
+    def set_one_rank_rccl(self, on: bool) -> None:
+        """One rank: gathers through ncclGather (True) or as device copies (False, the default)."""
+        _check(load().sdrg_dist_set_one_rank_rccl(self._h, 1 if on else 0), "sdrg_dist_set_one_rank_rccl")
+
     def info(self) -> dict:
-        r, w, v = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
-        _check(load().sdrg_dist_info(self._h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(v)), "sdrg_dist_info")
-        return {"rank": r.value, "world_size": w.value, "rccl_version": v.value}
+        r, w, v, x = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _check(load().sdrg_dist_info(self._h, ctypes.byref(r), ctypes.byref(w), ctypes.byref(v), ctypes.byref(x)),
+               "sdrg_dist_info")
+        return {"rank": r.value, "world_size": w.value, "rccl_version": v.value, "rccl_data": bool(x.value)}
 
     def close(self) -> None:
         if getattr(self, "_h", None):

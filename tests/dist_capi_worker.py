@@ -4,7 +4,7 @@ device memory from sdrg_device_alloc.  A one-rank RCCL communicator, a pipelined
 statistics) and STEPS calls with their gathers -- records, focus-window slices, full spectra and PCM -- enqueued
 after each call with no host synchronisation in the loop; the PCM buffer is shared by every call, so each gather must
 read it before the next call's SSB stage overwrites it.  A second, joined engine on the same inputs gives the
-expected outputs.  Prints one JSON line: {"ok": {...}, "torch_loaded": bool, "rccl_version": int}."""
+expected outputs.  Prints one JSON line: {"ok": {...}, "torch_loaded": bool, "rccl_version": int, "rccl_data": bool}."""
 import json
 import os
 import sys
@@ -43,6 +43,7 @@ def main() -> int:
     ref.close()
 
     dist = sdrg.Dist(sdrg.dist_unique_id(), 1, 0, device=0)
+    dist.set_one_rank_rccl(os.environ.get("DIST_CAPI_ONE_RANK_RCCL") == "1")
     info = dist.info()
     eng = sdrg.Engine(cfg, B, device=0)
     eng.set_pipelining(sdrg.PIPELINE_INPUTS_READY | sdrg.PIPELINE_STATS_ASYNC)
@@ -79,7 +80,7 @@ def main() -> int:
     eng.close()
     dist.close()
     print(json.dumps({"ok": ok, "torch_loaded": "torch" in sys.modules, "rccl_version": info["rccl_version"],
-                      "world": info["world_size"]}), flush=True)
+                      "world": info["world_size"], "rccl_data": info["rccl_data"]}), flush=True)
     return 0
 
 

@@ -1,10 +1,7 @@
 #!/bin/bash
-# r5n: does a one-rank RCCL communicator or gloo group in the process slow kernels that run alone?
+# r5x: the full GPU suite at HEAD (gathers on the producing stream, statistics stream created with the engine)
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-for i in 1 2; do
-  for d in "" rccl gloo both; do
-    SPEC_TIME_DIST=$d timeout -k 10 120 python tools/lab/spec_time.py 16384 cs8 4096 200 2>&1 | tail -1 || exit 1
-  done
-done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r5x_tests.log 2>&1 || { echo "tests FAILED"; grep -E "FAILED|Error|error" gpurun_out/r5x_tests.log | head -20; tail -30 gpurun_out/r5x_tests.log; exit 1; }
+tail -1 gpurun_out/r5x_tests.log
