@@ -1,7 +1,9 @@
 #!/bin/bash
-# r5x: the full GPU suite at HEAD (gathers on the producing stream, statistics stream created with the engine)
+# r5y: the default bench line with its labelled lines at HEAD (statistics stream created with the engine)
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r5x_tests.log 2>&1 || { echo "tests FAILED"; grep -E "FAILED|Error|error" gpurun_out/r5x_tests.log | head -20; tail -30 gpurun_out/r5x_tests.log; exit 1; }
-tail -1 gpurun_out/r5x_tests.log
+for i in 1 2; do
+  timeout -k 10 400 python bench.py > gpurun_out/r5y_bench$i.json 2> gpurun_out/r5y_bench$i.err || { tail gpurun_out/r5y_bench$i.err; exit 1; }
+  python tools/bench_summary.py gpurun_out/r5y_bench$i.json
+done
