@@ -826,6 +826,22 @@ __device__ __forceinline__ f2 convert_scaled(uint32_t v) {  // load_sample's val
     }
 }
 
+// Lab: the price of an in-launch hand-off of the intermediate Y, measured inside the persistent
+// four-step kernels without any waiting.  SDRG_FS_PUBLISH=1: every column tile publishes its Y slice the way a
+// producer must for another workgroup (plain stores, every wave's vmcnt(0), a barrier, lane 0's agent-scope release
+// fence, vmcnt(0), a relaxed agent flag store); =2: the write-through form (Y stored sc1, vmcnt(0), barrier, flag; no
+// fence).  SDRG_FS_ACQUIRE=1: every row tile begins as a consumer must (lane 0 reads the flag relaxed, agent-scope
+// acquire fence, vmcnt(0), barrier).  Results are unchanged (the flags are written and read, never waited on).
+#ifndef SDRG_FS_PUBLISH
+#define SDRG_FS_PUBLISH 0
+#endif
+#ifndef SDRG_FS_ACQUIRE
+#define SDRG_FS_ACQUIRE 0
+#endif
+#if SDRG_FS_PUBLISH || SDRG_FS_ACQUIRE
+__device__ unsigned g_fs_flags[1 << 16];
+#endif
+
 template <int LOG2N1, int LOG2N2, int FMT>
 __global__ __launch_bounds__(TILE_A) void four_step_a_p(const void *__restrict__ iq, f2 *__restrict__ Y,
                                                          const f2 *__restrict__ tw, int n_frames, int hi) {
@@ -883,10 +899,24 @@ __global__ __launch_bounds__(TILE_A) void four_step_a_p(const void *__restrict__
         auto noload = [](int, int) { return f2{0.0f, 0.0f}; };
         auto store = [&](int cc, int k1, f2 v) {
             const int n2 = c0 + cc;
-            y[k1 * N2 + n2] = cmul_v(v, tw_lds<1>(t_hi, t_lo, (n2 * k1) & (N - 1)));
+            const f2 w = cmul_v(v, tw_lds<1>(t_hi, t_lo, (n2 * k1) & (N - 1)));
+            if constexpr (SDRG_FS_PUBLISH == 2)
+                __hip_atomic_store(reinterpret_cast<unsigned long long *>(y + k1 * N2 + n2),
+                                   __builtin_bit_cast(unsigned long long, w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                y[k1 * N2 + n2] = w;
         };
         // pass 2 reads the tile, then a barrier (inside), so the next tile's pass-1 writes are safe
         tile_pass<N, N1, TP::RB, TP::RA, false, true, TILE_A>(lds, t_hi, t_lo, noload, store);
+#if SDRG_FS_PUBLISH
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if constexpr (SDRG_FS_PUBLISH == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&g_fs_flags[tile & 0xffff], (unsigned)tile + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#endif
     }
 }
 
@@ -912,6 +942,15 @@ __global__ __launch_bounds__(TILE_B) void four_step_b_p(const f2 *__restrict__ Y
     if (tile < total) issue(tile);
     for (; tile < total; tile += gridDim.x) {
         const int frame = tile / TPF, r0 = (tile % TPF) * C;
+#if SDRG_FS_ACQUIRE
+        if (threadIdx.x == 0) {
+            const unsigned seen = __hip_atomic_load(&g_fs_flags[tile & 0xffff], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (seen == 0xffffffffu) stage[0].x = 0.0f;  // keep the load
+        }
+        __syncthreads();
+#endif
 #pragma unroll
         for (int i = 0; i < S; ++i) {
             const int e = threadIdx.x + i * TILE_B;
