@@ -1408,6 +1408,17 @@ constexpr int MW_F = 4;                     // frames per workgroup
 #ifndef SDRG_MW_MAP
 #define SDRG_MW_MAP 0
 #endif
+#ifndef SDRG_MW_SETS  // register sets of 16 bins the chain wave cycles through (2: A / B, reads one block ahead)
+#define SDRG_MW_SETS 2
+#endif
+constexpr int MW_SETS = SDRG_MW_SETS;
+#ifndef SDRG_MW_WMASK  // lab: the chain writes back only the running-sum lanes' values (the only ones read)
+#define SDRG_MW_WMASK 0
+#endif
+#ifndef SDRG_MW_RDFIRST  // lab: scheduling barriers keep each block's LDS reads ahead of the previous block's sums
+#define SDRG_MW_RDFIRST 0
+#endif
+static_assert(MW_SETS == 2 || MW_SETS == 4, "the chain's sets");
 constexpr int MW_RECW = SDRG_MW_RECW;
 constexpr int MW_P0 = 1 + MW_RECW;          // first producer wave
 constexpr int MW_PROD = MW_T - 64 * MW_P0;  // producer lanes
@@ -1632,15 +1643,35 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
                         acc += X[i].w;
                         r[i].w = acc;
                     }
+                    if (!SDRG_MW_WMASK || cg == 1) {  // WMASK: only the running sums are read back (record waves)
 #pragma unroll
-                    for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];
+                        for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];
+                    }
                 };
-                rd(A, 0);
-                for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
-                    rd(B, t + 16);
-                    sum16(A, t);
-                    if (t + 32 < SC) rd(A, t + 32);
-                    sum16(B, t + 16);
+                if constexpr (MW_SETS == 2) {
+                    rd(A, 0);
+                    for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
+                        rd(B, t + 16);
+                        if (SDRG_MW_RDFIRST) __builtin_amdgcn_sched_barrier(0);  // the next block's reads before the sums
+                        sum16(A, t);
+                        if (t + 32 < SC) rd(A, t + 32);
+                        if (SDRG_MW_RDFIRST) __builtin_amdgcn_sched_barrier(0);
+                        sum16(B, t + 16);
+                    }
+                } else {
+                    // MW_SETS register sets of 16 bins: each set's reads are issued MW_SETS - 1 blocks before its sums
+                    // (the LDS latency under the producers' and record waves' traffic is longer than one block)
+                    float4 X[MW_SETS][4];
+#pragma unroll
+                    for (int k = 0; k < MW_SETS - 1; k++) rd(X[k], 16 * k);
+                    for (int t = 0; t < SC; t += 16 * MW_SETS) {  // SC >= 64, a power of two >= 16 MW_SETS
+#pragma unroll
+                        for (int k = 0; k < MW_SETS; k++) {
+                            const int ahead = t + 16 * (k + MW_SETS - 1);
+                            if (ahead < SC) rd(X[(k + MW_SETS - 1) % MW_SETS], ahead);
+                            sum16(X[k], t + 16 * k);
+                        }
+                    }
                 }
             }
         } else if (rec_lane && c >= 2) {

@@ -1,19 +1,18 @@
 #!/bin/bash
-# r5z: the in-launch hand-off's price inside the persistent four-step kernels (1024 x 65536 CS16, spectrum alone):
-# per-tile publish (plain + release fence, or write-through sc1 stores) and per-tile acquire, no waiting
+# r5ab: the multi-frame statistics' chain wave: writes masked to the running-sum lanes (wmask), each block's LDS reads
+# kept ahead of the previous block's sums (rdfirst), both (wmrd): bit-exactness, the kernel alone, the c5 200 kHz line
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
 D=sdr-for-android-lib_amd/lib
+for v in wmask rdfirst wmrd; do
+  SDRG_LIB_PATH=$D/libsdrg_$v.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_stats_geometry.py tests/test_gpu_stats_exact.py > gpurun_out/r5ab_tests_$v.log 2>&1 || { echo "tests FAILED on $v"; tail -20 gpurun_out/r5ab_tests_$v.log; exit 1; }
+  echo "tests $v: $(tail -1 gpurun_out/r5ab_tests_$v.log)"
+done
 for i in 1 2; do
-  for v in base pub1 pub2 acq1 pub1acq; do
+  for v in base wmask rdfirst wmrd; do
     L=$D/libsdrg_$v.so; [ $v == base ] && L=$D/libsdrg.so
-    echo "$v: $(SDRG_LIB_PATH=$L timeout -k 10 120 python tools/lab/spec_time.py 65536 cs16 1024 50 2>&1 | tail -1)"
+    echo "$v: $(SDRG_LIB_PATH=$L timeout -k 10 120 python tools/lab/stats_time.py 65536 200 1024 30 2>/dev/null | tail -1)"
   done
 done
-cd /tmp
-for v in base pub1 pub2 acq1; do
-  L=$GRAFT_REPO_ROOT/$D/libsdrg_$v.so; [ $v == base ] && L=$GRAFT_REPO_ROOT/$D/libsdrg.so
-  SDRG_LIB_PATH=$L timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r5z_$v -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/lab/spec_time.py 65536 cs16 1024 50 > $GRAFT_REPO_ROOT/gpurun_out/r5z_$v.log 2>&1 || { echo "prof $v failed"; exit 1; }
-done
-echo done
+bash tools/ab.sh -r 1 -o c5w base wmask rdfirst wmrd -- python bench.py --config c5 --focus 200 --steps 100 --warmup 20 --no-cpu-baseline
