@@ -497,7 +497,7 @@ int32_t sdrg_dist_unique_id(void *id, int32_t bytes);
 int32_t sdrg_dist_create(const void *id, int32_t world_size, int32_t rank, int32_t device, sdrg_dist **out);
 int32_t sdrg_dist_destroy(sdrg_dist *d);
 /* Rank, world size, the RCCL version in use and whether the gathers move their bytes through RCCL (1) or, for a
- * one-rank communicator, as device copies on the gather stream (0).  Any pointer may be NULL. */
+ * one-rank communicator, as hipMemcpyAsync device copies (0).  Any pointer may be NULL. */
 int32_t sdrg_dist_info(const sdrg_dist *d, int32_t *rank, int32_t *world_size, int32_t *rccl_version,
                        int32_t *rccl_data);
 /* A one-rank communicator's gathers are device copies by default (RCCL's one-rank gather kernel runs beside the SSB
@@ -524,12 +524,13 @@ typedef struct sdrg_gather_buffers {
     const int16_t *pcm;
     int16_t *pcm_out;
 } sdrg_gather_buffers;
-/* Enqueue the gathers (one RCCL group) on a gather stream of the engine, after the last process call's outputs they
- * read (records of asynchronous statistics and the PCM of a pipelined call included): no host synchronisation, and
- * none of the engine's own streams waits for them -- a later call that writes a buffer still being gathered (the
- * same pointer) waits for the gather on the GPU first, so a caller rotating its output buffers overlaps the gathers
- * with its next calls.  Every rank calls it with the same selection.  Complete after sdrg_engine_synchronize (or on
- * a stream after sdrg_engine_wait_outputs). */
+/* Enqueue the gathers (one RCCL group) behind the last process call's outputs they read, on the engine stream that
+ * produced them: the statistics stream when that call ran its statistics asynchronously (its records, and the spectra
+ * those statistics waited for), else the main stream; with PCM, the audio detector's stream (after the SSB stage).
+ * No host synchronisation; a later call that writes a buffer a gather reads (the same pointer) waits for that gather
+ * on the GPU first, and nothing else waits, so a caller rotating its output buffers overlaps the gathers with its next
+ * calls.  Every rank calls it with the same selection.  Complete after sdrg_engine_synchronize (or on a stream after
+ * sdrg_engine_wait_outputs).  Replaces nothing in the reference (one receiver per process): BASELINE configs[3]. */
 int32_t sdrg_engine_gather(sdrg_engine *eng, sdrg_dist *d, int32_t root, const sdrg_gather_buffers *bufs);
 /* Single-pair forms of sdrg_engine_gather. */
 int32_t sdrg_engine_gather_records(sdrg_engine *eng, sdrg_dist *d, int32_t root, const sdrg_frame_record *records,
