@@ -1412,6 +1412,11 @@ constexpr int MW_F = 4;                     // frames per workgroup
 #define SDRG_MW_SETS 2
 #endif
 constexpr int MW_SETS = SDRG_MW_SETS;
+#ifndef SDRG_MW_ILP2  // lab: two frames' chains per chain lane (lanes 0-31), their adds interleaved
+#define SDRG_MW_ILP2 0
+#endif
+constexpr bool MW_ILP2 = SDRG_MW_ILP2;
+static_assert(!MW_ILP2 || MW_F == 4, "MW_ILP2 pairs frames f and f + 2");
 #ifndef SDRG_MW_WMASK  // lab: the chain writes back only the running-sum lanes' values (the only ones read)
 #define SDRG_MW_WMASK 0
 #endif
@@ -1506,13 +1511,16 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
     auto frame_ptr = [&](int f) { return spectra + (size_t)frame_of(f) * (size_t)g.n; };
 
     // ---- chain wave: lane = LPFR x frame + j; j < nwin window sums, then running sums, then dB sums ----
-    const int cf = lane / LPFR, cjj = lane - cf * LPFR;
+    // MW_ILP2: lanes 0-31 each carry the same chain of two frames, cf and cf + 2, so two independent adds issue per bin
+    const int cl = MW_ILP2 ? (lane & 31) : lane;
+    const int cf = cl / LPFR, cjj = cl - cf * LPFR;
     int cg = 3, cj = 0;
     if (cjj < nwin) cg = 0, cj = cjj;
     else if (cjj < 2 * nwin) cg = 1, cj = cjj - nwin;
     else if (want_db && cjj < 3 * nwin - 1) cg = 2, cj = cjj - 2 * nwin;
+    if (MW_ILP2 && lane >= 32) cg = 3;
     const bool chain = wave == 0 && cg < 3;
-    float acc = 0.0f;
+    float acc = 0.0f, acc2 = 0.0f;  // acc2: frame cf + 2 (MW_ILP2)
     // ---- record waves: G lanes per (frame, window); one wave for all frames, or wave 1 + f for frame f ----
     const int rfr = MW_RECW == 1 ? F : 1;  // frames per record wave
     const int G = WAVE / (rfr * nwin), ritem = lane / G, rq0 = ritem % nwin, rk = lane - ritem * G;
@@ -1648,7 +1656,43 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
                         for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];
                     }
                 };
-                if constexpr (MW_SETS == 2) {
+                if constexpr (MW_ILP2) {
+                    // two frames' chains per lane in 8-bin blocks (the same registers as two 16-bin sets): frame cf
+                    // in X0 / acc, frame cf + 2 in X1 / acc2, their adds interleaved
+                    const int fo = 2 * frame_floats;
+                    float4 A0[2], A1[2], B0[2], B1[2];
+                    auto rd2 = [&](float4 (&X0)[2], float4 (&X1)[2], int u) {
+#pragma unroll
+                        for (int i = 0; i < 2; i++) {
+                            X0[i] = *reinterpret_cast<const float4 *>(src + u + 4 * i);
+                            X1[i] = *reinterpret_cast<const float4 *>(src + fo + u + 4 * i);
+                        }
+                    };
+                    auto sum8x2 = [&](const float4 (&X0)[2], const float4 (&X1)[2], int u) {
+                        float4 r0[2], r1[2];
+#pragma unroll
+                        for (int i = 0; i < 2; i++) {
+                            acc += X0[i].x; r0[i].x = acc; acc2 += X1[i].x; r1[i].x = acc2;
+                            acc += X0[i].y; r0[i].y = acc; acc2 += X1[i].y; r1[i].y = acc2;
+                            acc += X0[i].z; r0[i].z = acc; acc2 += X1[i].z; r1[i].z = acc2;
+                            acc += X0[i].w; r0[i].w = acc; acc2 += X1[i].w; r1[i].w = acc2;
+                        }
+                        if (!SDRG_MW_WMASK || cg == 1) {
+#pragma unroll
+                            for (int i = 0; i < 2; i++) {
+                                *reinterpret_cast<float4 *>(dst + u + 4 * i) = r0[i];
+                                *reinterpret_cast<float4 *>(dst + fo + u + 4 * i) = r1[i];
+                            }
+                        }
+                    };
+                    rd2(A0, A1, 0);
+                    for (int t = 0; t < SC; t += 16) {  // SC >= 64, a multiple of 16
+                        rd2(B0, B1, t + 8);
+                        sum8x2(A0, A1, t);
+                        if (t + 16 < SC) rd2(A0, A1, t + 16);
+                        sum8x2(B0, B1, t + 8);
+                    }
+                } else if constexpr (MW_SETS == 2) {
                     rd(A, 0);
                     for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
                         rd(B, t + 16);
@@ -1704,6 +1748,8 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
     if (rec_lane) atomicMax(&s_rec[rf][rq], vi_key(rm, ri));
     if (chain && cg == 0) s_sum[cf][cj] = acc;
     if (chain && cg == 2) s_dsum[cf][cj] = acc;
+    if (MW_ILP2 && chain && cg == 0) s_sum[cf + 2][cj] = acc2;
+    if (MW_ILP2 && chain && cg == 2) s_dsum[cf + 2][cj] = acc2;
     __syncthreads();
     MW_STAMP(1);
 
