@@ -318,6 +318,11 @@ constexpr int ABL = SDRG_K16_ABLATE;
 #define SDRG_K16_ALONE_X1 0
 #endif
 constexpr bool K16_ALONE_X1 = SDRG_K16_ALONE_X1;
+// the |X|^2 stores' cache policy (buffer-store aux bits, gfx950: 1 sc0, 2 nt, 16 sc1)
+#ifndef SDRG_K16_STORE_AUX
+#define SDRG_K16_STORE_AUX 2
+#endif
+constexpr int K16_STORE_AUX = SDRG_K16_STORE_AUX;
 
 constexpr int LOG2N = 14, N = 1 << LOG2N, T = N / E, HALF = N / 2;
 constexpr int XCH_F2 = HALF;              // half-frame exchange buffer, f2 slots (XOR-swizzled, no padding)
@@ -583,7 +588,7 @@ __device__ __forceinline__ void spectrum16k_body(const void *__restrict__ iq, fl
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, pw[r]), os, 8 * t,
-                                                      4 * ((r * 1024 + N / 2) & (N - 1)), 2 /* nt */);
+                                                      4 * ((r * 1024 + N / 2) & (N - 1)), K16_STORE_AUX);
         }
     }
 }
