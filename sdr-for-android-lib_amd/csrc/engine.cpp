@@ -1475,7 +1475,7 @@ int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdr
         if (g_pcm && e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
     } else if (g_pcm) {
         if ((g_rec || g_foc || g_spec) && e->last_in_main) HIP_TRY(hipStreamWaitEvent(s, e->last_in_main, 0));
-        if (g_rec && e->last_async_stats && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));
+        if (g_rec && e->last_stats_end) HIP_TRY(hipStreamWaitEvent(s, e->last_stats_end, 0));  // any async records
         if (e->last_in_ssb) HIP_TRY(hipStreamWaitEvent(s, e->last_in_ssb, 0));
     }
     // records an earlier call's asynchronous statistics wrote (the last call ran no statistics there)
