@@ -1,8 +1,7 @@
 #!/bin/bash
-# r5af: the spectrum's |X|^2 stores write-through (sc1) so that they leave no dirty L2 lines for the SSB kernel's
-# end-of-kernel write-back (the ~6 us gap between consecutive SSB kernels), against nt (product) and plain
+# r5ag: the C-ABI gather test over its three stream paths x two one-rank data paths
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-bash tools/ab.sh -r 2 -o st -t "tests/test_gpu_parity.py" base st16 st18 st0 -- python bench.py --no-cpu-baseline --no-labelled || exit 1
-bash tools/ab.sh -r 2 -o std base st16 st18 -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-labelled
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_dist_capi.py > gpurun_out/r5ag_tests.log 2>&1 || { echo "tests FAILED"; tail -30 gpurun_out/r5ag_tests.log; exit 1; }
+grep -E "PASSED|FAILED" gpurun_out/r5ag_tests.log; tail -1 gpurun_out/r5ag_tests.log
