@@ -978,10 +978,70 @@ __global__ __launch_bounds__(TILE_B) void four_step_b_p(const f2 *__restrict__ Y
 // hi: the waves run at issue priority 1, above statistics that run beside them on a stream of their own (configs[4]
 // at 5 kHz: 0.3096-0.3113 vs 0.3127-0.3130 ms per step, 200 kHz unchanged, tools/gpu_r4y.sh); not beside the SSB
 // pipeline, whose helper roles at priority 0 would yield to them
+// Lab (SDRG_FS_2STREAM=1): waves of half the frames with two intermediate buffers, the column kernel of wave w + 1
+// on the caller's stream beside the row kernel of wave w on a second stream (events order each buffer's reuse), so the
+// launches' tails and boundaries overlap.  The engine sizes the scratch by spectrum_scratch_floats (the same bytes).
+#ifndef SDRG_FS_2STREAM
+#define SDRG_FS_2STREAM 0
+#endif
+template <int LOG2N1, int LOG2N2, int FMT>
+hipError_t launch_four_step_2s(const void *iq, int n_frames, const float *twf, float *spectra, float *scratch, int wave,
+                               hipStream_t s, bool persistent, int hi) {
+    constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
+    static hipStream_t sb = nullptr;
+    static hipEvent_t ev0, ev_end, ev_a[2], ev_b[2];
+    if (!sb) {
+        hipError_t e = hipStreamCreateWithFlags(&sb, hipStreamNonBlocking);
+        const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev0, fl);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev_end, fl);
+        for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&ev_a[i], fl);
+        for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&ev_b[i], fl);
+        if (e != hipSuccess) return e;
+    }
+    const f2 *tw = reinterpret_cast<const f2 *>(twf);
+    const int half = wave / 2 > 0 ? wave / 2 : 1;
+    const int cus = k16::device_cus();
+    hipError_t e = hipEventRecord(ev0, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(sb, ev0, 0);
+    int w = 0;
+    for (int f0 = 0; f0 < n_frames && e == hipSuccess; f0 += half, ++w) {
+        const int nf = (n_frames - f0) < half ? (n_frames - f0) : half;
+        f2 *Y = reinterpret_cast<f2 *>(scratch) + (size_t)(w & 1) * half * N;
+        const char *src = reinterpret_cast<const char *>(iq) + (size_t)f0 * N * bytes_per_sample<FMT>();
+        if (w >= 2) e = hipStreamWaitEvent(s, ev_b[w & 1], 0);  // the row kernel of wave w - 2 read this buffer
+        if (e != hipSuccess) break;
+        if (persistent) {
+            const int ta = nf * (N2 / TilePlan<N1, TILE_A>::C), ga = ta < 2 * cus ? ta : 2 * cus;
+            hipLaunchKernelGGL((four_step_a_p<LOG2N1, LOG2N2, FMT>), dim3(ga), dim3(TILE_A), 0, s, src, Y, tw, nf, hi);
+        } else {
+            hipLaunchKernelGGL((four_step_a<LOG2N1, LOG2N2, FMT>), dim3(N2 / TilePlan<N1, TILE_A>::C, nf), dim3(TILE_A), 0,
+                               s, src, Y, tw, hi);
+        }
+        e = hipEventRecord(ev_a[w & 1], s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(sb, ev_a[w & 1], 0);
+        if (e != hipSuccess) break;
+        if (persistent) {
+            const int tb = nf * (N1 / TilePlan<N2, TILE_B>::C), gb = tb < 4 * cus ? tb : 4 * cus;
+            hipLaunchKernelGGL((four_step_b_p<LOG2N1, LOG2N2>), dim3(gb), dim3(TILE_B), 0, sb, Y, spectra + (size_t)f0 * N,
+                               tw, nf, hi);
+        } else {
+            hipLaunchKernelGGL((four_step_b<LOG2N1, LOG2N2>), dim3(N1 / TilePlan<N2, TILE_B>::C, nf), dim3(TILE_B), 0, sb, Y,
+                               spectra + (size_t)f0 * N, tw, hi);
+        }
+        e = hipEventRecord(ev_b[w & 1], sb);
+    }
+    if (e == hipSuccess) e = hipEventRecord(ev_end, sb);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_end, 0);  // later work on the caller's stream follows every wave
+    return e != hipSuccess ? e : hipGetLastError();
+}
+
 template <int LOG2N1, int LOG2N2, int FMT>
 hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, float *spectra, float *scratch,
                             int wave, hipStream_t s, bool persistent, bool hi_prio) {
     const int hi = hi_prio ? 1 : 0;
+    if (SDRG_FS_2STREAM) return launch_four_step_2s<LOG2N1, LOG2N2, FMT>(iq, n_frames, twf, spectra, scratch, wave, s,
+                                                                         persistent, hi);
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
     const f2 *tw = reinterpret_cast<const f2 *>(twf);
     f2 *Y = reinterpret_cast<f2 *>(scratch);
