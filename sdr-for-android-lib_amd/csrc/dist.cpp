@@ -1,7 +1,8 @@
 // dist.cpp — the multi-GPU data path behind the C ABI (include/sdrg.h, "Multi-GPU"): one process per GPU, the
 // streams sharded contiguously over the ranks (rank r owns global streams [r*B, (r+1)*B)), and the one collective of
 // the path -- the per-frame results of every rank gathered to a root rank -- as RCCL ncclGather over xGMI, enqueued
-// on the engine's own HIP stream so that it follows each call's kernels without a host synchronisation.
+// on the engine stream that produced the gathered outputs (engine.cpp, sdrg_engine_gather), so that it follows each
+// call's kernels without a host synchronisation.
 //
 // What the gather carries is what the reference's soapyCallback hands to Kotlin per frame
 // (src/sdr-bridge-java-soapy.cpp:456-466: the fftCallback spectrum, then the getters' values -- here the 72-byte
