@@ -649,8 +649,9 @@ class Engine:
 
     def gather(self, dist: "Dist", root: int = 0, records=None, records_out=None, focus_spectra=None, focus_out=None,
                spectra=None, spectra_out=None, pcm=None, pcm_out=None) -> None:
-        """sdrg_engine_gather: RCCL gathers of this rank's per-frame outputs (device pointers, ints) to `root`, one
-        RCCL group on the engine's main stream after the last call's outputs; *_out only on the root."""
+        """sdrg_engine_gather: gathers of this rank's per-frame outputs (device pointers, ints) to `root`, one RCCL group
+        behind the last call's outputs on the engine stream that produced them (device copies on a one-rank
+        communicator unless Dist.set_one_rank_rccl(True)); *_out only on the root."""
         b = _GatherBuffers(records, records_out, focus_spectra, focus_out, spectra, spectra_out, pcm, pcm_out)
         _check(load().sdrg_engine_gather(self._h, dist._h, root, ctypes.byref(b)), "sdrg_engine_gather")
 
