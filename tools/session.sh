@@ -1,6 +1,7 @@
 #!/bin/bash
-# r5aj: SSB pipeline role maps that take the equaliser off the low-pass wave's SIMD (lab SDRG_PIPE_MAP)
+# r5ak: lab-knob test with the round-5 knobs, C-ABI tests
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-bash tools/ab.sh -r 2 -o map -t "tests/test_gpu_ssb_schedule.py" base lab:SDRG_PIPE_MAP=7B9846A53210 lab:SDRG_PIPE_MAP=7B984A563210 lab:SDRG_PIPE_MAP=7B986A453210 -- python bench.py --no-cpu-baseline --no-labelled
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_lab_knobs.py tests/test_gpu_engine_api.py > gpurun_out/r5ak_tests.log 2>&1 || { echo "tests FAILED"; tail -30 gpurun_out/r5ak_tests.log; exit 1; }
+tail -1 gpurun_out/r5ak_tests.log
