@@ -46,7 +46,6 @@ ISO_LAUNCHES = 30  # launches of the spectrum stage alone behind roofline_isolat
 N_INPUTS = 3  # distinct input batches rotated per step: 3 x 128 MiB > the 256 MiB Infinity Cache
 SSB_ISO_CALLS = 20  # joined SSB-only calls timed for ssb_latency_floor.ssb_ms_alone
 LAB_HOST_TIMES = os.environ.get("SDRG_BENCH_HOST_TIMES") == "1"
-LAB_HOST_DELAY = float(os.environ.get("SDRG_BENCH_HOST_DELAY_US", "0")) * 1e-6
 LAB_NO_STEP_GATHER = os.environ.get("SDRG_BENCH_NO_STEP_GATHER") == "1"  # lab: the N > 1 path without its per-step gathers
 N_OUTPUTS = 3  # spectra / records buffers rotated per step (asynchronous statistics read a call's spectra late)
 # SSB floor: the sample-serial low-pass wave's own instruction issue.  Per sample it issues 6 VALU instructions
@@ -277,8 +276,9 @@ def main() -> int:
                          "loses more to co-resident statistics than they gain (0.148 vs 0.128 ms/step), and for N > 1 "
                          "(the per-step gathers read the records on the main stream)")
     ap.add_argument("--process-group", action="store_true",
-                    help="N = 1: run the N > 1 code path anyway on the one GPU -- a one-rank RCCL communicator from the "
-                         "C ABI with the per-step gathers on the engine's stream, barriers, max-over-ranks timing, the "
+                    help="N = 1: run the N > 1 code path anyway on the one GPU -- a one-rank communicator from the C "
+                         "ABI with the per-step gathers behind each step's outputs (device copies at one rank; "
+                         "SDRG_BENCH_ONE_RANK_RCCL=1 keeps RCCL's kernel), barriers, max-over-ranks timing, the "
                          "full-spectra gather (a rehearsal line)")
     ap.add_argument("--launch-dry-run", action="store_true", help=argparse.SUPPRESS)
     argv = sys.argv[1:]
@@ -435,10 +435,6 @@ def main() -> int:
                     shard.gather_records(f_stage.cpu(), world, rank, dst=0, out=f_out)
                 else:
                     shard.gather_focus(spec, f_lo, f_n, world, rank, dst=0, out=f_out, staging=f_stage)
-        if LAB_HOST_DELAY > 0:  # lab: a busy host delay in place of the gather call
-            t_end = time.perf_counter() + LAB_HOST_DELAY
-            while time.perf_counter() < t_end:
-                pass
         if LAB_HOST_TIMES:
             host_t[0] += h1 - h0
             host_t[1] += time.perf_counter() - h1
