@@ -78,12 +78,18 @@ def main() -> int:
         if with_pcm:
             ok[f"pcm{k}"] = bool(np.array_equal(g_pcm[k].download((B, plen), np.int16), w_pcm))
     ok["distinct_steps"] = not np.array_equal(want[0][2], want[1][2])
-    # a root outside the communicator is refused before anything is enqueued
-    try:
-        eng.gather(dist, 1, records=rec[0].ptr, records_out=g_rec[0].ptr)
-        ok["bad_root_refused"] = False
-    except sdrg.SdrgError as exc:
-        ok["bad_root_refused"] = "SDRG_E_INVALID" in str(exc)
+    # refused before anything is enqueued: a root outside the communicator, a missing output buffer on the root
+    def refused(**kw):
+        try:
+            eng.gather(dist, kw.pop("root", 0), **kw)
+            return False
+        except sdrg.SdrgError as exc:
+            return "SDRG_E_INVALID" in str(exc)
+    ok["bad_root_refused"] = refused(root=1, records=rec[0].ptr, records_out=g_rec[0].ptr)
+    ok["null_records_out_refused"] = refused(records=rec[0].ptr)
+    ok["null_focus_out_refused"] = refused(focus_spectra=spec[0].ptr)
+    ok["null_pcm_out_refused"] = refused(pcm=pcm.ptr)
+    ok["empty_selection_ok"] = not refused()  # nothing selected: a no-op
     eng.close()
     dist.close()
     print(json.dumps({"ok": ok, "torch_loaded": "torch" in sys.modules, "rccl_version": info["rccl_version"],

@@ -1,8 +1,7 @@
 #!/bin/bash
-# r5al: the SSB stream's kernel boundary with and without the spectrum beside it (kernel traces)
+# r5am: the C-ABI gather test with its refusal cases
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace -d $GRAFT_REPO_ROOT/gpurun_out/r5al_ssb -o run -- python3 $GRAFT_REPO_ROOT/bench.py --stages ssb --steps 50 --warmup 10 --no-labelled --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/r5al_ssb.log 2>&1 || { tail -5 $GRAFT_REPO_ROOT/gpurun_out/r5al_ssb.log; exit 1; }
-echo done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_dist_capi.py > gpurun_out/r5am_tests.log 2>&1 || { echo "tests FAILED"; tail -30 gpurun_out/r5am_tests.log; exit 1; }
+tail -1 gpurun_out/r5am_tests.log
