@@ -280,8 +280,11 @@ struct PipeLds {
     // 0..3 floats so that any 32-tap window is read with aligned ds_read_b128
     float taps_sh[4][TAPS_ROW];
 };
-// NCO variant only, in dynamic LDS: the phasor tables, then the current chunk's CH phasors {re, im}
-constexpr int NCO_LDS_BYTES = (2 * 1024 * 2 + 2 * CH) * 4;
+// NCO variant only, in dynamic LDS: the current chunk's CH phasors {re, im}.  The two phasor tables (16 KiB) are read
+// from global memory (L1/L2-resident) a chunk ahead by the loader: in LDS they took the pipeline workgroup to 101.7 KiB,
+// and the spectrum workgroup (72.3 KiB) no longer fitted beside it on a CU (r5an: configs[2] 168 G with the tables
+// in LDS)
+constexpr int NCO_LDS_BYTES = 2 * CH * 4;
 
 __device__ __forceinline__ int ceil_div_i(int a, int b) {  // b > 0, any sign of a
     return a >= 0 ? (a + b - 1) / b : -((-a) / b);
@@ -415,8 +418,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         const int k = j + sh - CH;  // copy sh holds taps_pad[j + sh] at index j
         L.taps_sh[sh][j] = (k >= 0 && k < NT) ? taps[k] : 0.0f;
     }
-    if (p.nco_on)
-        for (int i = tid; i < 2 * 1024 * 2; i += PIPE_T) nco_lds[i] = p.nco_tab[i];
 
     const int my_s = lane & (PG - 1);  // serial roles: lane = 16 x copy + stream (all 64 lanes run; lanes < PG store)
     // the hand-scheduled serial roles' lanes (SDRG_SERIAL_LANES): ser_on = the lane holds stream ser_s
@@ -666,7 +667,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             }
         });
     } else if (wave == W_LOAD) {
+        // NCO variant: the table entries of lane j's phasor for chunk c (sample c*CH + j), loaded a chunk ahead
+        const float2 *nco_tab2 = reinterpret_cast<const float2 *>(p.nco_tab);
+        float2 nco_h = make_float2(0.0f, 0.0f), nco_l = make_float2(0.0f, 0.0f);
+        auto nco_fetch = [&](int c) {
+            const uint32_t ph = p.nco_phase + p.nco_inc * (uint32_t)(c * CH + lane);
+            nco_h = nco_tab2[ph >> 22];
+            nco_l = nco_tab2[1024 + ((ph >> 12) & 1023)];
+        };
+        if (p.nco_on && nch > 0) nco_fetch(0);
         chunk_loop([&](int it) {
+            const float2 nco_hc = nco_h, nco_lc = nco_l;  // chunk it's entries
+            if (p.nco_on && it + 1 < nch) nco_fetch(it + 1);
             if constexpr (DMA) {
                 // batch kb + 2 starts moving when batch kb's first chunk is unpacked (its buffer held batch
                 // kb - 1); batch kb + 1 must have landed before the barrier that ends batch kb's last
@@ -684,15 +696,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 const int c = it;
                 if (c < nch) {
                     const int sl = lane >> 2, part = lane & 3;
-                    float *chunk_w = nco_lds + 2 * 1024 * 2;
+                    float *chunk_w = nco_lds;
                     if (p.nco_on) {
                         // every stream of the engine is at the same phase, so the chunk needs CH phasors, not
                         // PG x CH: lane j forms sample c*CH + j's (the table product of nco_mix with x = 1, 0:
                         // Re(w) = 1*wr - 0*wi = wr exactly, and likewise Im), written to LDS for the whole wave
                         static_assert(CH == 64, "one phasor per lane");
-                        const uint32_t ph = p.nco_phase + p.nco_inc * (uint32_t)(c * CH + lane);
-                        const float2 h = reinterpret_cast<const float2 *>(nco_lds)[ph >> 22];
-                        const float2 l = reinterpret_cast<const float2 *>(nco_lds)[1024 + ((ph >> 12) & 1023)];
+                        const float2 h = nco_hc, l = nco_lc;
                         reinterpret_cast<float2 *>(chunk_w)[lane] = make_float2(h.x * l.x - h.y * l.y, h.x * l.y + h.y * l.x);
                         // this wave reads what its own lanes wrote: LDS ops of one wave complete in order
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -1,7 +1,12 @@
 #!/bin/bash
-# r5am: the C-ABI gather test with its refusal cases
+# r5an: the NCO variant's phasor tables out of LDS (loaded a chunk ahead from global memory) so the spectrum
+# workgroup fits beside the pipeline again: variant + parity tests, the default bench line with configs[2]
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_dist_capi.py > gpurun_out/r5am_tests.log 2>&1 || { echo "tests FAILED"; tail -30 gpurun_out/r5am_tests.log; exit 1; }
-tail -1 gpurun_out/r5am_tests.log
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_ssb_variant.py tests/test_gpu_parity.py tests/test_gpu_ssb_schedule.py tests/test_gpu_pulse.py > gpurun_out/r5an_tests.log 2>&1 || { echo "tests FAILED"; tail -30 gpurun_out/r5an_tests.log; exit 1; }
+tail -1 gpurun_out/r5an_tests.log
+for i in 1 2; do
+  timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/r5an_bench$i.json 2> gpurun_out/r5an_bench$i.err || { tail gpurun_out/r5an_bench$i.err; exit 1; }
+  python tools/bench_summary.py gpurun_out/r5an_bench$i.json
+done
