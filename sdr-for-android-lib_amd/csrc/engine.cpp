@@ -183,6 +183,7 @@ struct sdrg_engine {
     // still being gathered (same pointer) waits for the gather on the GPU first, so a caller rotating its output
     // buffers never delays its next call's kernels behind a gather
     bool last_async_stats = false;  // the last call with a statistics stage ran it on s_stats
+    bool lab_ssb_first = false;     // lab SDRG_SSB_FIRST: host launch order of a forked SSB stage
     hipStream_t s_gather = nullptr;   // lab (SDRG_GATHER_STREAM=1): the gathers on a stream of their own
     hipStream_t s_last_gather = nullptr;  // the stream of the last gather
     hipEvent_t ev_gather = nullptr;  // the last gather's end (wait_outputs, synchronize)
@@ -653,11 +654,19 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             HIP_TRY(hipStreamWaitEvent(sm, e->ev_stats_end[pv], 0));
     }
     if (hipEvent_t g = do_spec ? e->gathering(spec) : nullptr) HIP_TRY(hipStreamWaitEvent(sm, g, 0));  // being gathered
-    if (do_spec) {
-        HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, sm, do_ssb && early_fork && !split,
-                                split ? e->spec_cus : 0, do_stats && stats_uses_wide(geo)));
-        if (prof) HIP_TRY(hipEventRecord(ev->spec, sm));
-    }
+    auto enqueue_spectrum = [&]() -> int32_t {
+        if (do_spec) {
+            HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, sm, do_ssb && early_fork && !split,
+                                    split ? e->spec_cus : 0, do_stats && stats_uses_wide(geo)));
+            if (prof) HIP_TRY(hipEventRecord(ev->spec, sm));
+        }
+        return SDRG_OK;
+    };
+    // host launch order (lab SDRG_SSB_FIRST=1: a forked SSB stage is enqueued before the spectrum, so on an idle chip
+    // its workgroups are placed first)
+    const bool ssb_first = e->lab_ssb_first && do_ssb && early_fork;
+    if (!ssb_first)
+        if (int32_t rc = enqueue_spectrum()) return rc;
     if (do_ssb) {  // fork
         if (!early_fork) {
             HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
@@ -690,6 +699,8 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             e->ap_calls++;
         }
     }
+    if (ssb_first)
+        if (int32_t rc = enqueue_spectrum()) return rc;
     if (do_stats) {
         hipStream_t st = sm;
         if (async) {  // after this call's spectrum, beside the next call's
@@ -944,6 +955,7 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
     if (const char *v = lab_getenv("SDRG_GATHER_STREAM"))
         if (atoi(v) == 1 && create_engine_stream(&e->s_gather, 16, device) != hipSuccess)
             return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
+    if (const char *v = lab_getenv("SDRG_SSB_FIRST")) e->lab_ssb_first = atoi(v) == 1;
     hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join, &e->ev_in_main, &e->ev_in_ssb, &e->ev_ap_end[0], &e->ev_ap_end[1],
                          &e->ev_ap_end[2]};
     static_assert(sdrg_pulse_bank::NEW_SETS == 3, "ev_ap_end creation");

@@ -41,13 +41,13 @@ if not lines:
     sys.exit(0)
 d = json.loads(lines[-1])
 k = d.get("kernel_ms", {})
-s = f"  {d['value']:.1f} G  {d['ms_per_step']:.4f} ms/step  spec {k.get('spectrum_ms', 0):.4f} stats {k.get('stats_ms', 0):.4f} ssb {k.get('ssb_ms', 0):.4f}"
+s = f"  {d['value'] / 1e3:.1f} G  {d['ms_per_step']:.4f} ms/step  spec {k.get('spectrum_ms', 0):.4f} stats {k.get('stats_ms', 0):.4f} ssb {k.get('ssb_ms', 0):.4f}"
 fl = d.get("ssb_latency_floor")
 if fl:
     s += f"  ssb_alone {fl['ssb_ms_alone']:.4f}"
 print(s)
 for name, l in d.get("labelled", {}).items():
-    print(f"    {name}: {l['value']} G {l['ms_per_step']} ms" + (f" spec {l['spectrum_ms']} stats {l['stats_ms']}" if 'stats_ms' in l else ""))
+    print(f"    {name}: {l['value'] / 1e3:.1f} G {l['ms_per_step']} ms" + (f" spec {l['spectrum_ms']} stats {l['stats_ms']}" if 'stats_ms' in l else ""))
 EOF
 }
 

@@ -1,12 +1,11 @@
 #!/bin/bash
-# r5an: the NCO variant's phasor tables out of LDS (loaded a chunk ahead from global memory) so the spectrum
-# workgroup fits beside the pipeline again: variant + parity tests, the default bench line with configs[2]
+# r5aq: the first steps after a host synchronisation (the driver command's ~250-300 us fixed cost per timed region):
+# per-step kernel durations of blocks right after a sync, after 20 ms idle, FFT+stats-only and SSB-only blocks
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_ssb_variant.py tests/test_gpu_parity.py tests/test_gpu_ssb_schedule.py tests/test_gpu_pulse.py > gpurun_out/r5an_tests.log 2>&1 || { echo "tests FAILED"; tail -30 gpurun_out/r5an_tests.log; exit 1; }
-tail -1 gpurun_out/r5an_tests.log
-for i in 1 2; do
-  timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/r5an_bench$i.json 2> gpurun_out/r5an_bench$i.err || { tail gpurun_out/r5an_bench$i.err; exit 1; }
-  python tools/bench_summary.py gpurun_out/r5an_bench$i.json
-done
+timeout -k 10 300 python tools/lab/startup_trace.py > gpurun_out/r5aq_plain.log 2>&1 || { tail gpurun_out/r5aq_plain.log; exit 1; }
+cat gpurun_out/r5aq_plain.log
+timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/r5aq_tr -o run --output-format csv -- python3 tools/lab/startup_trace.py > gpurun_out/r5aq_tr.log 2>&1 || { tail gpurun_out/r5aq_tr.log; exit 1; }
+grep '^P' gpurun_out/r5aq_tr.log
+python3 tools/lab/startup_blocks.py gpurun_out/r5aq_tr/run_kernel_trace.csv 8
