@@ -700,10 +700,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                     if (p.nco_on) {
                         // every stream of the engine is at the same phase, so the chunk needs CH phasors, not
                         // PG x CH: lane j forms sample c*CH + j's (the table product of nco_mix with x = 1, 0:
-                        // Re(w) = 1*wr - 0*wi = wr exactly, and likewise Im), written to LDS for the whole wave
+                        // Re(w) = 1*wr - 0*wi = wr exactly, and likewise Im), written to LDS for the whole wave,
+                        // planar (CH real parts, then CH imaginary parts) so the mix below runs on sample pairs
                         static_assert(CH == 64, "one phasor per lane");
                         const float2 h = nco_hc, l = nco_lc;
-                        reinterpret_cast<float2 *>(chunk_w)[lane] = make_float2(h.x * l.x - h.y * l.y, h.x * l.y + h.y * l.x);
+                        chunk_w[lane] = h.x * l.x - h.y * l.y;
+                        chunk_w[CH + lane] = h.x * l.y + h.y * l.x;
                         // this wave reads what its own lanes wrote: LDS ops of one wave complete in order
                         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     }
@@ -732,12 +734,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                             }
                         }
                         if (p.nco_on) {  // the NCO variant: Re(x w) as nco_mix, then the frame's zero padding
-                            const float4 *w4 = reinterpret_cast<const float4 *>(chunk_w + 2 * within);
+                            // x*wr - xq*wi on sample pairs: two packed products and a packed difference, each
+                            // lane of a packed op rounding as the scalar op (no contraction)
+                            const float4 *wr4 = reinterpret_cast<const float4 *>(chunk_w + within);
+                            const float4 *wi4 = reinterpret_cast<const float4 *>(chunk_w + CH + within);
 #pragma unroll
-                            for (int h = 0; h < 4; h++) {
-                                const float4 w = w4[h];  // phasors of samples within + 2h, + 2h + 1
-                                x[2 * h] = x[2 * h] * w.x - xq[2 * h] * w.y;
-                                x[2 * h + 1] = x[2 * h + 1] * w.z - xq[2 * h + 1] * w.w;
+                            for (int h = 0; h < 2; h++) {
+                                const float4 wr = wr4[h], wi = wi4[h];  // samples within + 4h .. + 4h + 3
+                                const f2v a0 = f2v{x[4 * h], x[4 * h + 1]} * f2v{wr.x, wr.y};
+                                const f2v b0 = f2v{xq[4 * h], xq[4 * h + 1]} * f2v{wi.x, wi.y};
+                                const f2v a1 = f2v{x[4 * h + 2], x[4 * h + 3]} * f2v{wr.z, wr.w};
+                                const f2v b1 = f2v{xq[4 * h + 2], xq[4 * h + 3]} * f2v{wi.z, wi.w};
+                                const f2v m0 = a0 - b0, m1 = a1 - b1;
+                                x[4 * h] = m0.x;
+                                x[4 * h + 1] = m0.y;
+                                x[4 * h + 2] = m1.x;
+                                x[4 * h + 3] = m1.y;
                             }
                         }
 #pragma unroll
@@ -1047,7 +1059,7 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
     if (chunk_out && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels()) {
         const dim3 grid((n_frames + PG - 1) / PG);
         size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
-        if (p.nco_on && pad < (size_t)NCO_LDS_BYTES) pad = NCO_LDS_BYTES;  // the dynamic part holds the NCO tables
+        if (p.nco_on && pad < (size_t)NCO_LDS_BYTES) pad = NCO_LDS_BYTES;  // the dynamic part holds the chunk phasors
 #if SDRG_PIPE_DYN_LDS
         pad = sizeof(PipeLds) + (p.nco_on ? NCO_LDS_BYTES : 0);
 #define SDRG_PIPE_ATTR_SET(F)                                                                                          \
