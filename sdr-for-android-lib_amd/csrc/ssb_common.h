@@ -52,26 +52,37 @@ __device__ __forceinline__ void load_i8(const char *frame, int n, float (&x)[8])
 }
 
 // I parts of 8 consecutive samples held in raw form in u[] (1, 2 or 4 uint4 by format).
+// The integer formats' scale (and CU8's offset) run on sample pairs: one packed op per two samples, each lane
+// rounding as the scalar expression of load_i8 / load_i1.
+template <int FMT>
+__device__ __forceinline__ void scale_pair(float a, float b, float &xa, float &xb) {
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    f2_t v = f2_t{a, b};
+    if constexpr (FMT == SDRG_IQ_CU8) v = v - f2_t{127.4f, 127.4f};
+    v = v * (FMT == SDRG_IQ_CS16 ? f2_t{1.0f / 32768.0f, 1.0f / 32768.0f} : f2_t{1.0f / 128.0f, 1.0f / 128.0f});
+    xa = v.x;
+    xb = v.y;
+}
+
 template <int FMT>
 __device__ __forceinline__ void unpack_i8(const uint4 *u, float (&x)[8]) {
     if constexpr (FMT == SDRG_IQ_CS8 || FMT == SDRG_IQ_CU8) {
         const uint32_t w[4] = {u[0].x, u[0].y, u[0].z, u[0].w};
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            if constexpr (FMT == SDRG_IQ_CS8) {
-                x[2 * q] = (float)(int8_t)(w[q] & 0xff) * (1.0f / 128.0f);
-                x[2 * q + 1] = (float)(int8_t)((w[q] >> 16) & 0xff) * (1.0f / 128.0f);
-            } else {
-                x[2 * q] = ((float)(w[q] & 0xff) - 127.4f) * (1.0f / 128.0f);
-                x[2 * q + 1] = ((float)((w[q] >> 16) & 0xff) - 127.4f) * (1.0f / 128.0f);
-            }
+            if constexpr (FMT == SDRG_IQ_CS8)
+                scale_pair<FMT>((float)(int8_t)(w[q] & 0xff), (float)(int8_t)((w[q] >> 16) & 0xff), x[2 * q], x[2 * q + 1]);
+            else
+                scale_pair<FMT>((float)(w[q] & 0xff), (float)((w[q] >> 16) & 0xff), x[2 * q], x[2 * q + 1]);
         }
     } else if constexpr (FMT == SDRG_IQ_CS16) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const uint32_t w[4] = {u[h].x, u[h].y, u[h].z, u[h].w};
 #pragma unroll
-            for (int q = 0; q < 4; q++) x[4 * h + q] = (float)(int16_t)(w[q] & 0xffff) * (1.0f / 32768.0f);
+            for (int q = 0; q < 4; q += 2)
+                scale_pair<FMT>((float)(int16_t)(w[q] & 0xffff), (float)(int16_t)(w[q + 1] & 0xffff), x[4 * h + q],
+                                x[4 * h + q + 1]);
         }
     } else {
 #pragma unroll
@@ -89,20 +100,18 @@ __device__ __forceinline__ void unpack_q8(const uint4 *u, float (&x)[8]) {
         const uint32_t w[4] = {u[0].x, u[0].y, u[0].z, u[0].w};
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            if constexpr (FMT == SDRG_IQ_CS8) {
-                x[2 * q] = (float)(int8_t)((w[q] >> 8) & 0xff) * (1.0f / 128.0f);
-                x[2 * q + 1] = (float)(int8_t)(w[q] >> 24) * (1.0f / 128.0f);
-            } else {
-                x[2 * q] = ((float)((w[q] >> 8) & 0xff) - 127.4f) * (1.0f / 128.0f);
-                x[2 * q + 1] = ((float)(w[q] >> 24) - 127.4f) * (1.0f / 128.0f);
-            }
+            if constexpr (FMT == SDRG_IQ_CS8)
+                scale_pair<FMT>((float)(int8_t)((w[q] >> 8) & 0xff), (float)(int8_t)(w[q] >> 24), x[2 * q], x[2 * q + 1]);
+            else
+                scale_pair<FMT>((float)((w[q] >> 8) & 0xff), (float)(w[q] >> 24), x[2 * q], x[2 * q + 1]);
         }
     } else if constexpr (FMT == SDRG_IQ_CS16) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const uint32_t w[4] = {u[h].x, u[h].y, u[h].z, u[h].w};
 #pragma unroll
-            for (int q = 0; q < 4; q++) x[4 * h + q] = (float)(int16_t)(w[q] >> 16) * (1.0f / 32768.0f);
+            for (int q = 0; q < 4; q += 2)
+                scale_pair<FMT>((float)(int16_t)(w[q] >> 16), (float)(int16_t)(w[q + 1] >> 16), x[4 * h + q], x[4 * h + q + 1]);
         }
     } else {
 #pragma unroll
