@@ -221,6 +221,10 @@ enum PipeWave : int { W_DC = 0, W_LPF = 1, W_AGC = 2, W_LOAD = 3, W_FIR0 = 4, W_
 // role of hardware wave w = nibble w: w0 DC, w1 LPF, w2 AGC, w3 load, w4 OUT, w5 EQ, w6 DES2, w7 FIR0,
 // w8 DES0, w9 DES1, w10 DES3, w11 FIR1
 constexpr unsigned long long DEFAULT_ROLE_MAP = 0x7B984A653210ull;
+// the NCO variant's loader does the mixing too: FIR1 beside the DC wave, the clamp beside it as well, DES0 beside the
+// loader (w4 FIR1, w8 OUT, w11 DES0).  configs[2] 199.0-200.6 -> 202.8 G with it; the reference chain's c3 line
+// loses 2.5 % under FIR1 <-> OUT alone (r5av, r5aw, tools/ab.sh, alternating, one box), so it keeps its own map.
+constexpr unsigned long long NCO_ROLE_MAP = 0x8B954A673210ull;
 constexpr int MAX_SLOTS = 32;   // concurrent FIR outputs per stream (up to 4 per FIR lane)
 constexpr int MAX_DONE = 8;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
@@ -1099,10 +1103,11 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
             return e ? (int)strtoul(e, nullptr, 0) : (int)0x802A00BFu;
         }();
         // role of hardware wave w = nibble w (wave w runs on SIMD w % 4); SDRG_PIPE_MAP overrides (diagnostic)
-        static const unsigned long long role_map = [] {
+        static const unsigned long long map_override = [] {
             const char *e = lab_getenv("SDRG_PIPE_MAP");
-            return e ? strtoull(e, nullptr, 16) : DEFAULT_ROLE_MAP;
+            return e ? strtoull(e, nullptr, 16) : 0ull;
         }();
+        const unsigned long long role_map = map_override ? map_override : p.nco_on ? NCO_ROLE_MAP : DEFAULT_ROLE_MAP;
         static const int skip_mask = [] {  // diagnostic only (wrong results): roles whose work is skipped
             const char *e = lab_getenv("SDRG_PIPE_SKIP");
             return e ? (int)strtol(e, nullptr, 0) : 0;

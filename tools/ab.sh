@@ -5,7 +5,8 @@
 #
 # VARIANT: "base" (the product library, sdr-for-android-lib_amd/lib/libsdrg.so) or NAME for a lab build made here by
 # tools/build_variant.sh NAME "FLAGS" (lib/libsdrg_NAME.so), optionally with lab environment knobs as
-# NAME:KEY=VAL,KEY=VAL (lab builds only read them).  For each round the variants run COMMAND in turn (alternating,
+# NAME:KEY=VAL,KEY=VAL (lab builds only read them); NAME+TAG runs build NAME under the label NAME+TAG (one build,
+# several knob settings).  For each round the variants run COMMAND in turn (alternating,
 # one box), each under its own time limit; a COMMAND that prints a bench.py JSON line is summarised (value, ms/step,
 # per-kernel ms, labelled lines), anything else is shown as its last line.  -t: the listed GPU tests run once per
 # non-base variant first (bit-exactness before timing).  Outputs under gpurun_out/ab_TAG_*.
@@ -27,8 +28,8 @@ mkdir -p gpurun_out
 run_env() {  # $1 = VARIANT spec: prints "KEY=VAL ..." for env
   local name=${1%%:*} knobs=""
   [ "$1" != "$name" ] && knobs=${1#*:}
-  local lib=$D/libsdrg.so
-  [ "$name" != "base" ] && lib=$D/libsdrg_$name.so
+  local libname=${name%%+*} lib=$D/libsdrg.so  # NAME+TAG: the build NAME under another label (other knobs)
+  [ "$libname" != "base" ] && lib=$D/libsdrg_$libname.so
   echo "SDRG_LIB_PATH=$lib ${knobs//,/ }"
 }
 
@@ -53,7 +54,7 @@ EOF
 
 if [ -n "$TESTS" ]; then
   for v in "${VARS[@]}"; do
-    [ "${v%%:*}" == "base" ] && continue
+    [ "${v%%[:+]*}" == "base" ] && continue
     env $(run_env "$v") timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu $TESTS \
       > gpurun_out/ab_${TAG}_tests_${v%%:*}.log 2>&1 || { echo "tests FAILED on $v"; tail -30 gpurun_out/ab_${TAG}_tests_${v%%:*}.log; exit 1; }
     echo "tests on $v: $(tail -1 gpurun_out/ab_${TAG}_tests_${v%%:*}.log)"
