@@ -184,6 +184,7 @@ struct sdrg_engine {
     // buffers never delays its next call's kernels behind a gather
     bool last_async_stats = false;  // the last call with a statistics stage ran it on s_stats
     bool lab_ssb_first = false;     // lab SDRG_SSB_FIRST: host launch order of a forked SSB stage
+    bool lab_stats_cus = false;     // lab SDRG_STATS_CUS: s_stats and s_spec on disjoint CU masks
     hipStream_t s_gather = nullptr;   // lab (SDRG_GATHER_STREAM=1): the gathers on a stream of their own
     hipStream_t s_last_gather = nullptr;  // the stream of the last gather
     hipEvent_t ev_gather = nullptr;  // the last gather's end (wait_outputs, synchronize)
@@ -644,7 +645,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
     // asynchronous statistics (SDRG_PIPELINE_STATS_ASYNC): the statistics of earlier calls may still read their
     // spectra on s_stats.  The host waits for the call two before; a spectrum that overwrites the buffer the
     // previous call's statistics read waits for them on the GPU.
-    const bool async = e->stats_async && early_fork && do_stats && do_spec && !split;
+    const bool async = e->stats_async && early_fork && do_stats && do_spec && (!split || e->lab_stats_cus);
     if (e->stats_async && do_spec) {
         const int64_t c = e->sa_calls;
         if (c >= 2 && e->sa_live[(c - 2) % sdrg_engine::SA_RING])
@@ -956,6 +957,30 @@ int32_t sdrg_engine_create(const sdrg_config *cfg, int32_t n_streams, int32_t de
         if (atoi(v) == 1 && create_engine_stream(&e->s_gather, 16, device) != hipSuccess)
             return cleanup(fail(SDRG_E_HIP, "hipStreamCreate failed"));
     if (const char *v = lab_getenv("SDRG_SSB_FIRST")) e->lab_ssb_first = atoi(v) == 1;
+    // lab: SDRG_STATS_CUS = k: the asynchronous statistics on every (ncu / k)-th CU (k CUs), the spectrum on the others
+    // (a CU partition for the FFT + statistics schedule with no SSB stage: each kernel on CUs of its own)
+    if (const char *v = lab_getenv("SDRG_STATS_CUS")) {
+        const int k = atoi(v), ncu = prop.multiProcessorCount;
+        if (k > 0 && k < ncu && !e->s_spec) {
+            const int stride = ncu / k;
+            std::vector<uint32_t> ms((ncu + 31) / 32, 0u), mf((ncu + 31) / 32, 0u);
+            int taken = 0;
+            for (int i = 0; i < ncu; i++) {
+                const bool st = (i % stride == 0) && taken < k;
+                taken += st;
+                (st ? ms : mf)[i / 32] |= 1u << (i % 32);
+            }
+            (void)hipStreamDestroy(e->s_stats);
+            e->s_stats = nullptr;
+            if (hipExtStreamCreateWithCUMask(&e->s_stats, (uint32_t)ms.size(), ms.data()) != hipSuccess ||
+                hipExtStreamCreateWithCUMask(&e->s_spec, (uint32_t)mf.size(), mf.data()) != hipSuccess ||
+                hipEventCreateWithFlags(&e->ev_fork_spec, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&e->ev_join_spec, hipEventDisableTiming) != hipSuccess)
+                return cleanup(fail(SDRG_E_HIP, "CU-masked stream creation failed"));
+            e->spec_cus = ncu - taken;
+            e->lab_stats_cus = true;
+        }
+    }
     hipEvent_t *evs[] = {&e->ev_fork, &e->ev_join, &e->ev_in_main, &e->ev_in_ssb, &e->ev_ap_end[0], &e->ev_ap_end[1],
                          &e->ev_ap_end[2]};
     static_assert(sdrg_pulse_bank::NEW_SETS == 3, "ev_ap_end creation");
