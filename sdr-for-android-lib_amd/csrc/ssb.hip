@@ -216,6 +216,7 @@ constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_
 constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
 constexpr int PIPE_WAVES = 12;
 constexpr int PIPE_T = PIPE_WAVES * 64;
+constexpr int STAMP_SLOTS = 4;  // diagnostic stamps per wave: work, loop cycles, loop time, kernel entry (s_memrealtime)
 enum PipeWave : int { W_DC = 0, W_LPF = 1, W_AGC = 2, W_LOAD = 3, W_FIR0 = 4, W_OUT = 5, W_EQ = 6, W_FIR1 = 7,
                       W_DES0 = 8, W_DES1 = 9, W_DES2 = 10, W_DES3 = 11 };
 // role of hardware wave w = nibble w: w0 DC, w1 LPF, w2 AGC, w3 load, w4 OUT, w5 EQ, w6 DES2, w7 FIR0,
@@ -409,6 +410,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     extern __shared__ __attribute__((aligned(16))) float nco_lds[];  // NCO_LDS_BYTES when p.nco_on
 #endif
     const int tid = threadIdx.x;
+    const unsigned long long st_entry = stamps ? __builtin_amdgcn_s_memrealtime() : 0;  // diagnostic stamps only
     const int hw_wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // runs on SIMD hw_wave % 4
     const int wave = (int)((role_map >> (4 * hw_wave)) & 15);     // the role it plays (PipeWave)
     const int lane = tid & 63;
@@ -892,9 +894,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         });
     }
     if (stamps && lane == 0) {  // diagnostic build only: per-wave work cycles and loop cycles
-        stamps[(blockIdx.x * PIPE_WAVES + wave) * 3] = st_work;
-        stamps[(blockIdx.x * PIPE_WAVES + wave) * 3 + 1] = __builtin_amdgcn_s_memtime() - st_t0;
-        stamps[(blockIdx.x * PIPE_WAVES + wave) * 3 + 2] = __builtin_amdgcn_s_memrealtime() - st_r0;
+        // the low-pass wave's loop is one asm block with no work stamps: its slot holds the loop's start instead
+        // (s_memrealtime, 100 MHz), for the workgroups' start skew
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * STAMP_SLOTS] = wave == W_LPF ? st_r0 : st_work;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * STAMP_SLOTS + 1] = __builtin_amdgcn_s_memtime() - st_t0;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * STAMP_SLOTS + 2] = __builtin_amdgcn_s_memrealtime() - st_r0;
+        stamps[(blockIdx.x * PIPE_WAVES + wave) * STAMP_SLOTS + 3] = st_entry;
     }
 
     if (high) __builtin_amdgcn_s_setprio(0);
@@ -953,7 +958,7 @@ unsigned long long *ssb_stamps_buffer(int n_frames) {
     }();
     if (!on) return nullptr;
     const int groups = (n_frames + PG - 1) / PG;
-    const size_t per_call = (size_t)groups * PIPE_WAVES * 3;
+    const size_t per_call = (size_t)groups * PIPE_WAVES * STAMP_SLOTS;
     if (groups > g_stamps_groups) {
         if (g_stamps) (void)hipFree(g_stamps);
         if (hipMalloc(reinterpret_cast<void **>(&g_stamps), sizeof(unsigned long long) * per_call * STAMP_CALLS) !=
@@ -964,20 +969,48 @@ unsigned long long *ssb_stamps_buffer(int n_frames) {
         g_stamps_groups = groups;
         g_stamp_call = 0;
     }
-    return g_stamps + (size_t)(g_stamp_call++ % STAMP_CALLS) * (size_t)g_stamps_groups * PIPE_WAVES * 3;
+    return g_stamps + (size_t)(g_stamp_call++ % STAMP_CALLS) * (size_t)g_stamps_groups * PIPE_WAVES * STAMP_SLOTS;
 }
 
 // Per role: work / loop cycles, loop time and effective clock of the last call; then the same averaged over the
 // recorded calls except the first and the last (the steady state of a pipelined run).
 void ssb_report_stamps() {
     if (!g_stamps || g_stamp_call == 0) return;
-    const size_t per_call = (size_t)g_stamps_groups * PIPE_WAVES * 3;
+    const size_t per_call = (size_t)g_stamps_groups * PIPE_WAVES * STAMP_SLOTS;
     const int ncalls = g_stamp_call < STAMP_CALLS ? g_stamp_call : STAMP_CALLS;
     std::vector<unsigned long long> h(per_call * STAMP_CALLS);
     if (hipMemcpy(h.data(), g_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     const char *names[PIPE_WAVES] = {"DC", "LPF", "AGC", "LOAD", "FIR-0", "OUT", "EQ", "FIR-1", "DES-0", "DES-1",
                                      "DES-2", "DES-3"};
     const int last = (g_stamp_call - 1) % STAMP_CALLS;
+    {  // the workgroups' loop starts (the low-pass wave's slot 0) and ends (start + loop time): skew and span, in us
+        double skew = 0, mean_late = 0, span = 0, prologue = 0;
+        int sc = 0;
+        for (int k = 0; k < ncalls; k++) {
+            if (ncalls > 2 && (k == last || k == (g_stamp_call - ncalls) % STAMP_CALLS)) continue;
+            const unsigned long long *c = h.data() + (size_t)k * per_call;
+            unsigned long long s0 = ~0ull, s1 = 0, e1 = 0;
+            double sum = 0, pro = 0;
+            for (int g = 0; g < g_stamps_groups; g++) {
+                const unsigned long long st = c[(g * PIPE_WAVES + W_LPF) * STAMP_SLOTS], en = st + c[(g * PIPE_WAVES + W_LPF) * STAMP_SLOTS + 2];
+                pro += (double)(st - c[(g * PIPE_WAVES + W_LPF) * STAMP_SLOTS + 3]);
+                s0 = std::min(s0, st);
+                s1 = std::max(s1, st);
+                e1 = std::max(e1, en);
+                sum += (double)st;
+            }
+            if (s1 == 0) continue;
+            skew += (s1 - s0) / 100.0;
+            mean_late += (sum / g_stamps_groups - (double)s0) / 100.0;
+            span += (e1 - s0) / 100.0;
+            prologue += pro / g_stamps_groups / 100.0;
+            sc++;
+        }
+        if (sc)
+            fprintf(stderr, "[sdrg stamps] workgroup loop starts over %d calls: last start - first %.1f us, mean start - first "
+                            "%.1f us, first start to last end %.1f us, entry to loop start (mean) %.1f us\n", sc, skew / sc, mean_late / sc,
+                    span / sc, prologue / sc);
+    }
     for (int w = 0; w < PIPE_WAVES; w++) {
         double work = 0, loop = 0, real = 0, swork = 0, sloop = 0, sreal = 0;
         int sc = 0;
@@ -985,9 +1018,9 @@ void ssb_report_stamps() {
             const unsigned long long *c = h.data() + (size_t)k * per_call;
             double a = 0, b = 0, r = 0;
             for (int g = 0; g < g_stamps_groups; g++) {
-                a += c[(g * PIPE_WAVES + w) * 3];
-                b += c[(g * PIPE_WAVES + w) * 3 + 1];
-                r += c[(g * PIPE_WAVES + w) * 3 + 2];
+                a += c[(g * PIPE_WAVES + w) * STAMP_SLOTS];
+                b += c[(g * PIPE_WAVES + w) * STAMP_SLOTS + 1];
+                r += c[(g * PIPE_WAVES + w) * STAMP_SLOTS + 2];
             }
             if (k == last) {
                 work = a;
