@@ -1006,6 +1006,18 @@ void ssb_report_stamps() {
             prologue += pro / g_stamps_groups / 100.0;
             sc++;
         }
+        for (int j = 0; j < ncalls; j++) {  // per call, in call order: first entry, first loop start, last loop end (10 ns)
+            const int k = (g_stamp_call - ncalls + j) % STAMP_CALLS;
+            const unsigned long long *c = h.data() + (size_t)k * per_call;
+            unsigned long long en0 = ~0ull, st0 = ~0ull, e1 = 0;
+            for (int g = 0; g < g_stamps_groups; g++) {
+                const unsigned long long *q = c + (size_t)(g * PIPE_WAVES + W_LPF) * STAMP_SLOTS;
+                en0 = std::min(en0, q[3]);
+                st0 = std::min(st0, q[0]);
+                e1 = std::max(e1, q[0] + q[2]);
+            }
+            fprintf(stderr, "[sdrg stamps] call %d abs entry %llu loop %llu end %llu\n", j, en0, st0, e1);
+        }
         if (sc)
             fprintf(stderr, "[sdrg stamps] workgroup loop starts over %d calls: last start - first %.1f us, mean start - first "
                             "%.1f us, first start to last end %.1f us, entry to loop start (mean) %.1f us\n", sc, skew / sc, mean_late / sc,

@@ -1,14 +1,8 @@
 #!/bin/bash
-# r5d: HEAD check after the last engine / SSB changes: smoke, GPU suite, the driver command and the default line
+# r5bg: SSB workgroups' start skew and loop cycles per co-resident stage set (lab stamps build)
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-TAG=r5d
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo "smoke failed"; tail gpurun_out/${TAG}_smoke.log; exit 1; }
-tail -1 gpurun_out/${TAG}_smoke.log
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { echo "GPU tests failed"; tail -30 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
-tail -1 gpurun_out/${TAG}_gpu_tests.log
-timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_driverlike.json 2> gpurun_out/${TAG}_driverlike.err || { echo "bench failed"; tail gpurun_out/${TAG}_driverlike.err; exit 1; }
-python tools/bench_summary.py gpurun_out/${TAG}_driverlike.json
-timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { echo "bench failed"; tail gpurun_out/${TAG}_bench.err; exit 1; }
-python tools/bench_summary.py gpurun_out/${TAG}_bench.json
+L=$PWD/sdr-for-android-lib_amd/lib/libsdrg_labt.so
+SDRG_LIB_PATH=$L SDRG_PIPE_STAMPS=1 timeout -k 10 300 python3 tools/lab/coresidency_stamps.py > gpurun_out/r5bg.log 2>&1 || { tail gpurun_out/r5bg.log; exit 1; }
+awk '/^BLOCK/{b=$2; getline; next} /workgroup loop starts/{if(b) w[b]=$0} /wave 1 LPF/{if(b){print b": "w[b]; print b": "$0; b=""}}' gpurun_out/r5bg.log | sed 's/\[sdrg stamps\]//' | cut -c1-250
