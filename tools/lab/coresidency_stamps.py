@@ -16,7 +16,7 @@ iqs = [bench.synth_device_frames(torch, dev, bench.B, seed=7 + k, n=bench.N, cs1
 specs = [torch.empty((bench.B, bench.N), dtype=torch.float32, device=dev) for _ in range(2)]
 recs = [torch.zeros((bench.B, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev) for _ in range(2)]
 pcm = torch.empty((bench.B, eng.pcm_len), dtype=torch.int16, device=dev)
-eng.set_pipelining(6)
+eng.set_pipelining(int(os.environ.get("LAB_PIPE_MODE", "6")))
 now, calls = [1000], [0]
 
 
@@ -32,7 +32,7 @@ def block(k, stages):
 
 
 S = sdrg
-legs = [("all", S.STAGE_ALL),
+legs = [("all", S.STAGE_ALL)] if os.environ.get("LAB_ALL_ONLY") else [("all", S.STAGE_ALL),
         ("no-stats", S.STAGE_SPECTRUM | S.STAGE_SSB | S.STAGE_AUDIO_PULSE),
         ("no-audio", S.STAGE_ALL & ~S.STAGE_AUDIO_PULSE),
         ("spectrum+ssb", S.STAGE_SPECTRUM | S.STAGE_SSB),
