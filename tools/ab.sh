@@ -30,7 +30,8 @@ run_env() {  # $1 = VARIANT spec: prints "KEY=VAL ..." for env
   [ "$1" != "$name" ] && knobs=${1#*:}
   local libname=${name%%+*} lib=$D/libsdrg.so  # NAME+TAG: the build NAME under another label (other knobs)
   [ "$libname" != "base" ] && lib=$D/libsdrg_$libname.so
-  echo "SDRG_LIB_PATH=$lib ${knobs//,/ }"
+  # knobs are split at commas that start a new KEY= (so a value may hold commas: SDRG_STREAM_PRIO=0,-1)
+  echo "SDRG_LIB_PATH=$lib $(echo "$knobs" | sed 's/,\([A-Z_][A-Z0-9_]*=\)/ \1/g')"
 }
 
 summarise() {
