@@ -231,6 +231,11 @@ constexpr int MAX_DONE = 8;     // FIR outputs completed per stream per chunk
 constexpr int PIPE_LDS_TARGET = 84 * 1024;  // > 80 KiB: at most one pipeline workgroup per CU
 
 constexpr int TAPS_ROW = CH + 256 + CH + 4;
+#ifndef SDRG_TAPS_COPIES  // lab: 2 copies (shifts 0, 1) read as 8-byte pairs free 3 KB of LDS against 4 (shifts 0-3, 16-byte reads)
+#define SDRG_TAPS_COPIES 4
+#endif
+constexpr int TAPS_COPIES = SDRG_TAPS_COPIES;
+static_assert(TAPS_COPIES == 4 || TAPS_COPIES == 2, "taps copies");
 // The low-pass wave one chunk behind the DC wave's output (1): its input ring gets a third slot and the wave runs
 // its whole loop as one asm block that reads the next chunk's first sub-blocks before each barrier (csrc/ssb_lpf_asm.h);
 // every later role moves one iteration later.  The raw-IQ batches shrink to 256 B x 3 to keep the LDS budget.
@@ -283,7 +288,7 @@ struct PipeLds {
     float fq[2][PG * MAX_DONE];
     // taps with CH zeros on both sides (out-of-window FIR steps multiply by 0), in 4 copies shifted by
     // 0..3 floats so that any 32-tap window is read with aligned ds_read_b128
-    float taps_sh[4][TAPS_ROW];
+    float taps_sh[TAPS_COPIES][TAPS_ROW];
 };
 // NCO variant only, in dynamic LDS: the current chunk's CH phasors {re, im}.  The two phasor tables (16 KiB) are read
 // from global memory (L1/L2-resident) a chunk ahead by the loader: in LDS they took the pipeline workgroup to 101.7 KiB,
@@ -374,7 +379,14 @@ __device__ __forceinline__ void fir_chunk(PipeLds &L, int c, int t0, int o_lo, i
         f2v lo[NP], hi[NP];
 #pragma unroll
         for (int j = 0; j < NP; j++) {
-            const float4 h = reinterpret_cast<const float4 *>(&L.taps_sh[k0[j] & 3][k0[j] & ~3])[i];
+            float4 h;
+            if constexpr (TAPS_COPIES == 4) {
+                h = reinterpret_cast<const float4 *>(&L.taps_sh[k0[j] & 3][k0[j] & ~3])[i];
+            } else {
+                const float2 *b2 = reinterpret_cast<const float2 *>(&L.taps_sh[k0[j] & 1][k0[j] & ~1]);
+                const float2 h01 = b2[2 * i], h23 = b2[2 * i + 1];
+                h = make_float4(h01.x, h01.y, h23.x, h23.y);
+            }
             lo[j] = f2v{x.x, x.y} * f2v{h.x, h.y};  // products are order-free: two per packed op
             hi[j] = f2v{x.z, x.w} * f2v{h.z, h.w};
         }
@@ -419,7 +431,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     const int nch = (S + CH - 1) / CH;
     const int D = p.decim, NT = p.n_taps, PL = p.pcm_len;
 
-    for (int i = tid; i < 4 * TAPS_ROW; i += PIPE_T) {
+    for (int i = tid; i < TAPS_COPIES * TAPS_ROW; i += PIPE_T) {
         const int sh = i / TAPS_ROW, j = i % TAPS_ROW;
         const int k = j + sh - CH;  // copy sh holds taps_pad[j + sh] at index j
         L.taps_sh[sh][j] = (k >= 0 && k < NT) ? taps[k] : 0.0f;
