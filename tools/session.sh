@@ -1,8 +1,12 @@
 #!/bin/bash
-# r5bj: SSB pipeline with two taps copies read as 8-byte pairs (lab SDRG_TAPS_COPIES=2, 3 KB less LDS): SSB tests on
-# the lab build, then the c3 line and the SSB stage alone against the product, alternating
+# r5f: HEAD check after the lab-only taps option (product code path unchanged): smoke, GPU suite, default bench line
 export TMPDIR=/tmp
 set -o pipefail
 mkdir -p gpurun_out
-bash tools/ab.sh -r 2 -o r5bj -t "tests/test_gpu_parity.py tests/test_gpu_ssb_variant.py tests/test_gpu_ssb_schedule.py" base taps2 -- \
-  python bench.py --no-cpu-baseline --no-labelled
+TAG=r5f
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo "smoke failed"; tail gpurun_out/${TAG}_smoke.log; exit 1; }
+tail -1 gpurun_out/${TAG}_smoke.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { echo "GPU tests failed"; tail -30 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
+tail -1 gpurun_out/${TAG}_gpu_tests.log
+timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/${TAG}_driverlike.json 2> gpurun_out/${TAG}_driverlike.err || { echo "bench failed"; tail gpurun_out/${TAG}_driverlike.err; exit 1; }
+python tools/bench_summary.py gpurun_out/${TAG}_driverlike.json | head -2
