@@ -892,9 +892,18 @@ __device__ float kth_smallest_wave(Visit visit, int k, int *hist, uint32_t *xch)
 // more than 64 allow and spilled).
 // Measured (tools/gpu_r4n.sh, alternating, one box): alone 27.2 vs 26.7 us per 4096 frames; the c3 step with the
 // statistics on their own stream 0.3077-0.3088 ms against 0.3121-0.3124 (76 VGPRs) and 0.3141 on the main stream.
-constexpr int NARROW_BATCH = 8;
+#ifndef SDRG_NARROW_BATCH  // lab: loads per lane in flight in the staging copy
+#define SDRG_NARROW_BATCH 8
+#endif
+#ifndef SDRG_NARROW_WPE  // lab: waves per SIMD the narrow kernel is compiled for
+#define SDRG_NARROW_WPE 8
+#endif
+#ifndef SDRG_STATS_ST_LDS  // lab: the stream's StatsState in LDS for the whole kernel instead of registers
+#define SDRG_STATS_ST_LDS 0
+#endif
+constexpr int NARROW_BATCH = SDRG_NARROW_BATCH;
 template <int R>
-__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(R > 8 ? 6 : 8))) void stats_narrow_kernel(
+__global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(R > 8 ? 6 : SDRG_NARROW_WPE))) void stats_narrow_kernel(
     const float *__restrict__ spectra, StatsGeometry g, int64_t now_ms, StatsState *__restrict__ state,
     sdrg_frame_record *__restrict__ records) {
     extern __shared__ __attribute__((aligned(16))) float stage[];
@@ -931,7 +940,16 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(R > 8 ? 6 
     __syncthreads();
     const int stage_total = sh_woff[n_ref + 1], stage_pad = (stage_total + 3) & ~3;
     const float *P = spectra + frame * (size_t)g.n;
+#if SDRG_STATS_ST_LDS
+    // one wave per workgroup: its LDS operations complete in order, so the copy lands before the writes below
+    __shared__ StatsState sh_st;
+    static_assert(sizeof(StatsState) % 4 == 0 && sizeof(StatsState) / 4 <= WAVE, "StatsState copy");
+    if (lane < (int)(sizeof(StatsState) / 4))
+        reinterpret_cast<uint32_t *>(&sh_st)[lane] = reinterpret_cast<const uint32_t *>(state + frame)[lane];
+    StatsState &st = sh_st;
+#else
     StatsState st = state[frame];
+#endif
     if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
     sdrg_frame_record rec;
     __builtin_memset(&rec, 0, sizeof(rec));  // tail padding included: records compare and gather as bytes
