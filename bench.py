@@ -45,6 +45,7 @@ ALG_BYTES_PER_SAMPLE = {"spectrum": 6.0}  # CS8: 2 B in + 4 B fftshifted float32
 ISO_LAUNCHES = 30  # launches of the spectrum stage alone behind roofline_isolated
 N_INPUTS = 3  # distinct input batches rotated per step: 3 x 128 MiB > the 256 MiB Infinity Cache
 SSB_ISO_CALLS = 20  # joined SSB-only calls timed for ssb_latency_floor.ssb_ms_alone
+PROFILED_STEPS = 20  # labelled lines: steps of the separate profiled pass behind their per-kernel times
 LAB_HOST_TIMES = os.environ.get("SDRG_BENCH_HOST_TIMES") == "1"
 LAB_NO_STEP_GATHER = os.environ.get("SDRG_BENCH_NO_STEP_GATHER") == "1"  # lab: the N > 1 path without its per-step gathers
 N_OUTPUTS = 3  # spectra / records buffers rotated per step (asynchronous statistics read a call's spectra late)
@@ -546,24 +547,30 @@ def main() -> int:
         eng.synchronize()
         ssb_iso_ms = eng.timing_stats()["ssb_ms"]
     d2d = d2d_copy_gbs(torch, dev)
+    stream_gbs = sdrg.measure_hbm_copy(local, 1 << 30, 10)  # the library's float4 streaming copy (roofline basis)
 
     def labelled_rate(st, k_steps, variant_on=False, mode=None):
-        """A separately labelled line measured in this same run: k_steps pipelined steps of stages st, with the
-        per-kernel times of those steps (HIP events on each kernel's stream, as kernel_ms), so a change of the line
-        between two records can be attributed to a kernel."""
+        """A separately labelled line measured in this same run: k_steps pipelined steps of stages st with profiling
+        off (value, ms_per_step), then a separate profiled pass of up to PROFILED_STEPS steps for the per-kernel times
+        (HIP events on each kernel's stream, as kernel_ms; an event marker costs a stream a few us, so it never sits in
+        the timed pass), so a change of the line between two records can be attributed to a kernel."""
         if variant_on:
             eng.set_ssb_variant(NCO_HZ, 127)
         eng.set_pipelining(pipe_mode if mode is None else mode)
-        eng.set_profiling(True)
+        eng.set_profiling(False)
         for _ in range(3):
             step(st)
         eng.synchronize()
-        eng.reset_timing_stats()
         t1 = time.perf_counter()
         for _ in range(k_steps):
             step(st)
         eng.synchronize()
         dt = time.perf_counter() - t1
+        eng.set_profiling(True)
+        eng.reset_timing_stats()
+        for _ in range(min(k_steps, PROFILED_STEPS)):
+            step(st)
+        eng.synchronize()
         tm = eng.timing_stats()
         eng.set_profiling(False)
         if variant_on:
@@ -585,7 +592,6 @@ def main() -> int:
         rc5 = [torch.zeros((s5, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev) for _ in range(N_OUTPUTS)]
         st5 = sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS
         torch.cuda.synchronize()
-        e5.set_profiling(True)
         if pipelined:  # each call's statistics beside the next call's spectrum (--stats-async)
             e5.set_pipelining(c5_mode)
         t5 = [1000]
@@ -597,11 +603,14 @@ def main() -> int:
                 t5[0] += n5 // 2000
         run(20)
         e5.synchronize()
-        e5.reset_timing_stats()
         t1 = time.perf_counter()
-        run(k_steps)
+        run(k_steps)  # profiling off: the value and ms_per_step
         e5.synchronize()
         dt = time.perf_counter() - t1
+        e5.set_profiling(True)  # a separate profiled pass for the per-kernel times
+        e5.reset_timing_stats()
+        run(min(k_steps, PROFILED_STEPS))
+        e5.synchronize()
         tm = e5.timing_stats()
         e5.close()
         ms = dt / k_steps * 1e3
@@ -703,10 +712,14 @@ def main() -> int:
         "roofline_isolated": {"kernel": kname, "bound": "hbm", "achieved": round(achieved_iso, 1),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_iso / HBM_PEAK_GBS, 4),
                               "measured": f"{ISO_LAUNCHES} launches of the spectrum stage alone after the timed region"},
-        "hbm_measured": {"d2d_copy_GBs": round(d2d, 1), "note": "device-to-device copy of 1 GiB, read + write bytes "
-                                                                "per second (SURVEY 8d's measured peak)",
-                         "frac_timed": round(achieved / d2d, 4) if d2d else None,
-                         "frac_isolated": round(achieved_iso / d2d, 4) if d2d else None},
+        "hbm_measured": {"stream_copy_GBs": round(stream_gbs, 1),
+                         "d2d_copy_GBs": round(d2d, 1),
+                         "note": "stream_copy: the library's float4 streaming copy of 1 GiB (sdrg_measure_hbm_copy: "
+                                 "nontemporal loads/stores, 16 workgroups per CU), read + write bytes per second, the "
+                                 "achievable rate the fractions below are priced against (MI355X_MICROARCH.md: 6.29 TB/s); "
+                                 "d2d_copy: a hipMemcpy D2D of 1 GiB, for comparison (the copy path is slower)",
+                         "frac_timed": round(achieved / stream_gbs, 4) if stream_gbs else None,
+                         "frac_isolated": round(achieved_iso / stream_gbs, 4) if stream_gbs else None},
         "roofline_step": {"bound": "hbm", "achieved": round(step_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(step_gbs / HBM_PEAK_GBS, 4),
                           "bytes_per_sample": round(step_bytes / (streams * n), 4),

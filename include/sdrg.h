@@ -527,9 +527,12 @@ typedef struct sdrg_gather_buffers {
 /* Enqueue the gathers (one RCCL group) behind the last process call's outputs they read, on the engine stream that
  * produced them: the statistics stream when that call ran its statistics asynchronously (its records, and the spectra
  * those statistics waited for), else the main stream; with PCM, the audio detector's stream (after the SSB stage).
- * No host synchronisation; a later call that writes a buffer a gather reads (the same pointer) waits for that gather
- * on the GPU first, and nothing else waits, so a caller rotating its output buffers overlaps the gathers with its next
- * calls.  Every rank calls it with the same selection.  Complete after sdrg_engine_synchronize (or on a stream after
+ * No host synchronisation; a later call that writes any byte a gather reads (byte ranges overlap: the same buffer, a
+ * slice of it, or an offset into it) waits for that gather on the GPU first, and nothing else waits, so a caller
+ * rotating its output buffers overlaps the gathers with its next calls.  Every rank calls it with the same selection
+ * (the stream choice above depends on it, and RCCL matches the ranks' gathers in issue order).  At world_size > 1 the
+ * path is compiled and checked only on one-rank communicators and on the world-2 CPU rehearsal: no two-GPU run has
+ * executed it.  Complete after sdrg_engine_synchronize (or on a stream after
  * sdrg_engine_wait_outputs).  Replaces nothing in the reference (one receiver per process): BASELINE configs[3]. */
 int32_t sdrg_engine_gather(sdrg_engine *eng, sdrg_dist *d, int32_t root, const sdrg_gather_buffers *bufs);
 /* Single-pair forms of sdrg_engine_gather. */
@@ -546,6 +549,10 @@ int32_t sdrg_engine_gather_pcm(sdrg_engine *eng, sdrg_dist *d, int32_t root, con
 int32_t sdrg_device_alloc(int32_t device, size_t bytes, void **out);
 int32_t sdrg_device_free(int32_t device, void *p);
 int32_t sdrg_memcpy(int32_t device, void *dst, const void *src, size_t bytes);
+/* Measurement (bench.py's roofline basis, not part of the reference's surface): the read + write GB/s of a float4
+ * streaming copy of `bytes` on `device` (nontemporal loads and stores, 16 workgroups per CU, `reps` timed launches
+ * after one untimed), the achievable HBM rate a memory-bound kernel is priced against beside the 8 TB/s spec. */
+int32_t sdrg_measure_hbm_copy(int32_t device, size_t bytes, int32_t reps, double *gbs);
 
 #ifdef __cplusplus
 }

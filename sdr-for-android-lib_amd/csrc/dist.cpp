@@ -65,6 +65,14 @@ const RcclApi &rccl() {
     return api;
 }
 
+// SDRG_OK if `device` names a HIP device of this process, else the failure (message via sdrg_last_error)
+int32_t check_device(int32_t device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(SDRG_E_NODEVICE, "no HIP device");
+    if (device < 0 || device >= count) return fail(SDRG_E_INVALID, "device %d out of range [0, %d)", device, count);
+    return SDRG_OK;
+}
+
 int32_t rccl_fail(const RcclApi &a, ncclResult_t r, const char *what) {
     return fail(SDRG_E_HIP, "%s: %s", what, a.error_string ? a.error_string(r) : "RCCL error");
 }
@@ -195,9 +203,7 @@ int32_t sdrg_device_alloc(int32_t device, size_t bytes, void **out) {
     if (!out) return fail(SDRG_E_INVALID, "null out");
     *out = nullptr;
     if (bytes == 0) return fail(SDRG_E_INVALID, "zero-byte device allocation");
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(SDRG_E_NODEVICE, "no HIP device");
-    if (device < 0 || device >= count) return fail(SDRG_E_INVALID, "device %d out of range [0, %d)", device, count);
+    if (const int32_t rc = check_device(device)) return rc;
     DeviceScope dscope(device);
     if (dscope.error() != hipSuccess) return fail(SDRG_E_HIP, "hipSetDevice(%d) failed", device);
     if (hipMalloc(out, bytes) != hipSuccess) {
@@ -209,15 +215,31 @@ int32_t sdrg_device_alloc(int32_t device, size_t bytes, void **out) {
 
 int32_t sdrg_device_free(int32_t device, void *p) {
     if (!p) return SDRG_OK;
+    if (const int32_t rc = check_device(device)) return rc;
     DeviceScope dscope(device);
+    if (dscope.error() != hipSuccess) return fail(SDRG_E_HIP, "hipSetDevice(%d) failed", device);
     if (hipFree(p) != hipSuccess) return fail(SDRG_E_HIP, "hipFree failed");
+    return SDRG_OK;
+}
+
+int32_t sdrg_measure_hbm_copy(int32_t device, size_t bytes, int32_t reps, double *gbs) {
+    if (!gbs) return fail(SDRG_E_INVALID, "null gbs");
+    *gbs = 0.0;
+    if (bytes < 16 || reps <= 0) return fail(SDRG_E_INVALID, "bytes %zu / reps %d", bytes, reps);
+    if (const int32_t rc = check_device(device)) return rc;
+    DeviceScope dscope(device);
+    if (dscope.error() != hipSuccess) return fail(SDRG_E_HIP, "hipSetDevice(%d) failed", device);
+    const hipError_t e = sdrg::measure_stream_copy(bytes, reps, gbs);
+    if (e != hipSuccess) return fail(SDRG_E_HIP, "stream copy probe: %s", hipGetErrorString(e));
     return SDRG_OK;
 }
 
 int32_t sdrg_memcpy(int32_t device, void *dst, const void *src, size_t bytes) {
     if ((!dst || !src) && bytes) return fail(SDRG_E_INVALID, "null buffer");
     if (!bytes) return SDRG_OK;
+    if (const int32_t rc = check_device(device)) return rc;
     DeviceScope dscope(device);
+    if (dscope.error() != hipSuccess) return fail(SDRG_E_HIP, "hipSetDevice(%d) failed", device);
     hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyDefault);  // synchronous with respect to the host
     if (e != hipSuccess) return fail(SDRG_E_HIP, "hipMemcpy: %s", hipGetErrorString(e));
     return SDRG_OK;

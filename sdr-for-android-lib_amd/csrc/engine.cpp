@@ -195,15 +195,20 @@ struct sdrg_engine {
     hipEvent_t ev_g[GRING] = {};
     int64_t g_calls = 0;
     struct GBuf {
-        const void *p;
+        uintptr_t lo, hi;  // the byte range [lo, hi) a gather reads
         int slot;
+        int64_t seq;       // g_calls of that gather (gathers run in call order: the latest covers the earlier ones)
     };
-    std::vector<GBuf> g_bufs;  // buffers read by gathers no later call has yet waited for
-    hipEvent_t gathering(const void *p) const {
-        if (p)
-            for (const GBuf &g : g_bufs)
-                if (g.p == p) return ev_g[g.slot];
-        return nullptr;
+    std::vector<GBuf> g_bufs;  // byte ranges read by gathers no later call has yet waited for
+    // the event of the latest gather that reads any byte of [p, p + bytes) (ranges, not base pointers: an output
+    // written at an offset into, or as a slice of, a gathered allocation still waits)
+    hipEvent_t gathering(const void *p, size_t bytes) const {
+        if (!p || !bytes) return nullptr;
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
+        const GBuf *best = nullptr;
+        for (const GBuf &g : g_bufs)
+            if (g.lo < hi && lo < g.hi && (!best || g.seq > best->seq)) best = &g;
+        return best ? ev_g[best->slot] : nullptr;
     }
     float *d_fft_scratch = nullptr;   // four-step intermediate (N > 16384)
     size_t fft_scratch_elems = 0;
@@ -550,12 +555,16 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         if (rc) return rc;
         recs = e->d_rec_scratch;
     }
+    // the byte ranges this call writes (checked against the ranges pending gathers read)
+    const size_t spec_bytes = (size_t)B * (size_t)n * sizeof(float), rec_bytes = (size_t)B * sizeof(sdrg_frame_record);
+    size_t pcm_bytes = 0;
     SsbParams sp;
     if (do_ssb) {
         // frame size and PCM length this call will use (sampCount freezes at the first SSB call, :224-227)
         const int64_t samp = ssb_frozen_or(e);
         const int plen = ssb_pcm_len(samp, (uint32_t)e->cfg.sample_rate, e->fir_taps);
         if (!pcm && plen > 0) return fail(SDRG_E_INVALID, "null pcm with SSB stage");
+        pcm_bytes = (size_t)B * (size_t)(plen > 0 ? plen : 0) * sizeof(int16_t);
         int32_t rc = ensure_device(&e->d_ssb_scratch, &e->ssb_scratch_elems, (size_t)B * ((size_t)samp + (size_t)plen));
         if (rc) return rc;
     }
@@ -654,7 +663,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         if (c >= 1 && e->sa_live[pv] && (e->sa_spec[pv] == spec || !async))
             HIP_TRY(hipStreamWaitEvent(sm, e->ev_stats_end[pv], 0));
     }
-    if (hipEvent_t g = do_spec ? e->gathering(spec) : nullptr) HIP_TRY(hipStreamWaitEvent(sm, g, 0));  // being gathered
+    if (hipEvent_t g = do_spec ? e->gathering(spec, spec_bytes) : nullptr) HIP_TRY(hipStreamWaitEvent(sm, g, 0));  // being gathered
     auto enqueue_spectrum = [&]() -> int32_t {
         if (do_spec) {
             HIP_TRY(launch_spectrum(iq, fmt, n, B, e->d_twiddles, spec, e->d_fft_scratch, sm, do_ssb && early_fork && !split,
@@ -673,7 +682,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             HIP_TRY(hipEventRecord(e->ev_fork, e->s_main));
             HIP_TRY(hipStreamWaitEvent(e->s_ssb, e->ev_fork, 0));
         }
-        if (hipEvent_t g = e->gathering(pcm)) HIP_TRY(hipStreamWaitEvent(e->s_ssb, g, 0));  // still being gathered
+        if (hipEvent_t g = e->gathering(pcm, pcm_bytes)) HIP_TRY(hipStreamWaitEvent(e->s_ssb, g, 0));  // still being gathered
         if (prof && ev->ssb_timed) HIP_TRY(hipEventRecord(ev->ssb0, e->s_ssb));
         // AudioPulseDetector::process(pcm) after processSSB_opt (ssb_processor.cpp:109): its per-sample front
         // end runs inside the SSB kernel on the PCM it produces, the detector right after
@@ -709,7 +718,7 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
             HIP_TRY(hipStreamWaitEvent(e->s_stats, e->ev_spec_done, 0));
             st = e->s_stats;
         }
-        if (hipEvent_t g = e->gathering(recs)) HIP_TRY(hipStreamWaitEvent(st, g, 0));  // still being gathered
+        if (hipEvent_t g = e->gathering(recs, rec_bytes)) HIP_TRY(hipStreamWaitEvent(st, g, 0));  // still being gathered
         HIP_TRY(launch_stats(spec, B, geo, now_ms, e->d_stats, recs, e->d_pool, st));
         if (do_sp) {  // spectralPulseDetector.process(best1kHzSnrSigma, best1kHzCenterFreqHz) (:477-479)
             int32_t rc = pulse_bank_spectral(&e->spec_bank, &recs->best1khz_snr_sigma, &recs->best1khz_center_freq_hz,
@@ -748,14 +757,18 @@ int32_t enqueue(sdrg_engine *e, const void *iq, int32_t fmt, int32_t stages, flo
         e->nco_phase = nco_next;
     }
     if (do_stats) e->cf_changed_pending = false;
-    // a buffer this call waited for is rewritten on a stream ordered after the gathers: no longer pending (the other
-    // gathered buffers stay pending until a call writes them)
-    const void *written[] = {do_spec ? (const void *)spec : nullptr, do_stats ? (const void *)recs : nullptr,
-                             do_ssb ? (const void *)pcm : nullptr};
-    for (const void *w : written)
-        if (w)
-            e->g_bufs.erase(std::remove_if(e->g_bufs.begin(), e->g_bufs.end(), [w](const sdrg_engine::GBuf &g) { return g.p == w; }),
+    // a gathered range this call wrote whole was waited for on a stream ordered after the gathers: no longer pending
+    // (ranges it wrote only in part, and the other gathered ranges, stay pending until a call writes them whole)
+    const std::pair<const void *, size_t> written[] = {{do_spec ? (const void *)spec : nullptr, spec_bytes},
+                                                       {do_stats ? (const void *)recs : nullptr, rec_bytes},
+                                                       {do_ssb ? (const void *)pcm : nullptr, pcm_bytes}};
+    for (const auto &w : written)
+        if (w.first) {
+            const uintptr_t lo = reinterpret_cast<uintptr_t>(w.first), hi = lo + w.second;
+            e->g_bufs.erase(std::remove_if(e->g_bufs.begin(), e->g_bufs.end(),
+                                           [lo, hi](const sdrg_engine::GBuf &g) { return lo <= g.lo && g.hi <= hi; }),
                             e->g_bufs.end());
+        }
     if (do_spec) e->last_in_main = mk_main_end;
     if (do_ssb) e->last_in_ssb = mk_ssb_end;
     if (do_spec || do_stats) e->last_async_stats = do_stats && async;
@@ -1537,14 +1550,18 @@ int32_t sdrg_engine_gather(sdrg_engine *e, sdrg_dist *d, int32_t root, const sdr
     e->g_calls++;
     // the buffers this gather reads, mapped to its slot; a slot re-recorded by a later gather still covers this one
     // (gathers follow each other)
-    const void *read[] = {g_rec ? (const void *)b->records : nullptr, g_foc ? (const void *)b->focus_spectra : nullptr,
-                          g_spec ? (const void *)b->spectra : nullptr, g_pcm ? (const void *)b->pcm : nullptr};
-    for (const void *r : read) {
-        if (!r) continue;
+    const std::pair<const void *, size_t> read[] = {
+        {g_rec ? (const void *)b->records : nullptr, B * sizeof(sdrg_frame_record)},
+        {g_foc ? (const void *)b->focus_spectra : nullptr, B * (size_t)n * sizeof(float)},
+        {g_spec ? (const void *)b->spectra : nullptr, B * (size_t)n * sizeof(float)},
+        {g_pcm ? (const void *)b->pcm : nullptr, B * (size_t)plen * sizeof(int16_t)}};
+    for (const auto &r : read) {
+        if (!r.first || !r.second) continue;
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(r.first), hi = lo + r.second;
         bool found = false;
         for (sdrg_engine::GBuf &g : e->g_bufs)
-            if (g.p == r) g.slot = slot, found = true;
-        if (!found) e->g_bufs.push_back({r, slot});
+            if (g.lo == lo && g.hi == hi) g.slot = slot, g.seq = e->g_calls - 1, found = true;
+        if (!found) e->g_bufs.push_back({lo, hi, slot, e->g_calls - 1});
     }
     return SDRG_OK;
 }

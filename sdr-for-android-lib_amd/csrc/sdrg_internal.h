@@ -100,12 +100,6 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
                       const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,
                       const AudioFront *audio, hipStream_t stream, hipEvent_t stop = nullptr,
                       bool *stop_recorded = nullptr);
-// ssb64.hip: the chain with 64 streams per serial wave (a front and a back workgroup per 64 streams); launch_ssb takes
-// it when ssb64_supported (scratch: [n_frames][samp_count] floats for the front -> back hand-off)
-bool ssb64_supported(const SsbParams &p, const void *iq, int fmt, int n_frames, int nsl_mask, bool have_scratch);
-hipError_t launch_ssb64(const void *iq, int fmt, int n_frames, const SsbParams &p, int nsl_mask, const int *chunk_table,
-                        const float *taps, SsbStreamState *state, float *scratch, int16_t *pcm, const AudioFront *audio,
-                        hipStream_t stream, hipEvent_t stop, bool *stop_recorded);
 
 // Pulse detectors (pulse.hip): one wavefront per stream.  Rings are [n_streams][cap] (cap = cap_mask + 1),
 // fh [n_streams][2][PULSE_FH_SLOTS].
@@ -137,6 +131,8 @@ int dist_device(const sdrg_dist *d);
 int dist_world(const sdrg_dist *d);
 int dist_rank(const sdrg_dist *d);
 // out[s][j] = spectra[s][lo + j], j < nb: each stream's focus-window slice, contiguous for the gather
+// gather.hip: the read + write GB/s of a float4 streaming copy of `bytes` (reps timed launches) on the current device
+hipError_t measure_stream_copy(size_t bytes, int reps, double *gbs);
 hipError_t launch_focus_pack(const float *spectra, int n_streams, int n, int lo, int nb, float *out, hipStream_t stream);
 
 }  // namespace sdrg

@@ -276,8 +276,19 @@ constexpr int batch_chunks() {  // chunks per RAWB-per-stream prefetch batch (DM
 #define SDRG_PIPE_MINW 6
 #endif
 constexpr int NRAW = SDRG_PIPE_NRAW;  // raw-IQ batches in LDS: one being unpacked, NRAW - 1 in flight
+// Synchronisation of the roles: 0 = one LDS-only workgroup barrier per chunk iteration, every role
+// a fixed number of chunks behind the loader; 1 = no barrier in the loop: each role publishes how many chunks it has
+// finished in an LDS counter (PipeLds::prog, layout SDRG_PROG_* from tools/gen/gen_lpf_asm.py) and waits only on the
+// counters of its producers (the chunk it reads is complete) and of its consumers (the ring slot it writes is free).
+// LDS executes one wave's operations in issue order, so a count that another wave can see was stored after every
+// LDS read and write of the chunks it counts; the poll is a plain LDS read, retried after s_sleep 1, bounded.
+#ifndef SDRG_PIPE_FLAGS
+#define SDRG_PIPE_FLAGS 0
+#endif
+static_assert(!SDRG_PIPE_FLAGS || SDRG_LPF_LOOKAHEAD, "the counter conditions assume the low-pass lookahead");
 
 struct PipeLds {
+    int prog[16];             // chunk counters (SDRG_PIPE_FLAGS): SDRG_PROG_* index, SDRG_PROG_ABORT the give-up word
     uint4 raw[NRAW][RAW_U4];  // raw IQ bytes of the prefetch batches (LDS-DMA), [piece][loader lane]
     float re[2][BUFF];
     float a[NA][BUFF];
@@ -298,6 +309,40 @@ constexpr int NCO_LDS_BYTES = 2 * CH * 4;
 
 __device__ __forceinline__ int ceil_div_i(int a, int b) {  // b > 0, any sign of a
     return a >= 0 ? (a + b - 1) / b : -((-a) / b);
+}
+
+// Chunk counters (SDRG_PIPE_FLAGS): plain LDS reads (volatile: re-read on every poll; through an LDS pointer, since
+// address-space inference leaves volatile accesses flat, and a flat load waits on vmcnt, i.e. on the loader's DMA too),
+// one lane stores.
+typedef int prog_v4 __attribute__((ext_vector_type(4)));
+typedef int prog_v2 __attribute__((ext_vector_type(2)));
+template <class T>
+__device__ __forceinline__ const volatile __attribute__((address_space(3))) T *prog_ptr(const PipeLds &L, int k) {
+    return (const volatile __attribute__((address_space(3))) T *)(&L.prog[k]);
+}
+__device__ __forceinline__ int prog1(const PipeLds &L, int k) { return *prog_ptr<int>(L, k); }
+__device__ __forceinline__ prog_v2 prog2(const PipeLds &L, int k) { return *prog_ptr<prog_v2>(L, k); }  // k even
+__device__ __forceinline__ prog_v4 prog4(const PipeLds &L, int k) { return *prog_ptr<prog_v4>(L, k); }  // k % 4 == 0
+__device__ __forceinline__ void prog_store(PipeLds &L, int k, int v) {
+    *(volatile __attribute__((address_space(3))) int *)(&L.prog[k]) = v;
+}
+__device__ __forceinline__ int min4(prog_v4 v) { return min(min(v.x, v.y), min(v.z, v.w)); }
+// Wait until ok() holds: poll after s_sleep 1, at most SDRG_PIPE_SPIN_LIMIT times (a wait that long means a broken
+// schedule: raise the abort word so that every other wait gives up at once, and run on with wrong results).
+template <class Ok>
+__device__ __forceinline__ void pipe_wait(PipeLds &L, int lane, Ok ok) {
+    if (ok()) return;
+    for (int n = 0; n < SDRG_PIPE_SPIN_LIMIT; ++n) {
+        __builtin_amdgcn_s_sleep(1);
+        if (prog1(L, SDRG_PROG_ABORT) != 0 || ok()) return;
+    }
+    if (lane == 0) prog_store(L, SDRG_PROG_ABORT, 1);
+}
+// Publish `count` finished chunks: after every LDS access of those chunks in program order (the asm barrier stops
+// the compiler moving them below the store; LDS keeps one wave's order)
+__device__ __forceinline__ void pipe_publish(PipeLds &L, int k, int count, int lane) {
+    asm volatile("" ::: "memory");
+    if (lane == 0) prog_store(L, k, count);
 }
 
 template <int FMT>
@@ -436,6 +481,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         const int k = j + sh - CH;  // copy sh holds taps_pad[j + sh] at index j
         L.taps_sh[sh][j] = (k >= 0 && k < NT) ? taps[k] : 0.0f;
     }
+    if (tid < 16) L.prog[tid] = 0;
 
     const int my_s = lane & (PG - 1);  // serial roles: lane = 16 x copy + stream (all 64 lanes run; lanes < PG store)
     // the hand-scheduled serial roles' lanes (SDRG_SERIAL_LANES): ser_on = the lane holds stream ser_s
@@ -499,13 +545,46 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             lds_barrier();
         }
     };
+    // body(c) for the chunks c = 0 .. nch-1 of a role whose counter is `k`: with the barrier at iteration c + off of
+    // the common loop; with the counters (SDRG_PIPE_FLAGS) as soon as ok(c) holds, then publishing c + 1
+    auto run = [&](int off, int k, auto &&ok, auto &&body) {
+#if SDRG_PIPE_FLAGS
+        (void)off;
+        for (int c = 0; c < nch; ++c) {
+            pipe_wait(L, lane, [&] { return ok(c); });
+            if (stamps) st_a = __builtin_amdgcn_s_memtime();
+            body(c);
+            if (stamps) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                st_work += __builtin_amdgcn_s_memtime() - st_a;
+            }
+            pipe_publish(L, k, c + 1, lane);
+        }
+#else
+        (void)k;
+        (void)ok;
+        chunk_loop([&](int it) {
+            const int c = it - off;
+            if (c >= 0 && c < nch) body(c);
+        });
+#endif
+    };
+    // this wave's counter (SDRG_PIPE_FLAGS)
+    const int my_prog = wave == W_DC ? SDRG_PROG_DC : wave == W_LPF ? SDRG_PROG_LPF : wave == W_AGC ? SDRG_PROG_AGC
+                      : wave == W_LOAD ? SDRG_PROG_LOAD : wave == W_FIR0 ? SDRG_PROG_FIR0 : wave == W_FIR1 ? SDRG_PROG_FIR1
+                      : wave == W_OUT ? SDRG_PROG_OUT : wave == W_EQ ? SDRG_PROG_EQ : SDRG_PROG_DES + (wave - W_DES0);
     if ((skip_mask >> wave) & 1) {
+#if SDRG_PIPE_FLAGS
+        pipe_publish(L, my_prog, nch, lane);
+#else
         chunk_loop([&](int) {});
+#endif
     } else if (wave == W_DC) {
         float dc = 0.0f;  // removeDC: reset per call (:50)
-        chunk_loop([&](int it) {
+        // needs: the loader's chunk c; the low-pass wave done with chunk c - 3 (it reads c - 2 during c - 3)
+        run(1, my_prog, [&](int c) { const prog_v2 f = prog2(L, SDRG_PROG_LPF); return (f.y >= c + 1) & (f.x >= c - 2); },
+            [&](int c) {
             // ---- removeDC (:49-55) and the a0*x term of iir2Process, chunk it-1 ----
-            const int c = it - 1;
             // the frame's last chunk runs whole too: dc restarts every frame and the samples past the frame end
             // (zeros from the loader) only feed outputs nothing reads
             const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
@@ -554,6 +633,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             const int nit = nch + 8 + LA;
             unsigned long long sv;
             int t_it, t_cc, t_r, t_yo;
+#if SDRG_PIPE_FLAGS
+            static_assert(SDRG_LPF_INTERLEAVE && !SDRG_SERIAL_LANES, "the counter loop is the interleaved 16-lane form");
+            (void)nit;
+            (void)t_it;
+            int t1, t2;
+            unsigned long long tm;
+            const uint32_t pbase = lds_addr(reinterpret_cast<const float *>(&L.prog[0]));
+            // no stamps inside the block: its work slot holds the loop start (see the report below)
+            asm volatile(SDRG_LPF_LOOP_FLAGS_ASM
+                         : [z] "+v"(z), [sv] "=&s"(sv), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo),
+                           [t1] "=&s"(t1), [t2] "=&s"(t2), [tm] "=&s"(tm)
+                         : [abase] "v"(abase), [ybase] "v"(ybase), [pbase] "v"(pbase), [c1] "s"(c1), [c2] "s"(c2),
+                           [nch] "s"(nch)
+                         : SDRG_CHUNK_CLOBBERS, "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "vcc",
+                           "memory");
+#else
             if (SDRG_LPF_INTERLEAVE && SDRG_SERIAL_LANES)
                 asm volatile(SDRG_LPF_LOOP_IL_SPREAD_ASM
                              : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
@@ -569,11 +664,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                              : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                              : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
                              : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+#endif
             z1 = z.x;
             z2 = z.y;
-        } else chunk_loop([&](int it) {
+        } else run(2 + LA, my_prog, [&](int c) {
+                // needs: the DC wave's chunk c; every reader of output slot c mod 4 done with chunk c - 4
+                const int dc = prog1(L, SDRG_PROG_DC), y = min(min4(prog4(L, SDRG_PROG_DES)), prog1(L, SDRG_PROG_OUT));
+                return (dc >= c + 1) & (y >= c - 3);
+            }, [&](int c) {
             // ---- iir2Process recurrence (:75-84), chunk it-2 ----
-            const int c = it - 2 - LA;
             if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 2) || lane < PG)) {
                 const int lim = min(CH, S - c * CH);
 #ifdef SDRG_DIAG_LPF_NOLDS  // diagnostic build only: the recurrence on register data, no LDS traffic
@@ -654,9 +753,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         // frame and outputs past the frame end are zeroed by the clamp role.
         const f2v rates = {p.agc_fast, 0.00035f};
         const f2v keep = {1.0f - p.agc_fast, 1.0f - 0.00035f};
-        chunk_loop([&](int it) {
+        // needs: the four desired-level waves' chunk c; the clamp wave done with chunk c - 2
+        run(4 + LA, my_prog, [&](int c) {
+                const int d = min4(prog4(L, SDRG_PROG_DES)), o = prog1(L, SDRG_PROG_OUT);
+                return (d >= c + 1) & (o >= c - 1);
+            },
+            [&](int c) {
             // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
-            const int c = it - 4 - LA;
             if (SDRG_AGC_ASM && !(SDRG_SERIAL_FULL_EXEC & 4) && c >= 0 && c < nch && ser_on) {
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 f2v g = {gain, gain};
@@ -694,7 +797,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             nco_l = nco_tab2[1024 + ((ph >> 12) & 1023)];
         };
         if (p.nco_on && nch > 0) nco_fetch(0);
-        chunk_loop([&](int it) {
+        // needs: the DC wave done with chunk c - 2 (slot c mod 2)
+        run(0, my_prog, [&](int c) { return prog1(L, SDRG_PROG_DC) >= c - 1; }, [&](int it) {
             const float2 nco_hc = nco_h, nco_lc = nco_l;  // chunk it's entries
             if (p.nco_on && it + 1 < nch) nco_fetch(it + 1);
             if constexpr (DMA) {
@@ -780,12 +884,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 }
             }
         });
+        // no LDS-DMA may still be writing when the workgroup's LDS is released
+        if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (wave == W_FIR0 || wave == W_FIR1) {
         float facc[MAX_SLOTS / 4] = {};  // FIR accumulators (slots j*4 + lane/16)
-        chunk_loop([&](int it) {
+        // needs: the clamp wave's chunk c; the equaliser done with chunk c - 2
+        run(6 + LA, my_prog, [&](int c) {
+                const int o = prog1(L, SDRG_PROG_OUT), e = prog1(L, SDRG_PROG_EQ);
+                return (o >= c + 1) & (e >= c - 1);
+            },
+            [&](int c) {
             // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot mod 4, stream); slot groups
             //      4j..4j+3 split between the two FIR waves ----
-            const int c = it - 6 - LA;
             if (c >= 0 && c < nch && PL > 0) {
                 const int4 r = chunk_out[c];  // outputs overlapping chunk c: [r.x, r.y] (host table, no division)
                 const int sl = lane % PG, sub = lane / PG;
@@ -802,12 +912,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             }
         });
     } else if (wave == W_OUT) {
-        chunk_loop([&](int it) {
+        // needs: the AGC wave's chunk c (the low-pass output of chunk c is older); both FIR waves done with chunk c - 2
+        run(5 + LA, my_prog, [&](int c) { const prog_v4 f = prog4(L, SDRG_PROG_AGC); return (f.x >= c + 1) & (min(f.y, f.z) >= c - 1); },
+            [&](int c) {
             // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5; zero beyond the frame end ----
             // lane = 4 x stream + part of 8 samples.  x = demodSSB(y, y) = y + y (upper) or y - y (lower)
             // is y * 2 or y * 0: equal values (the lower sideband's zero may carry y's sign, which the
             // clamp keeps and the FIR's sums absorb: acc + (+-0) == acc).  clamp == med3 for non-NaN input.
-            const int c = it - 5 - LA;
             if (c >= 0 && c < nch) {
 #pragma unroll
                 for (int g8 = 0; g8 < CH / 32; ++g8) {
@@ -850,9 +961,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         if (front && serial_live) fst = front_load(af.state + s0 + my_s);
         float *my_new = front ? af.new_e + (size_t)(serial_live ? s0 + my_s : 0) * (size_t)af.max_new : nullptr;
         int np = 0;
-        chunk_loop([&](int it) {
+        // needs: both FIR waves' chunk c
+        run(7 + LA, my_prog, [&](int c) { const prog_v4 f = prog4(L, SDRG_PROG_AGC); return min(f.y, f.z) >= c + 1; },
+            [&](int ce) {
             // ---- HP -> BP -> transientBoost -> floatToPCM on the outputs the FIR completed, chunk it-7 ----
-            const int ce = it - 7 - LA;
             if (ce >= 0 && ce < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
                 const int c = ce;
                 const int4 r = chunk_out[c];  // outputs completed in chunk c: [r.z, r.w]
@@ -885,13 +997,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             }
         }
     } else {
-        chunk_loop([&](int it) {
+        // needs: the low-pass wave's chunk c; the AGC wave done with chunk c - 2
+        run(3 + LA, my_prog, [&](int c) {
+                const int y = prog1(L, SDRG_PROG_LPF), a = prog1(L, SDRG_PROG_AGC);
+                return (y >= c + 1) & (a >= c - 1);
+            },
+            [&](int c) {
             // waves 8-11: lane = CH/16 consecutive samples of one stream (256 lanes = the 16 x CH chunk)
             constexpr int SPL = CH / 16;
             const int hl = (wave == W_DES0 ? 0 : wave == W_DES1 ? 1 : wave == W_DES2 ? 2 : 3) * 64 + lane;
             const int sl = hl / (CH / SPL), i0 = (hl % (CH / SPL)) * SPL;
             // ---- AGC "desired" level (:104-107), chunk it-3 ----
-            const int c = it - 3 - LA;
             if (c >= 0 && c < nch) {
 #pragma unroll
                 for (int h = 0; h < SPL; h += 2) {
@@ -1094,8 +1210,16 @@ int ssb_pipe_chunk(void) { return CH; }
 #ifndef SDRG_EXT_STOP
 #define SDRG_EXT_STOP 1
 #endif
-#ifndef SDRG_SSB64  // 1: the 64-stream front/back split where it applies (ssb64.hip)
+#ifndef SDRG_SSB64  // 1 (lab builds only): the 64-stream front/back split where it applies (tools/lab/ssb64.hip)
 #define SDRG_SSB64 0
+#endif
+#if SDRG_SSB64
+// tools/lab/ssb64.hip: the chain with 64 streams per serial wave (a front and a back workgroup per 64 streams); launch_ssb
+// takes it when ssb64_supported (scratch: [n_frames][samp_count] floats for the front -> back hand-off)
+bool ssb64_supported(const SsbParams &p, const void *iq, int fmt, int n_frames, int nsl_mask, bool have_scratch);
+hipError_t launch_ssb64(const void *iq, int fmt, int n_frames, const SsbParams &p, int nsl_mask, const int *chunk_table,
+                        const float *taps, SsbStreamState *state, float *scratch, int16_t *pcm, const AudioFront *audio,
+                        hipStream_t stream, hipEvent_t stop, bool *stop_recorded);
 #endif
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,

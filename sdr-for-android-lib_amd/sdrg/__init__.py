@@ -102,7 +102,7 @@ EXPORTS = [
     "sdrg_dist_unique_id", "sdrg_dist_create", "sdrg_dist_destroy", "sdrg_dist_info", "sdrg_dist_set_one_rank_rccl",
     "sdrg_engine_gather",
     "sdrg_engine_gather_records", "sdrg_engine_gather_focus", "sdrg_engine_gather_spectra", "sdrg_engine_gather_pcm",
-    "sdrg_device_alloc", "sdrg_device_free", "sdrg_memcpy",
+    "sdrg_device_alloc", "sdrg_device_free", "sdrg_memcpy", "sdrg_measure_hbm_copy",
 ]
 DIST_ID_BYTES = 128  # SDRG_DIST_ID_BYTES (ncclUniqueId)
 
@@ -295,6 +295,7 @@ def load() -> ctypes.CDLL:
         "sdrg_device_alloc": (_I32, [_I32, ctypes.c_size_t, ctypes.POINTER(P)]),
         "sdrg_device_free": (_I32, [_I32, P]),
         "sdrg_memcpy": (_I32, [_I32, P, P, ctypes.c_size_t]),
+        "sdrg_measure_hbm_copy": (_I32, [_I32, ctypes.c_size_t, _I32, ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -377,6 +378,14 @@ class DeviceBuffer:
             self.close()
         except Exception:
             pass
+
+
+def measure_hbm_copy(device: int = 0, nbytes: int = 1 << 30, reps: int = 10) -> float:
+    """Read + write GB/s of the library's float4 streaming copy of nbytes (sdrg_measure_hbm_copy): the achievable
+    HBM rate behind bench.py's roofline basis."""
+    g = ctypes.c_double(0.0)
+    _check(load().sdrg_measure_hbm_copy(device, nbytes, reps, ctypes.byref(g)), "sdrg_measure_hbm_copy")
+    return g.value
 
 
 def dist_unique_id() -> bytes:

@@ -27,6 +27,7 @@
 #include "sdrg_internal.h"
 #include "ssb_common.h"
 #include "ssb_lpf_asm.h"
+#include "ssb64_lpf_asm.h"
 #include "ssb_math.h"
 
 #pragma clang fp contract(off)
