@@ -342,6 +342,9 @@ typedef float f2s __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float4 pair4(f2 a, f2 b) { return make_float4(a.x, a.y, b.x, b.y); }
 
 // pass-0 outputs (radix 32, NS = 1: thread t writes slots 32 t + r) -> pass-1 inputs (thread t reads t + 512 r)
+#ifndef SDRG_K16_XCH_TRIM  // 1: the exchange addresses without the LDS base add per access (see exch1 / exch2); 0: as round 5
+#define SDRG_K16_XCH_TRIM 1
+#endif
 __device__ __forceinline__ void exch1(f2 *lds, f2 (&v)[E]) {
     const int t = threadIdx.x;
     char *lb = reinterpret_cast<char *>(lds);
@@ -350,14 +353,29 @@ __device__ __forceinline__ void exch1(f2 *lds, f2 (&v)[E]) {
     for (int h = 0; h < 2; ++h) {
         if ((t >= T / 2) == (h == 1)) {
             const int tp = t - h * (T / 2);
-            int row = 256 * tp + ((tp & 15) << 4);  // byte offset of the row, ORed with its XOR
-            asm volatile("" : "+v"(row));  // per frame: hoisted out of the frame loop, the 16 addresses hold 16 VGPRs
+            if constexpr (SDRG_K16_XCH_TRIM) {
+                // the row's LDS byte address with the buffer's base in it: the base is 256-byte aligned (the dynamic
+                // allocation starts the kernel's LDS), so the XOR of the unit index touches the row offset only, and
+                // each write costs one v_xor (the compiler's form also added the base, a relocation literal, per write)
+                uint32_t row = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)lb + 256 * tp + ((tp & 15) << 4);
+                asm volatile("" : "+v"(row));
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                *reinterpret_cast<float4 *>(lb + (row ^ (q << 4))) = pair4(v[2 * q], v[2 * q + 1]);
-                __builtin_amdgcn_sched_barrier(0);  // one pair's 4-register tuple at a time
+                for (int q = 0; q < 16; ++q) {
+                    typedef float v4f __attribute__((ext_vector_type(4)));
+                    const v4f x = {v[2 * q].x, v[2 * q].y, v[2 * q + 1].x, v[2 * q + 1].y};
+                    asm volatile("ds_write_b128 %0, %1" ::"v"(row ^ (q << 4)), "v"(x) : "memory");
+                }
+            } else {
+                int row = 256 * tp + ((tp & 15) << 4);  // byte offset of the row, ORed with its XOR
+                asm volatile("" : "+v"(row));  // per frame: hoisted out of the frame loop, the 16 addresses hold 16 VGPRs
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    *reinterpret_cast<float4 *>(lb + (row ^ (q << 4))) = pair4(v[2 * q], v[2 * q + 1]);
+                    __builtin_amdgcn_sched_barrier(0);  // one pair's 4-register tuple at a time
+                }
             }
         }
+        if constexpr (SDRG_K16_XCH_TRIM) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm writes
         __syncthreads();
         const f2 *rb = lds + (t ^ (2 * ((t >> 5) & 15)));
 #pragma unroll
@@ -369,20 +387,24 @@ __device__ __forceinline__ void exch1(f2 *lds, f2 (&v)[E]) {
 }
 
 // pass-1 outputs (radix 32, NS = 32: slots (t / 32) 1024 + t mod 32 + 32 r) -> pass-2 inputs (radix 16, butterflies
-// 2t and 2t + 1: slots 2t + b + 1024 r, read as float4 pairs)
+// 2t and 2t + 1: slots 2t + b + 1024 r, read as float4 pairs).  SDRG_K16_XCH_TRIM: a linear layout (no XOR): a
+// half-wave's writes of one r are 32 consecutive slots (256 B, every bank once) and a wave's float4 reads 1 KiB of
+// consecutive slots, so neither side conflicts, and every access is the thread's base plus a constant offset (no
+// address VALU; the XOR layout, shared with exch1's, cost one v_xor per write)
 __device__ __forceinline__ void exch2(f2 *lds, f2 (&v)[E]) {
     const int t = threadIdx.x;
     f2 nxt[E];
+    constexpr int X = SDRG_K16_XCH_TRIM ? 0 : 1;  // 1: the XOR layout
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         if (((t >> 5) >= 8) == (h == 1)) {
             int row = ((t >> 5) - 8 * h) * 1024 + (t & 31);
             asm volatile("" : "+v"(row));  // as in exch1
 #pragma unroll
-            for (int r = 0; r < 32; ++r) lds[(row ^ (2 * (r & 15))) + 32 * r] = v[r];
+            for (int r = 0; r < 32; ++r) lds[(row ^ (X * 2 * (r & 15))) + 32 * r] = v[r];
         }
         __syncthreads();
-        const float4 *rb = reinterpret_cast<const float4 *>(lds + ((2 * t) ^ (2 * ((t >> 4) & 15))));
+        const float4 *rb = reinterpret_cast<const float4 *>(lds + ((2 * t) ^ (X * 2 * ((t >> 4) & 15))));
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const float4 p = rb[512 * r];  // slots 2t, 2t + 1 of row 1024 r
