@@ -342,6 +342,9 @@ typedef float f2s __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float4 pair4(f2 a, f2 b) { return make_float4(a.x, a.y, b.x, b.y); }
 
 // pass-0 outputs (radix 32, NS = 1: thread t writes slots 32 t + r) -> pass-1 inputs (thread t reads t + 512 r)
+#ifndef SDRG_K16_FUSE_PROBE  // lab: extra VALU per thread and frame standing in for a fused statistics tail
+#define SDRG_K16_FUSE_PROBE 0
+#endif
 #ifndef SDRG_K16_XCH_TRIM  // 1: the exchange addresses without the LDS base add per access (see exch1 / exch2); 0: as round 5
 #define SDRG_K16_XCH_TRIM 1
 #endif
@@ -596,6 +599,21 @@ __device__ __forceinline__ void spectrum16k_body(const void *__restrict__ iq, fl
             asm("v_fma_f32 %0, %1, %1, %2" : "=v"(p1) : "v"(x1[r].x), "v"(q1));
             pw[r] = f2s{p0, p1};
         }
+#if SDRG_K16_FUSE_PROBE
+        // lab: the VALU a fused narrow-statistics tail would add, as independent packed FMAs on the
+        // frame's powers (no dependency chain, no LDS, no barrier: the best case for the fusion), SDRG_K16_FUSE_PROBE
+        // per thread and frame; kept alive without a store.  The statistics issue ~3016 VALU per frame (one wave):
+        // spread over the workgroup's 8 waves, 377 per thread.
+        {
+            f2s acc[8] = {pw[0], pw[1], pw[2], pw[3], pw[4], pw[5], pw[6], pw[7]};
+#pragma unroll
+            for (int i = 0; i < SDRG_K16_FUSE_PROBE / 8; ++i)
+#pragma unroll
+                for (int a = 0; a < 8; ++a) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(acc[a]) : "v"(pw[(8 * i + a) & 15]), "v"(pw[(8 * i + a + 5) & 15]));
+#pragma unroll
+            for (int a = 0; a < 8; ++a) asm volatile("; keep %0" ::"v"(acc[a]));
+        }
+#endif
         if constexpr (STAGE) issue_raw<FMT>(iq, next < n_frames ? next : frame, src, raw, next < n_frames);
         float *o = spectra + (size_t)frame * N + 2 * t;
         if constexpr (ABL & 16) {  // keep the values live without the stores
