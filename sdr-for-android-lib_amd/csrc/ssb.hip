@@ -249,6 +249,10 @@ constexpr int LA = SDRG_LPF_LOOKAHEAD ? 1 : 0;
 #define SDRG_LPF_INTERLEAVE 1
 #endif
 constexpr int NA = 2 + LA;  // slots of the DC -> low-pass ring
+// lab: the low-pass loop on all 64 lanes as four copies of the 16 streams (full EXEC for the dependent chain)
+#ifndef SDRG_LPF_COPIES
+#define SDRG_LPF_COPIES 0
+#endif
 #ifndef SDRG_PIPE_RAWB  // bytes of raw IQ per stream per prefetch batch
 #define SDRG_PIPE_RAWB (SDRG_LPF_LOOKAHEAD ? 256 : 512)
 #endif
@@ -286,6 +290,7 @@ constexpr int NRAW = SDRG_PIPE_NRAW;  // raw-IQ batches in LDS: one being unpack
 #define SDRG_PIPE_FLAGS 0
 #endif
 static_assert(!SDRG_PIPE_FLAGS || SDRG_LPF_LOOKAHEAD, "the counter conditions assume the low-pass lookahead");
+static_assert(!SDRG_LPF_COPIES || (SDRG_LPF_INTERLEAVE && !SDRG_SERIAL_LANES && !SDRG_PIPE_FLAGS), "copies: the IL loop");
 
 struct PipeLds {
     int prog[16];             // chunk counters (SDRG_PIPE_FLAGS): SDRG_PROG_* index, SDRG_PROG_ABORT the give-up word
@@ -649,7 +654,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                          : SDRG_CHUNK_CLOBBERS, "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "vcc",
                            "memory");
 #else
-            if (SDRG_LPF_INTERLEAVE && SDRG_SERIAL_LANES)
+            if (SDRG_LPF_COPIES)  // lab: four copies of the 16 streams on all 64 lanes (lane l: stream l mod 16)
+                asm volatile(SDRG_LPF_LOOP_IL_COPIES_ASM
+                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
+                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+            else if (SDRG_LPF_INTERLEAVE && SDRG_SERIAL_LANES)
                 asm volatile(SDRG_LPF_LOOP_IL_SPREAD_ASM
                              : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                              : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)

@@ -238,7 +238,7 @@ def lpf_loop():
     return out
 
 
-def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3):
+def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copies=False):
     """lpf_loop() with the LDS traffic spread through the VALU stream: sub-blocks are numbered g = 4c + sb across
     chunks and live in buffer g mod 3; while sub-block g runs, after each 4-sample quad t its output quad is written
     and quad t of sub-block g + 2 is read (for sb = 2, 3 that is the next chunk's sub-block 0, 1, complete in its
@@ -248,8 +248,10 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3):
     out = []
     u = "%="
     # the 16 stream lanes: 0-15, or (spread) lanes {0-3, 16-19, 32-35, 48-51}; all_lanes: 64 streams, one per lane
-    # (ssb64.hip), with `slot` bytes per ring slot and the output ring's slot = chunk & ymask
-    lanes = (["s_mov_b64 exec, -1"] if all_lanes else
+    # (ssb64.hip), with `slot` bytes per ring slot and the output ring's slot = chunk & ymask; copies (lab): all 64 lanes,
+    # lane l running stream l mod 16 (four identical copies: a dependent chain issues faster on a full EXEC mask, and
+    # the copies write the same values to the same LDS addresses)
+    lanes = (["s_mov_b64 exec, -1"] if all_lanes or copies else
              ["s_mov_b32 exec_lo, 0xf000f", "s_mov_b32 exec_hi, 0xf000f"] if spread else ["s_mov_b64 exec, 0xffff"])
     out += ["s_mov_b64 %[sv], exec"] + lanes + [
         "s_nop 4",
@@ -482,6 +484,8 @@ def main():
     for k, v in PROG.items():
         print(f"#define SDRG_PROG_{k.upper()} {v // 4}")
     print(f"#define SDRG_PIPE_SPIN_LIMIT {SPIN_LIMIT}")
+    print("// lab (SDRG_LPF_COPIES=1): the same loop on all 64 lanes, lane l running stream l mod 16 (four copies)")
+    emit("SDRG_LPF_LOOP_IL_COPIES_ASM", lpf_loop_interleaved(copies=True))
     print("// the same on the lanes {0-3, 16-19, 32-35, 48-51} (SDRG_SERIAL_LANES=1)")
     emit("SDRG_LPF_LOOP_IL_SPREAD_ASM", lpf_loop_interleaved(spread=True))
     print("// the low-pass chunk with its VALU on all 64 lanes and the LDS operations on the caller's lanes; extra operand")
