@@ -253,6 +253,18 @@ constexpr int NA = 2 + LA;  // slots of the DC -> low-pass ring
 #ifndef SDRG_LPF_COPIES
 #define SDRG_LPF_COPIES 0
 #endif
+// The low-pass outputs through a global ring instead of LDS (tools/lab/lpf_io.hip: a ds_write_b128 on the wave's 16
+// lanes costs it ~8 cycles per sample, a global_store_dwordx4 ~5): the wave stores each chunk to slot c mod GRING of its
+// workgroup's ring in the SSB scratch, waits at each barrier until only its current chunk's stores are in flight, and
+// the readers (desired-level waves, clamp) load a chunk one iteration later than from LDS, past L1 (sc1)
+#ifndef SDRG_LPF_GSTORE
+#define SDRG_LPF_GSTORE 0
+#endif
+constexpr int GS = SDRG_LPF_GSTORE ? 1 : 0;  // extra iterations of lag for every role after the low-pass
+// lab: the low-pass adds with the running sum as src1 (a + b == b + a: the same bits)
+#ifndef SDRG_LPF_SRC1
+#define SDRG_LPF_SRC1 0
+#endif
 #ifndef SDRG_PIPE_RAWB  // bytes of raw IQ per stream per prefetch batch
 #define SDRG_PIPE_RAWB (SDRG_LPF_LOOKAHEAD ? 256 : 512)
 #endif
@@ -297,7 +309,7 @@ struct PipeLds {
     uint4 raw[NRAW][RAW_U4];  // raw IQ bytes of the prefetch batches (LDS-DMA), [piece][loader lane]
     float re[2][BUFF];
     float a[NA][BUFF];
-    float y[4][BUFF];
+    float y[4][BUFF];  // the low-pass outputs (SDRG_LPF_GSTORE: unused, kept so the other rings keep their offsets)
     float d[2][BUFF];
     float g[2][BUFF];
     float out[2][BUFF];
@@ -460,7 +472,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                                                           int nsl_mask, const int4 *__restrict__ chunk_out,
                                                           const float *__restrict__ taps,
                                                           SsbStreamState *__restrict__ state,
-                                                          int16_t *__restrict__ pcm,
+                                                          int16_t *__restrict__ pcm, float *__restrict__ yring,
                                                           unsigned long long *__restrict__ stamps, int prio_mask,
                                                           int skip_mask, unsigned long long role_map, AudioFront af) {
 #if SDRG_PIPE_DYN_LDS  // the whole LDS dynamic: the compiler's occupancy model then sees no LDS limit
@@ -480,6 +492,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     const int S = p.samp_count;
     const int nch = (S + CH - 1) / CH;
     const int D = p.decim, NT = p.n_taps, PL = p.pcm_len;
+    // the low-pass outputs of chunk c, stream row sl: the LDS ring, or (SDRG_LPF_GSTORE) slot c mod GRING of this
+    // workgroup's global ring ([slot][stream][CH] floats), read past L1 (sc1: the stores came from another wave of the CU)
+#if SDRG_LPF_GSTORE
+    // (formed where used: values live across the role branches would take VGPRs from every role)
+    auto y_wg = [&]() { return yring + (size_t)blockIdx.x * SDRG_LPF_GRING * PG * CH; };
+    auto y_row = [&](int c, int sl) { return y_wg() + ((c & (SDRG_LPF_GRING - 1)) * PG + sl) * CH; };
+    auto y_load4 = [&](int c, int sl, int i) {
+        const __amdgpu_buffer_rsrc_t y_rs =
+            __builtin_amdgcn_make_buffer_rsrc(y_wg(), (short)0, SDRG_LPF_GRING * PG * CH * 4, 0x00020000);
+        const auto u = __builtin_amdgcn_raw_buffer_load_b128(y_rs, (((c & (SDRG_LPF_GRING - 1)) * PG + sl) * CH + i) * 4, 0, 16);
+        return make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
+    };
+#else
+    (void)yring;
+    auto y_row = [&](int c, int sl) { return &L.y[c & 3][sl * ROW]; };
+#endif
 
     for (int i = tid; i < TAPS_COPIES * TAPS_ROW; i += PIPE_T) {
         const int sh = i / TAPS_ROW, j = i % TAPS_ROW;
@@ -540,7 +568,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     // the register allocator sees one role per loop and the kernel's VGPR count is the largest role's,
     // not the sum of every role's loop-invariant values.
     auto chunk_loop = [&](auto &&body) {
-        for (int it = 0; it < nch + 8 + LA; ++it) {
+        for (int it = 0; it < nch + 8 + LA + GS; ++it) {
             if (stamps) st_a = __builtin_amdgcn_s_memtime();
             body(it);
             if (stamps) {
@@ -634,8 +662,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             // the whole loop as one block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py): nch + 8 + LA iterations
             // with one s_barrier each, the same count as every other role's chunk_loop
             f2v z = {z1, z2};
+#if SDRG_LPF_GSTORE
+            const uint32_t abase = lds_addr(&L.a[0][ser_s * ROW]), ybase = (uint32_t)(ser_s * CH * 4);
+#else
             const uint32_t abase = lds_addr(&L.a[0][ser_s * ROW]), ybase = lds_addr(&L.y[0][ser_s * ROW]);
-            const int nit = nch + 8 + LA;
+#endif
+            const int nit = nch + 8 + LA + GS;
             unsigned long long sv;
             int t_it, t_cc, t_r, t_yo;
 #if SDRG_PIPE_FLAGS
@@ -653,8 +685,27 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                            [nch] "s"(nch)
                          : SDRG_CHUNK_CLOBBERS, "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "vcc",
                            "memory");
+#elif SDRG_LPF_GSTORE
+            static_assert(SDRG_LPF_INTERLEAVE && !SDRG_SERIAL_LANES && !SDRG_LPF_COPIES && !SDRG_LPF_SRC1, "gstore: the IL loop");
+            static_assert(PG * CH * 4 == (1 << SDRG_LPF_GSLOT_LOG2), "global ring slot");
+            float *ygs = yring + (size_t)blockIdx.x * SDRG_LPF_GRING * PG * CH;
+            asm volatile(SDRG_LPF_LOOP_IL_GSTORE_ASM
+                         : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                         : [abase] "v"(abase), [ybase] "v"(ybase), [ygs] "s"(ygs), [c1] "s"(c1), [c2] "s"(c2),
+                           [nit] "s"(nit), [nch] "s"(nch)
+                         : SDRG_CHUNK_CLOBBERS, "v54", "memory");
 #else
-            if (SDRG_LPF_COPIES)  // lab: four copies of the 16 streams on all 64 lanes (lane l: stream l mod 16)
+            if (SDRG_LPF_COPIES && SDRG_LPF_SRC1)
+                asm volatile(SDRG_LPF_LOOP_IL_COPIES_SRC1_ASM
+                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
+                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+            else if (SDRG_LPF_SRC1)
+                asm volatile(SDRG_LPF_LOOP_IL_SRC1_ASM
+                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
+                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+            else if (SDRG_LPF_COPIES)  // lab: four copies of the 16 streams on all 64 lanes (lane l: stream l mod 16)
                 asm volatile(SDRG_LPF_LOOP_IL_COPIES_ASM
                              : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                              : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
@@ -699,10 +750,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                     }
                 } else
 #endif
-                if (lim == CH && SDRG_LPF_ASM && !(SDRG_SERIAL_FULL_EXEC & 2)) {
+                if (lim == CH && SDRG_LPF_ASM && !GS && !(SDRG_SERIAL_FULL_EXEC & 2)) {
                     // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                     f2v z = {z1, z2};
-                    const uint32_t src = lds_addr(&L.a[c % NA][my_s * ROW]), dst = lds_addr(&L.y[c & 3][my_s * ROW]);
+                    const uint32_t src = lds_addr(&L.a[c % NA][my_s * ROW]), dst = lds_addr(y_row(c, my_s));
                     if (SDRG_LPF_ASM == 3) {  // lab: the chain on register data, no LDS (wrong results)
                         asm volatile(SDRG_LPF_CHUNK_NOLDS_ASM
                                      : [z] "+v"(z)
@@ -729,7 +780,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                     z1 = z.x;
                     z2 = z.y;
                 } else if (lim == CH) {
-                    row_pipeline(&L.a[c % NA][my_s * ROW], &L.y[c & 3][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
+                    row_pipeline(&L.a[c % NA][my_s * ROW], y_row(c, my_s), lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                         for (int q = 0; q < SB; q++) {
                             const f2v p1 = c1 * z1, p2 = c2 * z2;
@@ -747,10 +798,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                         const float y = (((L.a[c % NA][my_s * ROW + q] + p1.x) + p2.x) + p1.y) + p2.y;
                         z2 = z1;
                         z1 = y;
-                        if (lane < PG) L.y[c & 3][my_s * ROW + q] = y;
+                        if (lane < PG) y_row(c, my_s)[q] = y;
                     }
                 }
             }
+            // global ring: the chunk's stores complete before the barrier (its readers load it one iteration later)
+            if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         });
         if ((lpf_asm_loop ? ser_on : lane < PG) && s0 + ls < n_frames) {
             state[s0 + ls].lpf_z1 = z1;
@@ -764,7 +817,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         const f2v rates = {p.agc_fast, 0.00035f};
         const f2v keep = {1.0f - p.agc_fast, 1.0f - 0.00035f};
         // needs: the four desired-level waves' chunk c; the clamp wave done with chunk c - 2
-        run(4 + LA, my_prog, [&](int c) {
+        run(4 + LA + GS, my_prog, [&](int c) {
                 const int d = min4(prog4(L, SDRG_PROG_DES)), o = prog1(L, SDRG_PROG_OUT);
                 return (d >= c + 1) & (o >= c - 1);
             },
@@ -899,7 +952,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     } else if (wave == W_FIR0 || wave == W_FIR1) {
         float facc[MAX_SLOTS / 4] = {};  // FIR accumulators (slots j*4 + lane/16)
         // needs: the clamp wave's chunk c; the equaliser done with chunk c - 2
-        run(6 + LA, my_prog, [&](int c) {
+        run(6 + LA + GS, my_prog, [&](int c) {
                 const int o = prog1(L, SDRG_PROG_OUT), e = prog1(L, SDRG_PROG_EQ);
                 return (o >= c + 1) & (e >= c - 1);
             },
@@ -923,7 +976,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         });
     } else if (wave == W_OUT) {
         // needs: the AGC wave's chunk c (the low-pass output of chunk c is older); both FIR waves done with chunk c - 2
-        run(5 + LA, my_prog, [&](int c) { const prog_v4 f = prog4(L, SDRG_PROG_AGC); return (f.x >= c + 1) & (min(f.y, f.z) >= c - 1); },
+        run(5 + LA + GS, my_prog, [&](int c) { const prog_v4 f = prog4(L, SDRG_PROG_AGC); return (f.x >= c + 1) & (min(f.y, f.z) >= c - 1); },
             [&](int c) {
             // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5; zero beyond the frame end ----
             // lane = 4 x stream + part of 8 samples.  x = demodSSB(y, y) = y + y (upper) or y - y (lower)
@@ -933,9 +986,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
 #pragma unroll
                 for (int g8 = 0; g8 < CH / 32; ++g8) {
                     const int sl = lane >> 2, part = lane & 3, within = part * (CH / 4) + g8 * 8;
-                    const float *yr = &L.y[c & 3][sl * ROW + within];
                     const float *gr = &L.g[c & 1][sl * ROW + within];
+#if SDRG_LPF_GSTORE
+                    const float4 ya = y_load4(c, sl, within), yb = y_load4(c, sl, within + 4);
+#else
+                    const float *yr = &L.y[c & 3][sl * ROW + within];
                     const float4 ya = *reinterpret_cast<const float4 *>(yr), yb = *reinterpret_cast<const float4 *>(yr + 4);
+#endif
                     const float4 ga = *reinterpret_cast<const float4 *>(gr), gb = *reinterpret_cast<const float4 *>(gr + 4);
                     const f2v k2 = {demod_k, demod_k};
                     f2v o[4] = {(f2v{ya.x, ya.y} * k2) * f2v{ga.x, ga.y}, (f2v{ya.z, ya.w} * k2) * f2v{ga.z, ga.w},
@@ -972,7 +1029,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         float *my_new = front ? af.new_e + (size_t)(serial_live ? s0 + my_s : 0) * (size_t)af.max_new : nullptr;
         int np = 0;
         // needs: both FIR waves' chunk c
-        run(7 + LA, my_prog, [&](int c) { const prog_v4 f = prog4(L, SDRG_PROG_AGC); return min(f.y, f.z) >= c + 1; },
+        run(7 + LA + GS, my_prog, [&](int c) { const prog_v4 f = prog4(L, SDRG_PROG_AGC); return min(f.y, f.z) >= c + 1; },
             [&](int ce) {
             // ---- HP -> BP -> transientBoost -> floatToPCM on the outputs the FIR completed, chunk it-7 ----
             if (ce >= 0 && ce < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
@@ -1008,7 +1065,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         }
     } else {
         // needs: the low-pass wave's chunk c; the AGC wave done with chunk c - 2
-        run(3 + LA, my_prog, [&](int c) {
+        run(3 + LA + GS, my_prog, [&](int c) {
                 const int y = prog1(L, SDRG_PROG_LPF), a = prog1(L, SDRG_PROG_AGC);
                 return (y >= c + 1) & (a >= c - 1);
             },
@@ -1019,9 +1076,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             const int sl = hl / (CH / SPL), i0 = (hl % (CH / SPL)) * SPL;
             // ---- AGC "desired" level (:104-107), chunk it-3 ----
             if (c >= 0 && c < nch) {
+#if SDRG_LPF_GSTORE
+                static_assert(SPL == 4, "one 16-byte load per lane");
+                const float4 y4 = y_load4(c, sl, i0);
+#endif
 #pragma unroll
                 for (int h = 0; h < SPL; h += 2) {
+#if SDRG_LPF_GSTORE
+                    const float2 y2 = h == 0 ? make_float2(y4.x, y4.y) : make_float2(y4.z, y4.w);
+#else
                     const float2 y2 = *reinterpret_cast<const float2 *>(&L.y[c & 3][sl * ROW + i0 + h]);
+#endif
                     // fabsf(demodSSB(y, y)) == |y| * k exactly (k = 2 or 0)
                     const f2v a = f2v{fabsf(y2.x), fabsf(y2.y)} * f2v{demod_k, demod_k};
                     // target / (sqrtf(fabsf(a) + 1e-8f) + 1e-6f), correctly rounded, two lanes per op (ssb_math.h)
@@ -1251,7 +1316,11 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
         return launch_ssb64(iq, fmt, n_frames, p, nsl_mask, chunk_table, taps, state, scratch, pcm, audio, stream, stop,
                             stop_recorded);
 #endif
-    if (chunk_out && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels()) {
+    // SDRG_LPF_GSTORE: the low-pass ring lives in the SSB scratch ([n_frames][samp_count + pcm_len] floats)
+    float *yring = scratch;
+    const bool ring_ok = !GS || (scratch && (size_t)((n_frames + PG - 1) / PG) * SDRG_LPF_GRING * PG * CH <=
+                                                (size_t)n_frames * (size_t)p.samp_count);
+    if (chunk_out && ring_ok && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels()) {
         const dim3 grid((n_frames + PG - 1) / PG);
         size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
         if (p.nco_on && pad < (size_t)NCO_LDS_BYTES) pad = NCO_LDS_BYTES;  // the dynamic part holds the chunk phasors
@@ -1308,13 +1377,13 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
     if (ext)                                                                                                     \
         hipExtLaunchKernelGGL(dma ? ssb_pipe_kernel<F, true> : ssb_pipe_kernel<F, false>, grid, dim3(PIPE_T),   \
                               (uint32_t)pad, stream, nullptr, stop, 0u, src, n_frames, p, nsl_mask, chunk_out, taps,   \
-                              state, pcm, stamps, prio_mask, skip_mask, role_map, af);                           \
+                              state, pcm, yring, stamps, prio_mask, skip_mask, role_map, af);                    \
     else if (dma)                                                                                                \
         hipLaunchKernelGGL((ssb_pipe_kernel<F, true>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
-                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map, af);                                                \
+                           chunk_out, taps, state, pcm, yring, stamps, prio_mask, skip_mask, role_map, af);                                         \
     else                                                                                                         \
         hipLaunchKernelGGL((ssb_pipe_kernel<F, false>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
-                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map, af);
+                           chunk_out, taps, state, pcm, yring, stamps, prio_mask, skip_mask, role_map, af);
         switch (fmt) {
         case SDRG_IQ_CS8: SDRG_PIPE_LAUNCH(SDRG_IQ_CS8); break;
         case SDRG_IQ_CU8: SDRG_PIPE_LAUNCH(SDRG_IQ_CU8); break;

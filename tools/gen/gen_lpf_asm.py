@@ -35,17 +35,20 @@ def pair(reg):
     return f"v[{base}:{base + 1}]", reg & 1
 
 
-def lpf_sample(x, z1, z2):
-    """x: input/output VGPR; z1, z2: (pair text, half) of the previous two outputs"""
+def lpf_sample(x, z1, z2, src1=False):
+    """x: input/output VGPR; z1, z2: (pair text, half) of the previous two outputs.  src1 (lab): the running sum, the
+    operand each add waits for, as src1 (a + b == b + a exactly; tools/lab/lpf_exec.hip timed a dependent add whose fresh
+    operand is src1 faster on a partial EXEC mask)"""
     p1, h1 = z1
     p2, h2 = z2
+    add = (lambda a: f"v_add_f32 v{x}, v{a}, v{x}") if src1 else (lambda a: f"v_add_f32 v{x}, v{x}, v{a}")
     return [
         f"v_pk_mul_f32 v[{P1}:{P1 + 1}], %[c1], {p1} op_sel:[0,{h1}] op_sel_hi:[1,{h1}]",
         f"v_pk_mul_f32 v[{P2}:{P2 + 1}], %[c2], {p2} op_sel:[0,{h2}] op_sel_hi:[1,{h2}]",
-        f"v_add_f32 v{x}, v{x}, v{P1}",
-        f"v_add_f32 v{x}, v{x}, v{P2}",
-        f"v_add_f32 v{x}, v{x}, v{P1 + 1}",
-        f"v_add_f32 v{x}, v{x}, v{P2 + 1}",
+        add(P1),
+        add(P2),
+        add(P1 + 1),
+        add(P2 + 1),
     ]
 
 
@@ -238,13 +241,22 @@ def lpf_loop():
     return out
 
 
-def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copies=False):
+GSLOT_LOG2 = 12  # SDRG_LPF_GSTORE: bytes per chunk slot of the global output ring (16 streams x 64 floats), 8 slots
+GRING = 8
+
+
+def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copies=False, src1=False, gstore=False):
     """lpf_loop() with the LDS traffic spread through the VALU stream: sub-blocks are numbered g = 4c + sb across
     chunks and live in buffer g mod 3; while sub-block g runs, after each 4-sample quad t its output quad is written
     and quad t of sub-block g + 2 is read (for sb = 2, 3 that is the next chunk's sub-block 0, 1, complete in its
     ring slot).  So at the barrier only the chunk's last write is outstanding (lgkmcnt(1)), and the first two
     sub-blocks of the next chunk are already in registers.  The last chunk's reads of a next chunk fetch a stale
-    ring slot and are never used; the block drains them (lgkmcnt(0)) before it ends."""
+    ring slot and are never used; the block drains them (lgkmcnt(0)) before it ends.
+    gstore (SDRG_LPF_GSTORE): the outputs go to a global ring of GRING chunk slots (%[ygs]: its base, SGPR pair; %[ybase]:
+    the lane's row offset in a slot) as global_store_dwordx4 -- a ds_write_b128 on 16 lanes costs the wave about 8
+    cycles per sample, a global store about 5 (tools/lab/lpf_io.hip) --; only the reads count on lgkmcnt, and before each
+    barrier the wave waits until only this chunk's 16 stores are in flight (vmcnt(16)), so the readers, one iteration
+    later, find the previous chunk's outputs in L2 (they load them past L1, sc1)."""
     out = []
     u = "%="
     # the 16 stream lanes: 0-15, or (spread) lanes {0-3, 16-19, 32-35, 48-51}; all_lanes: 64 streams, one per lane
@@ -265,8 +277,8 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
         f"s_cbranch_scc1 L_pre_{u}",
         "s_cmp_ge_i32 %[cc], %[nch]",
         f"s_cbranch_scc1 L_drain_{u}",
-        f"s_and_b32 %[yo], %[cc], {ymask}",
-        f"s_mul_i32 %[yo], %[yo], {slot}",
+        f"s_and_b32 %[yo], %[cc], {GRING - 1 if gstore else ymask}",
+        f"s_lshl_b32 %[yo], %[yo], {GSLOT_LOG2}" if gstore else f"s_mul_i32 %[yo], %[yo], {slot}",
         "v_add_u32 v54, %[yo], %[ybase]",
         "s_cmp_eq_u32 %[r], 0",
         f"s_cbranch_scc1 L_r0_{u}",
@@ -279,16 +291,19 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
         zb = BUFS[(r + 2) % 3]
         prev1, prev2 = pair(zb + 15), pair(zb + 14)
         for sb in range(4):
-            out.append(f"s_waitcnt lgkmcnt({4 if sb == 0 else 8})")
+            out.append(f"s_waitcnt lgkmcnt({4 if sb == 0 or gstore else 8})")
             b = BUFS[(r + sb) % 3]
             rb = BUFS[(r + sb + 2) % 3]                      # buffer of sub-block g + 2
             rslot, rsb = (r, sb + 2) if sb < 2 else ((r + 1) % 3, sb - 2)
             for q in range(16):
-                out += lpf_sample(b + q, prev1, prev2)
+                out += lpf_sample(b + q, prev1, prev2, src1)
                 prev2, prev1 = prev1, pair(b + q)
                 if q % 4 == 3:
                     t = q // 4
-                    out.append(f"ds_write_b128 v54, v[{b + 4 * t}:{b + 4 * t + 3}] offset:{(16 * sb + 4 * t) * 4}")
+                    if gstore:
+                        out.append(f"global_store_dwordx4 v54, v[{b + 4 * t}:{b + 4 * t + 3}], %[ygs] offset:{(16 * sb + 4 * t) * 4}")
+                    else:
+                        out.append(f"ds_write_b128 v54, v[{b + 4 * t}:{b + 4 * t + 3}] offset:{(16 * sb + 4 * t) * 4}")
                     out.append(f"ds_read_b128 v[{rb + 4 * t}:{rb + 4 * t + 3}], %[abase] offset:{rslot * slot + (16 * rsb + 4 * t) * 4}")
         last = BUFS[(r + 3) % 3] + 15
         out.append(f"v_pk_mov_b32 v[52:53], v[{last - 1}:{last}], v[{last - 1}:{last}] op_sel:[1,0]")
@@ -305,10 +320,12 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
     out += [
         f"s_branch L_bar_{u}",
         f"L_bar1_{u}:",
-        "s_waitcnt lgkmcnt(1)",            # this chunk's writes done; the last read of the next chunk may fly on
+        # this chunk's writes done (LDS), or all but this chunk's 16 stores (global); the last read of the next chunk
+        # may fly on
+        "s_waitcnt vmcnt(16)" if gstore else "s_waitcnt lgkmcnt(1)",
         f"s_branch L_bar_{u}",
         f"L_drain_{u}:",
-        "s_waitcnt lgkmcnt(0)",
+        "s_waitcnt vmcnt(0) lgkmcnt(0)" if gstore else "s_waitcnt lgkmcnt(0)",
         f"L_bar_{u}:",
         "s_barrier",
         "s_add_u32 %[it], %[it], 1",
@@ -321,7 +338,8 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
         f"L_next_{u}:",
         "s_cmp_lt_u32 %[it], %[nit]",
         f"s_cbranch_scc1 L_top_{u}",
-        "s_waitcnt lgkmcnt(0)",            # the last chunk's reads of a next chunk that does not exist
+        # the last chunk's reads of a next chunk that does not exist (and, gstore, the last stores)
+        "s_waitcnt vmcnt(0) lgkmcnt(0)" if gstore else "s_waitcnt lgkmcnt(0)",
         "s_mov_b64 exec, %[sv]",
         "s_nop 4",
         "v_pk_mov_b32 %[z], v[52:53], v[52:53] op_sel:[0,1]",
@@ -486,6 +504,14 @@ def main():
     print(f"#define SDRG_PIPE_SPIN_LIMIT {SPIN_LIMIT}")
     print("// lab (SDRG_LPF_COPIES=1): the same loop on all 64 lanes, lane l running stream l mod 16 (four copies)")
     emit("SDRG_LPF_LOOP_IL_COPIES_ASM", lpf_loop_interleaved(copies=True))
+    print("// lab (SDRG_LPF_SRC1=1, 2 with the copies): the interleaved loop with each add's running sum as src1")
+    emit("SDRG_LPF_LOOP_IL_SRC1_ASM", lpf_loop_interleaved(src1=True))
+    emit("SDRG_LPF_LOOP_IL_COPIES_SRC1_ASM", lpf_loop_interleaved(copies=True, src1=True))
+    print("// SDRG_LPF_GSTORE: the interleaved loop with its outputs stored to a global ring (see lpf_loop_interleaved); extra")
+    print("// operand %[ygs] (s, 64-bit: the ring's base), %[ybase] = the lane's row offset in a slot")
+    emit("SDRG_LPF_LOOP_IL_GSTORE_ASM", lpf_loop_interleaved(gstore=True))
+    print(f"#define SDRG_LPF_GSLOT_LOG2 {GSLOT_LOG2}")
+    print(f"#define SDRG_LPF_GRING {GRING}")
     print("// the same on the lanes {0-3, 16-19, 32-35, 48-51} (SDRG_SERIAL_LANES=1)")
     emit("SDRG_LPF_LOOP_IL_SPREAD_ASM", lpf_loop_interleaved(spread=True))
     print("// the low-pass chunk with its VALU on all 64 lanes and the LDS operations on the caller's lanes; extra operand")

@@ -1,0 +1,85 @@
+// Lab: the product's low-pass loop (SDRG_LPF_LOOP_IL_ASM, csrc/ssb_lpf_asm.h) alone on a CU, with 11 more waves in the
+// workgroup that only meet its per-chunk barrier (the pipeline's other roles skipped), against the same chain with the
+// same per-quad LDS traffic at fixed addresses and a plain per-chunk barrier ("bar").  s_memtime cycles per sample,
+// the minimum of 5 launches after a warm-up.  Build: hipcc --offload-arch=gfx950 -O3 -I sdr-for-android-lib_amd/csrc
+//   -o tools/lab/lpf_loop_lab tools/lab/lpf_loop_lab.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "ssb_lpf_asm.h"
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+constexpr int SLOT_F = 16 * 68;
+constexpr int NCH = 256;
+
+template <int V>
+__global__ __launch_bounds__(768) void k(unsigned long long *out, int prio, int cw) {
+    __shared__ __attribute__((aligned(16))) float lds[7 * SLOT_F];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < 7 * SLOT_F; i += 768) lds[i] = 1e-3f * (i % 97);
+    __syncthreads();
+    const int nit = NCH + 9;
+    if (wave != cw) {  // cw: the wave that runs the chain (hardware wave w runs on SIMD w mod 4)
+        for (int r = 0; r < nit; r++) asm volatile("s_waitcnt lgkmcnt(0)\n s_barrier" ::: "memory");
+        return;
+    }
+    if (prio) __builtin_amdgcn_s_setprio(3);
+    const int s = lane & 15;
+    const uint32_t abase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float *)&lds[s * 68];
+    const uint32_t ybase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float *)&lds[3 * SLOT_F + s * 68];
+    const f2v c1 = {1.9f, -0.9f}, c2 = {0.01f, -0.005f};
+    f2v z = {0.0f, 0.0f};
+    unsigned long long sv;
+    int t_it, t_cc, t_r, t_yo;
+    const int nch = NCH;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    if (lane < 16 || V == 1) {
+#define LOOP(M)                                                                                                  \
+    asm volatile(M                                                                                               \
+                 : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo) \
+                 : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch) \
+                 : SDRG_CHUNK_CLOBBERS, "v54", "memory")
+        if constexpr (V == 0) LOOP(SDRG_LPF_LOOP_IL_ASM);
+        else LOOP(SDRG_LPF_LOOP_IL_COPIES_ASM);
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) out[blockIdx.x] = t1 - t0;
+    if (lane == 0 && z.x == 12345.0f) out[1] = 1;
+}
+
+template <int V>
+void run(const char *name, unsigned long long *d, int prio, int grid, int cw) {
+    unsigned long long best = ~0ull;
+    static unsigned long long h[256];
+    for (int r = 0; r < 8; r++) {
+        k<V><<<grid, 768>>>(d, prio, cw);
+        if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(h, d, 8 * grid, hipMemcpyDeviceToHost) != hipSuccess) return;
+        double mean = 0;
+        for (int g = 0; g < grid; g++) mean += (double)h[g] / grid;
+        if (r >= 3 && mean < best) best = (unsigned long long)mean;
+    }
+    printf("%-28s prio %d grid %3d chain wave %d: %6.2f cyc/sample (%llu cycles per %d chunks, mean over workgroups)\n",
+           name, prio, grid, cw, best / (double)(NCH * 64), best, NCH);
+}
+
+__global__ void warm(float *x, int n) {  // a few ms of work so the clocks settle
+    float a = x[threadIdx.x];
+    for (int i = 0; i < n; i++) a = a * 1.0000001f + 1e-7f;
+    x[threadIdx.x] = a;
+}
+
+int main() {
+    unsigned long long *d;
+    float *w;
+    if (hipMalloc(&d, 8 * 256) != hipSuccess || hipMalloc(&w, 4096) != hipSuccess) return 2;
+    hipLaunchKernelGGL(warm, dim3(1024), dim3(256), 0, 0, w, 1 << 18);
+    if (hipDeviceSynchronize() != hipSuccess) return 3;
+    for (int grid : {1, 256}) {
+        for (int cw : {0, 1}) {
+            run<0>("product IL loop, 16 lanes", d, 1, grid, cw);
+            run<1>("IL loop, 4 copies, 64 lanes", d, 1, grid, cw);
+        }
+    }
+    return 0;
+}
