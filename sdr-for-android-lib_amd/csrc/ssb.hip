@@ -261,6 +261,10 @@ constexpr int NA = 2 + LA;  // slots of the DC -> low-pass ring
 #define SDRG_LPF_GSTORE 0
 #endif
 constexpr int GS = SDRG_LPF_GSTORE ? 1 : 0;  // extra iterations of lag for every role after the low-pass
+// lab: the low-pass loop's VALU on all 64 lanes and its LDS operations on the 16 stream lanes
+#ifndef SDRG_LPF_SPLIT
+#define SDRG_LPF_SPLIT 0
+#endif
 // lab: the low-pass adds with the running sum as src1 (a + b == b + a: the same bits)
 #ifndef SDRG_LPF_SRC1
 #define SDRG_LPF_SRC1 0
@@ -695,7 +699,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                            [nit] "s"(nit), [nch] "s"(nch)
                          : SDRG_CHUNK_CLOBBERS, "v54", "memory");
 #else
-            if (SDRG_LPF_COPIES && SDRG_LPF_SRC1)
+            if (SDRG_LPF_SPLIT)  // lab: VALU on all 64 lanes, the LDS operations on the 16 stream lanes
+                asm volatile(SDRG_LPF_LOOP_IL_SPLIT_ASM
+                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
+                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+            else if (SDRG_LPF_COPIES && SDRG_LPF_SRC1)
                 asm volatile(SDRG_LPF_LOOP_IL_COPIES_SRC1_ASM
                              : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                              : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)

@@ -245,7 +245,8 @@ GSLOT_LOG2 = 12  # SDRG_LPF_GSTORE: bytes per chunk slot of the global output ri
 GRING = 8
 
 
-def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copies=False, src1=False, gstore=False):
+def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copies=False, src1=False, gstore=False,
+                         split=False):
     """lpf_loop() with the LDS traffic spread through the VALU stream: sub-blocks are numbered g = 4c + sb across
     chunks and live in buffer g mod 3; while sub-block g runs, after each 4-sample quad t its output quad is written
     and quad t of sub-block g + 2 is read (for sb = 2, 3 that is the next chunk's sub-block 0, 1, complete in its
@@ -256,14 +257,18 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
     the lane's row offset in a slot) as global_store_dwordx4 -- a ds_write_b128 on 16 lanes costs the wave about 8
     cycles per sample, a global store about 5 (tools/lab/lpf_io.hip) --; only the reads count on lgkmcnt, and before each
     barrier the wave waits until only this chunk's 16 stores are in flight (vmcnt(16)), so the readers, one iteration
-    later, find the previous chunk's outputs in L2 (they load them past L1, sc1)."""
+    later, find the previous chunk's outputs in L2 (they load them past L1, sc1).
+    split (lab, SDRG_LPF_SPLIT): the chain's VALU on all 64 lanes (lanes 16-63 compute on whatever they hold and store
+    nothing), each quad's LDS write and read on the 16 stream lanes (EXEC switched by SALU around the pair)."""
     out = []
     u = "%="
     # the 16 stream lanes: 0-15, or (spread) lanes {0-3, 16-19, 32-35, 48-51}; all_lanes: 64 streams, one per lane
     # (ssb64.hip), with `slot` bytes per ring slot and the output ring's slot = chunk & ymask; copies (lab): all 64 lanes,
     # lane l running stream l mod 16 (four identical copies: a dependent chain issues faster on a full EXEC mask, and
     # the copies write the same values to the same LDS addresses)
-    lanes = (["s_mov_b64 exec, -1"] if all_lanes or copies else
+    if split:
+        assert not (spread or all_lanes or copies or gstore)
+    lanes = (["s_mov_b64 exec, -1"] if all_lanes or copies or split else
              ["s_mov_b32 exec_lo, 0xf000f", "s_mov_b32 exec_hi, 0xf000f"] if spread else ["s_mov_b64 exec, 0xffff"])
     out += ["s_mov_b64 %[sv], exec"] + lanes + [
         "s_nop 4",
@@ -300,11 +305,15 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
                 prev2, prev1 = prev1, pair(b + q)
                 if q % 4 == 3:
                     t = q // 4
+                    if split:
+                        out.append("s_mov_b64 exec, 0xffff")
                     if gstore:
                         out.append(f"global_store_dwordx4 v54, v[{b + 4 * t}:{b + 4 * t + 3}], %[ygs] offset:{(16 * sb + 4 * t) * 4}")
                     else:
                         out.append(f"ds_write_b128 v54, v[{b + 4 * t}:{b + 4 * t + 3}] offset:{(16 * sb + 4 * t) * 4}")
                     out.append(f"ds_read_b128 v[{rb + 4 * t}:{rb + 4 * t + 3}], %[abase] offset:{rslot * slot + (16 * rsb + 4 * t) * 4}")
+                    if split:
+                        out.append("s_mov_b64 exec, -1")
         last = BUFS[(r + 3) % 3] + 15
         out.append(f"v_pk_mov_b32 v[52:53], v[{last - 1}:{last}], v[{last - 1}:{last}] op_sel:[1,0]")
         out.append(f"s_branch L_bar1_{u}")
@@ -315,8 +324,10 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
         "s_cmp_le_i32 %[nch], 0",
         f"s_cbranch_scc1 L_drain_{u}",
     ]
+    out += ["s_mov_b64 exec, 0xffff"] if split else []
     out += [f"ds_read_b128 v[{BUFS[0] + 4 * i}:{BUFS[0] + 4 * i + 3}], %[abase] offset:{(4 * i) * 4}" for i in range(4)]
     out += [f"ds_read_b128 v[{BUFS[1] + 4 * i}:{BUFS[1] + 4 * i + 3}], %[abase] offset:{(16 + 4 * i) * 4}" for i in range(4)]
+    out += ["s_mov_b64 exec, -1"] if split else []
     out += [
         f"s_branch L_bar_{u}",
         f"L_bar1_{u}:",
@@ -510,6 +521,8 @@ def main():
     print("// SDRG_LPF_GSTORE: the interleaved loop with its outputs stored to a global ring (see lpf_loop_interleaved); extra")
     print("// operand %[ygs] (s, 64-bit: the ring's base), %[ybase] = the lane's row offset in a slot")
     emit("SDRG_LPF_LOOP_IL_GSTORE_ASM", lpf_loop_interleaved(gstore=True))
+    print("// lab (SDRG_LPF_SPLIT=1): the interleaved loop's VALU on all 64 lanes, its LDS operations on the 16 stream lanes")
+    emit("SDRG_LPF_LOOP_IL_SPLIT_ASM", lpf_loop_interleaved(split=True))
     print(f"#define SDRG_LPF_GSLOT_LOG2 {GSLOT_LOG2}")
     print(f"#define SDRG_LPF_GRING {GRING}")
     print("// the same on the lanes {0-3, 16-19, 32-35, 48-51} (SDRG_SERIAL_LANES=1)")

@@ -34,14 +34,17 @@ __global__ __launch_bounds__(768) void k(unsigned long long *out, int prio, int 
     int t_it, t_cc, t_r, t_yo;
     const int nch = NCH;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    if (lane < 16 || V == 1) {
+    if (lane < 16 || V >= 1) {
 #define LOOP(M)                                                                                                  \
     asm volatile(M                                                                                               \
                  : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo) \
                  : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch) \
                  : SDRG_CHUNK_CLOBBERS, "v54", "memory")
         if constexpr (V == 0) LOOP(SDRG_LPF_LOOP_IL_ASM);
-        else LOOP(SDRG_LPF_LOOP_IL_COPIES_ASM);
+        else if constexpr (V == 1) LOOP(SDRG_LPF_LOOP_IL_COPIES_ASM);
+        else {  // split: the block sets EXEC itself (VALU on 64 lanes, LDS on the 16 stream lanes)
+            LOOP(SDRG_LPF_LOOP_IL_SPLIT_ASM);
+        }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) out[blockIdx.x] = t1 - t0;
@@ -79,6 +82,7 @@ int main() {
         for (int cw : {0, 1}) {
             run<0>("product IL loop, 16 lanes", d, 1, grid, cw);
             run<1>("IL loop, 4 copies, 64 lanes", d, 1, grid, cw);
+            run<2>("IL loop, split EXEC", d, 1, grid, cw);
         }
     }
     return 0;
