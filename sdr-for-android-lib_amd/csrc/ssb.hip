@@ -261,6 +261,10 @@ constexpr int NA = 2 + LA;  // slots of the DC -> low-pass ring
 #define SDRG_LPF_GSTORE 0
 #endif
 constexpr int GS = SDRG_LPF_GSTORE ? 1 : 0;  // extra iterations of lag for every role after the low-pass
+// lab: the DC (bit 0) and AGC (bit 2) chunks with their VALU on all 64 lanes, their LDS operations on the 16 stream lanes
+#ifndef SDRG_SERIAL_SPLIT
+#define SDRG_SERIAL_SPLIT 0
+#endif
 // lab: the low-pass loop's VALU on all 64 lanes and its LDS operations on the 16 stream lanes
 #ifndef SDRG_LPF_SPLIT
 #define SDRG_LPF_SPLIT 0
@@ -629,7 +633,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 const f2v om2 = {one_minus, one_minus}, a02 = {a0, a0};
                 const uint32_t src = lds_addr(&L.re[c & 1][ser_s * ROW]), dst = lds_addr(&L.a[c % NA][ser_s * ROW]);
-                if (SDRG_DC_ASM == 2)
+                if (SDRG_SERIAL_SPLIT & 1) {
+                    unsigned long long sv;
+                    asm volatile(SDRG_DC_CHUNK_IL_SPLIT_ASM
+                                 : [dc] "+v"(dc), [sv] "=&s"(sv)
+                                 : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
+                                 : SDRG_CHUNK_CLOBBERS, "memory");
+                } else if (SDRG_DC_ASM == 2)
                     asm volatile(SDRG_DC_CHUNK_IL_ASM
                                  : [dc] "+v"(dc)
                                  : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
@@ -693,11 +703,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             static_assert(SDRG_LPF_INTERLEAVE && !SDRG_SERIAL_LANES && !SDRG_LPF_COPIES && !SDRG_LPF_SRC1, "gstore: the IL loop");
             static_assert(PG * CH * 4 == (1 << SDRG_LPF_GSLOT_LOG2), "global ring slot");
             float *ygs = yring + (size_t)blockIdx.x * SDRG_LPF_GRING * PG * CH;
+#if SDRG_LPF_SPLIT
+            asm volatile(SDRG_LPF_LOOP_IL_SPLIT_GSTORE_ASM
+                         : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
+                         : [abase] "v"(abase), [ybase] "v"(ybase), [ygs] "s"(ygs), [c1] "s"(c1), [c2] "s"(c2),
+                           [nit] "s"(nit), [nch] "s"(nch)
+                         : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+#else
             asm volatile(SDRG_LPF_LOOP_IL_GSTORE_ASM
                          : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                          : [abase] "v"(abase), [ybase] "v"(ybase), [ygs] "s"(ygs), [c1] "s"(c1), [c2] "s"(c2),
                            [nit] "s"(nit), [nch] "s"(nch)
                          : SDRG_CHUNK_CLOBBERS, "v54", "memory");
+#endif
 #else
             if (SDRG_LPF_SPLIT)  // lab: VALU on all 64 lanes, the LDS operations on the 16 stream lanes
                 asm volatile(SDRG_LPF_LOOP_IL_SPLIT_ASM
@@ -836,7 +854,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 f2v g = {gain, gain};
                 const uint32_t src = lds_addr(&L.d[c & 1][ser_s * ROW]), dst = lds_addr(&L.g[c & 1][ser_s * ROW]);
-                if (SDRG_AGC_ASM == 2)
+                if (SDRG_SERIAL_SPLIT & 4) {
+                    unsigned long long sv;
+                    asm volatile(SDRG_AGC_CHUNK_IL_SPLIT_ASM
+                                 : [g] "+v"(g), [sv] "=&s"(sv)
+                                 : [src] "v"(src), [dst] "v"(dst), [keep] "s"(keep), [rates] "s"(rates)
+                                 : SDRG_CHUNK_CLOBBERS, "vcc", "memory");
+                } else if (SDRG_AGC_ASM == 2)
                     asm volatile(SDRG_AGC_CHUNK_IL_ASM
                                  : [g] "+v"(g)
                                  : [src] "v"(src), [dst] "v"(dst), [keep] "s"(keep), [rates] "s"(rates)

@@ -128,7 +128,7 @@ def chunk(role, lds=True, split=False, il=False):
                 g = b + q
             if il and lds and q % 4 == 3:  # interleaved: this quad's write and sub-block sb + 2's same quad
                 t = q // 4
-                out += writes(sb, b)[t:t + 1] + (reads(sb + 2, buf[sb + 2])[t:t + 1] if sb + 2 < 4 else [])
+                out += exec_lds(writes(sb, b)[t:t + 1] + (reads(sb + 2, buf[sb + 2])[t:t + 1] if sb + 2 < 4 else []))
         if lds and not il:
             out += exec_lds(writes(sb, b) + (reads(sb + 2, buf[sb + 2]) if sb + 2 < 4 else []))
     last = buf[3] + 15
@@ -267,7 +267,7 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
     # lane l running stream l mod 16 (four identical copies: a dependent chain issues faster on a full EXEC mask, and
     # the copies write the same values to the same LDS addresses)
     if split:
-        assert not (spread or all_lanes or copies or gstore)
+        assert not (spread or all_lanes or copies)
     lanes = (["s_mov_b64 exec, -1"] if all_lanes or copies or split else
              ["s_mov_b32 exec_lo, 0xf000f", "s_mov_b32 exec_hi, 0xf000f"] if spread else ["s_mov_b64 exec, 0xffff"])
     out += ["s_mov_b64 %[sv], exec"] + lanes + [
@@ -523,6 +523,12 @@ def main():
     emit("SDRG_LPF_LOOP_IL_GSTORE_ASM", lpf_loop_interleaved(gstore=True))
     print("// lab (SDRG_LPF_SPLIT=1): the interleaved loop's VALU on all 64 lanes, its LDS operations on the 16 stream lanes")
     emit("SDRG_LPF_LOOP_IL_SPLIT_ASM", lpf_loop_interleaved(split=True))
+    print("// lab (SDRG_SERIAL_SPLIT): the DC and AGC interleaved chunks with their VALU on all 64 lanes and their LDS operations")
+    print("// on the caller's lanes (extra operand %[sv], =&s 64-bit)")
+    emit("SDRG_DC_CHUNK_IL_SPLIT_ASM", chunk("dc", il=True, split=True))
+    emit("SDRG_AGC_CHUNK_IL_SPLIT_ASM", chunk("agc", il=True, split=True))
+    print("// lab (SDRG_LPF_SPLIT=1 with SDRG_LPF_GSTORE=1): both")
+    emit("SDRG_LPF_LOOP_IL_SPLIT_GSTORE_ASM", lpf_loop_interleaved(split=True, gstore=True))
     print(f"#define SDRG_LPF_GSLOT_LOG2 {GSLOT_LOG2}")
     print(f"#define SDRG_LPF_GRING {GRING}")
     print("// the same on the lanes {0-3, 16-19, 32-35, 48-51} (SDRG_SERIAL_LANES=1)")
