@@ -344,3 +344,14 @@ def test_signal_strength_host_keeps_odd_n_carried_bin(S, O):
     spec1, _, _ = eng.process(raw[:, 1], fmt=S.CS8, stages=S.STAGE_SPECTRUM | S.STAGE_STATS, now_ms=1010)
     assert np.all(spec1[:, n - 1] == 0), spec1[:, n - 1]
     eng.close()
+
+
+def test_hbm_copy_probe(S):
+    """sdrg_measure_hbm_copy (bench.py's roofline basis): a float4 streaming copy reports a plausible read + write rate
+    (well above PCIe, below the 8 TB/s spec), and bad arguments are rejected with a status, not a crash."""
+    gbs = S.measure_hbm_copy(0, 256 << 20, 5)
+    assert 1000.0 < gbs < 8000.0, gbs
+    with pytest.raises(S.SdrgError):
+        S.measure_hbm_copy(0, 8, 1)  # fewer than 16 bytes
+    with pytest.raises(S.SdrgError):
+        S.measure_hbm_copy(1 << 20, 1 << 20, 1)  # no such device
