@@ -1443,6 +1443,15 @@ static_assert(!MW_ILP2 || MW_F == 4, "MW_ILP2 pairs frames f and f + 2");
 #endif
 static_assert(MW_SETS == 2 || MW_SETS == 4, "the chain's sets");
 constexpr int MW_RECW = SDRG_MW_RECW;
+// The pooled gaps' dB values: 0 = evaluated again after the scan (13107 glibc-exact log10s per frame
+// at 65536 / 200 kHz, the "pool logs" phase); 1 = the record waves copy every reference window's dB row of the chunk the
+// chain is reading from the LDS ring to a per-frame HBM scratch during the scan (they issue no loads, so their stores
+// hold up no wait), and the pool phase loads the bottom window's values from it (the same floats: the producers'
+// db_fold), past L1 (sc1)
+#ifndef SDRG_MW_DBPOOL
+#define SDRG_MW_DBPOOL 0
+#endif
+static_assert(!SDRG_MW_DBPOOL || MW_RECW == MW_F, "the dB copies run on the per-frame record waves");
 constexpr int MW_P0 = 1 + MW_RECW;          // first producer wave
 constexpr int MW_PROD = MW_T - 64 * MW_P0;  // producer lanes
 constexpr int MW_PR = 12;                   // bins per producer lane per chunk at most (the host sizes SC for it)
@@ -1479,8 +1488,9 @@ __host__ __device__ inline void mw_lanes(int n_ref, bool want_db, int *pgf, int 
 template <bool want_db>
 __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256))) void stats_wide_multi_kernel(
     const float *__restrict__ spectra, int n_frames, StatsGeometry g, int64_t now_ms, StatsState *__restrict__ state,
-    sdrg_frame_record *__restrict__ records, int lg) {
+    sdrg_frame_record *__restrict__ records, int lg, float *__restrict__ gdb, int wst) {
     constexpr int F = MW_F, GT = MW_T / F, REG = (MW_POOL + GT - 1) / GT, LPFR = WAVE / F, GW = GT / WAVE;
+    // SDRG_MW_DBPOOL: frame f's reference window q's dB values at gdb[((f0 + f) * n_ref + q) * wst + e]
     extern __shared__ __attribute__((aligned(16))) float ring[];
     __shared__ __attribute__((aligned(16))) int hist[F][256];
     __shared__ uint32_t sxch[F][2];
@@ -1736,7 +1746,20 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
                     }
                 }
             }
-        } else if (rec_lane && c >= 2) {
+        } else if (rwave >= 0) {
+            if (SDRG_MW_DBPOOL && want_db && c >= 1 && c <= nch) {
+                // chunk c - 1's reference dB rows of this wave's frame (stable in the ring until the producers' store of
+                // chunk c + 1) to the frame's HBM scratch, 16 bytes per lane and store
+                const int c0 = (c - 1) << lg;
+                const float *rows = ring + rf * frame_floats + ((c - 1) & 1) * slot_floats + 2 * RS;
+                float *fdb = gdb + (size_t)(f0 + rf) * (size_t)fq * (size_t)wst;
+                for (int i4 = lane; i4 < (fq << lg) / 4; i4 += WAVE) {
+                    const int q = (4 * i4) >> lg, t = (4 * i4) & (SC - 1), e = c0 + t;
+                    if (e < sh_geo_hi[q] - sh_geo_lo[q] + 1)
+                        *reinterpret_cast<float4 *>(fdb + q * wst + e) = *reinterpret_cast<const float4 *>(rows + q * 3 * RS + t);
+                }
+            }
+            if (rec_lane && c >= 2) {
             // chunk c - 2's running sums: lane k of the group visits bins k, k + G, ... in increasing order
             const int c0 = (c - 2) << lg;
             const float *rsrow = ring + rf * frame_floats + 2 * slot_floats + ((c & 1) * nwin + rq) * RS;
@@ -1747,6 +1770,7 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
                     rm = gt ? v : rm;
                     ri = gt ? c0 + t : ri;
                 }
+            }
             }
         }
         if (SDRG_MW_STAMPS) {
@@ -1760,6 +1784,8 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
         const int slot = wave == 0 ? 7 : rwave == 0 ? 8 : (is_prod_wave && pwave == 0) ? 9 : wave == MW_T / 64 - 1 ? 10 : -1;
         if (slot > 0) g_stats_stamps[blockIdx.x * STAMP_PHASES + slot] = busy;
     }
+    // the dB scratch: every store done before the barrier below, after which other waves load it
+    if (SDRG_MW_DBPOOL && want_db && rwave >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // ---- per-frame results through LDS ----
     if (foc_lane && cm > -INFINITY) atomicMax(&s_pmax[pf], ord_f(cm));
     if (foc_lane && ovf) atomicOr(&s_ovf[pf], 1);
@@ -1882,19 +1908,29 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
         const int wb = order[sf][0];
         const int lo = sh_geo_lo[wb], cnt = sh_geo_hi[wb] - lo + 1;
         const float m = s_dsum[sf][wb] / (float)cnt;
-        const float *Pw = frame_ptr(sf) + lo;
         float v[REG];
-#pragma unroll
-        for (int r = 0; r < REG; r++) {
-            const int q = stid + GT * r;
-            v[r] = q < cnt ? Pw[q] : 0.0f;
-        }
         // slots past the window hold all-ones bits: a gap is never negative (bit 31 clear), so bit 31 is never a
         // differing bit of the real values and the select's prefix never matches them (no per-slot masks to keep)
+        if constexpr (SDRG_MW_DBPOOL) {
+            const float *Dw = gdb + ((size_t)(f0 + sf) * (size_t)fq + (size_t)wb) * (size_t)wst;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(Dw), (short)0, cnt * 4, 0x00020000);
 #pragma unroll
-        for (int r = 0; r < REG; r++) {
-            v[r] = stid + GT * r < cnt ? fabsf(db_fold(v[r]) - m) : __uint_as_float(0xffffffffu);
-            if (!SDRG_MW_ILP) __builtin_amdgcn_sched_barrier(0);  // one log10 at a time
+            for (int r = 0; r < REG; r++)  // out-of-range offsets read 0 from the buffer resource
+                v[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (stid + GT * r) * 4, 0, 16));
+#pragma unroll
+            for (int r = 0; r < REG; r++) v[r] = stid + GT * r < cnt ? fabsf(v[r] - m) : __uint_as_float(0xffffffffu);
+        } else {
+            const float *Pw = frame_ptr(sf) + lo;
+#pragma unroll
+            for (int r = 0; r < REG; r++) {
+                const int q = stid + GT * r;
+                v[r] = q < cnt ? Pw[q] : 0.0f;
+            }
+#pragma unroll
+            for (int r = 0; r < REG; r++) {
+                v[r] = stid + GT * r < cnt ? fabsf(db_fold(v[r]) - m) : __uint_as_float(0xffffffffu);
+                if (!SDRG_MW_ILP) __builtin_amdgcn_sched_barrier(0);  // one log10 at a time
+            }
         }
         MW_STAMP(4);
         uint32_t band = 0xffffffffu, bor = 0u;
@@ -2127,8 +2163,16 @@ static MultiPlan multi_for(const StatsGeometry &geo) {
 static bool multi_runs(const StatsGeometry &geo) {
     return wide_for(geo) && multi_for(geo).ok && !(SDRG_STATS_STAMPS || lab_getenv("SDRG_WIDE_SINGLE"));
 }
+// SDRG_MW_DBPOOL: the multi-frame kernel's dB scratch, n_ref windows of wst floats per frame (frames rounded up to whole
+// workgroups: a workgroup's missing frames write and read their own slots)
+static int mw_db_stride(const StatsGeometry &geo) { return (geo.max_pool + 3) & ~3; }
+static bool mw_dbpool_for(const StatsGeometry &geo) {
+    return SDRG_MW_DBPOOL && multi_runs(geo) && multi_for(geo).want_db && geo.n_ref >= 1;
+}
 
 size_t stats_global_pool_floats(const StatsGeometry &geo, int n_frames) {
+    if (mw_dbpool_for(geo))
+        return (size_t)((n_frames + MW_F - 1) / MW_F * MW_F) * (size_t)geo.n_ref * (size_t)mw_db_stride(geo);
     return global_pool_for(geo) ? (size_t)n_frames * (size_t)pool_stride_for(geo) : 0;
 }
 
@@ -2149,12 +2193,14 @@ hipError_t launch_stats(const float *spectra, int n_frames, const StatsGeometry 
         hipError_t e = ensure_dynamic_lds(k, (int)lds);
         if (e != hipSuccess) return e;
         const dim3 grid((n_frames + MW_F - 1) / MW_F);
+        const bool dbp = mw_dbpool_for(geo);
+        if (dbp && !gpool) return hipErrorInvalidValue;
         if (mp.want_db)
             hipLaunchKernelGGL(stats_wide_multi_kernel<true>, grid, dim3(MW_T), lds, stream, spectra, n_frames, geo, now_ms,
-                               state, records, mp.lg);
+                               state, records, mp.lg, dbp ? gpool : nullptr, mw_db_stride(geo));
         else
             hipLaunchKernelGGL(stats_wide_multi_kernel<false>, grid, dim3(MW_T), lds, stream, spectra, n_frames, geo, now_ms,
-                               state, records, mp.lg);
+                               state, records, mp.lg, nullptr, 0);
         if (SDRG_MW_STAMPS) {  // lab: mean cycles per phase over the workgroups of this call
             std::vector<unsigned long long> h((size_t)STAMP_PHASES * 8192);
             if (hipStreamSynchronize(stream) == hipSuccess &&
