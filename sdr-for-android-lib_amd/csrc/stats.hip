@@ -1448,8 +1448,10 @@ constexpr int MW_RECW = SDRG_MW_RECW;
 // chain is reading from the LDS ring to a per-frame HBM scratch during the scan (they issue no loads, so their stores
 // hold up no wait), and the pool phase loads the bottom window's values from it (the same floats: the producers'
 // db_fold), past L1 (sc1)
+// Measured (r6m, alternating, one box): the kernel alone at 1024 x 65536 / 200 kHz 183.8 / 184.6 -> 173.3 / 176.0 us,
+// the configs[4] 200 kHz line 137.3 / 137.4 -> 141.1 / 140.8 G; the statistics GPU tests bit-exact (105 passed).
 #ifndef SDRG_MW_DBPOOL
-#define SDRG_MW_DBPOOL 0
+#define SDRG_MW_DBPOOL 1
 #endif
 static_assert(!SDRG_MW_DBPOOL || MW_RECW == MW_F, "the dB copies run on the per-frame record waves");
 constexpr int MW_P0 = 1 + MW_RECW;          // first producer wave
