@@ -16,6 +16,8 @@ spec = torch.empty((bench.B, bench.N), dtype=torch.float32, device=dev)
 rec = torch.zeros((bench.B, sdrg.RECORD_DTYPE.itemsize), dtype=torch.uint8, device=dev)
 pcm = torch.empty((bench.B, eng.pcm_len), dtype=torch.int16, device=dev)
 eng.set_pipelining(int(os.environ.get("LAB_PIPE_MODE", "2")))
+if os.environ.get("LAB_NCO") == "1":  # the configs[2] variant: NCO at +250 kHz, 127-tap FIR (bench.py's configs2_nco127)
+    eng.set_ssb_variant(bench.NCO_HZ, 127)
 now = [1000]
 def run(k, prof):
     eng.set_profiling(prof)
