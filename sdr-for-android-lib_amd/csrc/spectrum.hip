@@ -314,10 +314,6 @@ namespace k16 {
 #define SDRG_K16_ABLATE 0
 #endif
 constexpr int ABL = SDRG_K16_ABLATE;
-#ifndef SDRG_K16_ALONE_X1  // lab: the alone kernel with the cross-wave first exchange (isolates the occupancy)
-#define SDRG_K16_ALONE_X1 0
-#endif
-constexpr bool K16_ALONE_X1 = SDRG_K16_ALONE_X1;
 // the |X|^2 stores' cache policy (buffer-store aux bits, gfx950: 1 sc0, 2 nt, 16 sc1)
 #ifndef SDRG_K16_STORE_AUX
 #define SDRG_K16_STORE_AUX 2
@@ -342,12 +338,6 @@ typedef float f2s __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float4 pair4(f2 a, f2 b) { return make_float4(a.x, a.y, b.x, b.y); }
 
 // pass-0 outputs (radix 32, NS = 1: thread t writes slots 32 t + r) -> pass-1 inputs (thread t reads t + 512 r)
-#ifndef SDRG_K16_FUSE_PROBE  // lab: extra VALU per thread and frame standing in for a fused statistics tail
-#define SDRG_K16_FUSE_PROBE 0
-#endif
-#ifndef SDRG_K16_XCH_TRIM  // 1: the exchange addresses without the LDS base add per access (see exch1 / exch2); 0: as round 5
-#define SDRG_K16_XCH_TRIM 1
-#endif
 __device__ __forceinline__ void exch1(f2 *lds, f2 (&v)[E]) {
     const int t = threadIdx.x;
     char *lb = reinterpret_cast<char *>(lds);
@@ -356,29 +346,19 @@ __device__ __forceinline__ void exch1(f2 *lds, f2 (&v)[E]) {
     for (int h = 0; h < 2; ++h) {
         if ((t >= T / 2) == (h == 1)) {
             const int tp = t - h * (T / 2);
-            if constexpr (SDRG_K16_XCH_TRIM) {
-                // the row's LDS byte address with the buffer's base in it: the base is 256-byte aligned (the dynamic
-                // allocation starts the kernel's LDS), so the XOR of the unit index touches the row offset only, and
-                // each write costs one v_xor (the compiler's form also added the base, a relocation literal, per write)
-                uint32_t row = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)lb + 256 * tp + ((tp & 15) << 4);
-                asm volatile("" : "+v"(row));
+            // the row's LDS byte address with the buffer's base in it: the base is 256-byte aligned (the dynamic
+            // allocation starts the kernel's LDS), so the XOR of the unit index touches the row offset only, and
+            // each write costs one v_xor (the compiler's form also added the base, a relocation literal, per write)
+            uint32_t row = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)lb + 256 * tp + ((tp & 15) << 4);
+            asm volatile("" : "+v"(row));
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    typedef float v4f __attribute__((ext_vector_type(4)));
-                    const v4f x = {v[2 * q].x, v[2 * q].y, v[2 * q + 1].x, v[2 * q + 1].y};
-                    asm volatile("ds_write_b128 %0, %1" ::"v"(row ^ (q << 4)), "v"(x) : "memory");
-                }
-            } else {
-                int row = 256 * tp + ((tp & 15) << 4);  // byte offset of the row, ORed with its XOR
-                asm volatile("" : "+v"(row));  // per frame: hoisted out of the frame loop, the 16 addresses hold 16 VGPRs
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    *reinterpret_cast<float4 *>(lb + (row ^ (q << 4))) = pair4(v[2 * q], v[2 * q + 1]);
-                    __builtin_amdgcn_sched_barrier(0);  // one pair's 4-register tuple at a time
-                }
+            for (int q = 0; q < 16; ++q) {
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                const v4f x = {v[2 * q].x, v[2 * q].y, v[2 * q + 1].x, v[2 * q + 1].y};
+                asm volatile("ds_write_b128 %0, %1" ::"v"(row ^ (q << 4)), "v"(x) : "memory");
             }
         }
-        if constexpr (SDRG_K16_XCH_TRIM) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm writes
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the asm writes
         __syncthreads();
         const f2 *rb = lds + (t ^ (2 * ((t >> 5) & 15)));
 #pragma unroll
@@ -390,24 +370,23 @@ __device__ __forceinline__ void exch1(f2 *lds, f2 (&v)[E]) {
 }
 
 // pass-1 outputs (radix 32, NS = 32: slots (t / 32) 1024 + t mod 32 + 32 r) -> pass-2 inputs (radix 16, butterflies
-// 2t and 2t + 1: slots 2t + b + 1024 r, read as float4 pairs).  SDRG_K16_XCH_TRIM: a linear layout (no XOR): a
+// 2t and 2t + 1: slots 2t + b + 1024 r, read as float4 pairs), in a linear layout (no XOR): a
 // half-wave's writes of one r are 32 consecutive slots (256 B, every bank once) and a wave's float4 reads 1 KiB of
 // consecutive slots, so neither side conflicts, and every access is the thread's base plus a constant offset (no
 // address VALU; the XOR layout, shared with exch1's, cost one v_xor per write)
 __device__ __forceinline__ void exch2(f2 *lds, f2 (&v)[E]) {
     const int t = threadIdx.x;
     f2 nxt[E];
-    constexpr int X = SDRG_K16_XCH_TRIM ? 0 : 1;  // 1: the XOR layout
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         if (((t >> 5) >= 8) == (h == 1)) {
             int row = ((t >> 5) - 8 * h) * 1024 + (t & 31);
             asm volatile("" : "+v"(row));  // as in exch1
 #pragma unroll
-            for (int r = 0; r < 32; ++r) lds[(row ^ (X * 2 * (r & 15))) + 32 * r] = v[r];
+            for (int r = 0; r < 32; ++r) lds[row + 32 * r] = v[r];
         }
         __syncthreads();
-        const float4 *rb = reinterpret_cast<const float4 *>(lds + ((2 * t) ^ (X * 2 * ((t >> 4) & 15))));
+        const float4 *rb = reinterpret_cast<const float4 *>(lds + 2 * t);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             const float4 p = rb[512 * r];  // slots 2t, 2t + 1 of row 1024 r
@@ -418,67 +397,6 @@ __device__ __forceinline__ void exch2(f2 *lds, f2 (&v)[E]) {
     }
 #pragma unroll
     for (int i = 0; i < E; ++i) v[i] = nxt[i];
-}
-
-// ---- the spectrum-alone layout (spectrum16k_alone_kernel): pass 0 on half-waves ----
-// Pass 0 thread 32 h + a (half-wave h, lane a) holds x[16 a + h + 512 r]: the inputs of the current kernel's thread
-// 16 a + h, so the same radix-32 codelet gives the same values.  Pass 1 needs, in lane c of half-wave h, the pass-0
-// outputs c of the 32 lanes a of the SAME half-wave: the first exchange becomes a 32 x 32 transpose inside a wave,
-// through the wave's own 16 KiB of the (full-frame) exchange buffer, with no workgroup barrier.  The block of
-// half-wave h is the buffer's row h of the second exchange, which half-wave h writes itself, so the two uses of
-// the buffer never overlap between waves.  Same exch1 swizzle: slot 32 a + c at 32 a + (c ^ 2 (a mod 16)).
-__device__ __forceinline__ void transpose_local(f2 *lds, f2 (&v)[E]) {
-    const int t = threadIdx.x, l = t & 31;
-    f2 *blk = lds + 1024 * (t >> 5);
-    char *lb = reinterpret_cast<char *>(blk);
-    int row = 256 * l + ((l & 15) << 4);
-    asm volatile("" : "+v"(row));
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        *reinterpret_cast<float4 *>(lb + (row ^ (q << 4))) = pair4(v[2 * q], v[2 * q + 1]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // one wave writes and reads its block: LDS executes a wave's instructions in order, so no barrier; the
-    // compiler keeps the reads behind the writes (they alias the same block)
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = blk[32 * r + (l ^ (2 * (r & 15)))];
-}
-
-// lab (SDRG_K16_ALONE_X1=1): the first exchange over the whole frame, cross-wave as in exch1 (two barriers)
-__device__ __forceinline__ void exch1_full(f2 *lds, f2 (&v)[E]) {
-    const int t = threadIdx.x;
-    char *lb = reinterpret_cast<char *>(lds);
-    int row = 256 * t + ((t & 15) << 4);
-    asm volatile("" : "+v"(row));
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        *reinterpret_cast<float4 *>(lb + (row ^ (q << 4))) = pair4(v[2 * q], v[2 * q + 1]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();
-    const f2 *rb = lds + (t ^ (2 * ((t >> 5) & 15)));
-#pragma unroll
-    for (int r = 0; r < 32; ++r) v[r] = rb[512 * r];
-    __syncthreads();
-}
-
-// the second exchange over the whole frame (exch2 with both halves at once): two barriers per frame
-__device__ __forceinline__ void exch2_full(f2 *lds, f2 (&v)[E]) {
-    const int t = threadIdx.x;
-    int row = (t >> 5) * 1024 + (t & 31);
-    asm volatile("" : "+v"(row));
-#pragma unroll
-    for (int r = 0; r < 32; ++r) lds[(row ^ (2 * (r & 15))) + 32 * r] = v[r];
-    __syncthreads();
-    const float4 *rb = reinterpret_cast<const float4 *>(lds + ((2 * t) ^ (2 * ((t >> 4) & 15))));
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const float4 p = rb[512 * r];  // slots 2t, 2t + 1 of row 1024 r
-        v[r] = f2{p.x, p.y};
-        v[16 + r] = f2{p.z, p.w};
-    }
-    __syncthreads();
 }
 
 // raw samples x[t + 512 r] of frame f into registers (zero-extended 16/32-bit words); live = false gives a
@@ -492,17 +410,16 @@ __device__ __forceinline__ void issue_raw(const void *iq, int f, int t, uint32_t
     for (int r = 0; r < E; ++r) raw[r] = load_raw_word<FMT>(rs, t * BPS, r * (N / 32) * BPS);
 }
 
-// ALONE: the spectrum-alone layout (full-frame exchange buffer, pass 0 on half-waves, see transpose_local)
-template <int FMT, bool ALONE>
+template <int FMT>
 __device__ __forceinline__ void spectrum16k_body(const void *__restrict__ iq, float *__restrict__ spectra,
                                                  const float *__restrict__ tabs, int n_frames) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int XB = (ALONE ? N : XCH_F2) * 8;  // exchange buffer bytes
+    constexpr int XB = XCH_F2 * 8;  // exchange buffer bytes
     f2 *xch = reinterpret_cast<f2 *>(smem);
     f2 *p1 = reinterpret_cast<f2 *>(smem + XB);
     float4 *a2 = reinterpret_cast<float4 *>(smem + XB + P1_F2 * 8);
     const int t = threadIdx.x;
-    const int src = ALONE && !K16_ALONE_X1 ? 16 * (t & 31) + (t >> 5) : t;  // pass 0 reads x[src + 512 r]
+    const int src = t;  // pass 0 reads x[src + 512 r]
     for (int i = t; i < P1_F2; i += T) p1[i] = reinterpret_cast<const f2 *>(tabs)[i];
     for (int i = t; i < A2_F4; i += T) a2[i] = reinterpret_cast<const float4 *>(tabs + 2 * P1_F2)[i];
     __syncthreads();
@@ -533,9 +450,7 @@ __device__ __forceinline__ void spectrum16k_body(const void *__restrict__ iq, fl
         const int next = frame + gridDim.x;
         if constexpr (!(ABL & 8)) dft<32>(v);
         if constexpr (!(ABL & 4)) {
-            if constexpr (ALONE && K16_ALONE_X1) exch1_full(xch, v);
-            else if constexpr (ALONE) transpose_local(xch, v);
-            else exch1(xch, v);
+            exch1(xch, v);
         }
         // ---- pass 1: radix 32, NS = 32 ----
         if constexpr (!(ABL & 1)) {
@@ -544,8 +459,7 @@ __device__ __forceinline__ void spectrum16k_body(const void *__restrict__ iq, fl
         }
         if constexpr (!(ABL & 8)) dft<32>(v);
         if constexpr (!(ABL & 4)) {
-            if constexpr (ALONE) exch2_full(xch, v);
-            else exch2(xch, v);
+            exch2(xch, v);
         }
         // ---- pass 2: radix 16, NS = 1024, butterflies j = 2t + b held as v[16 b + r] ----
         if constexpr (!(ABL & 2)) {
@@ -599,21 +513,6 @@ __device__ __forceinline__ void spectrum16k_body(const void *__restrict__ iq, fl
             asm("v_fma_f32 %0, %1, %1, %2" : "=v"(p1) : "v"(x1[r].x), "v"(q1));
             pw[r] = f2s{p0, p1};
         }
-#if SDRG_K16_FUSE_PROBE
-        // lab: the VALU a fused narrow-statistics tail would add, as independent packed FMAs on the
-        // frame's powers (no dependency chain, no LDS, no barrier: the best case for the fusion), SDRG_K16_FUSE_PROBE
-        // per thread and frame; kept alive without a store.  The statistics issue ~3016 VALU per frame (one wave):
-        // spread over the workgroup's 8 waves, 377 per thread.
-        {
-            f2s acc[8] = {pw[0], pw[1], pw[2], pw[3], pw[4], pw[5], pw[6], pw[7]};
-#pragma unroll
-            for (int i = 0; i < SDRG_K16_FUSE_PROBE / 8; ++i)
-#pragma unroll
-                for (int a = 0; a < 8; ++a) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(acc[a]) : "v"(pw[(8 * i + a) & 15]), "v"(pw[(8 * i + a + 5) & 15]));
-#pragma unroll
-            for (int a = 0; a < 8; ++a) asm volatile("; keep %0" ::"v"(acc[a]));
-        }
-#endif
         if constexpr (STAGE) issue_raw<FMT>(iq, next < n_frames ? next : frame, src, raw, next < n_frames);
         float *o = spectra + (size_t)frame * N + 2 * t;
         if constexpr (ABL & 16) {  // keep the values live without the stores
@@ -637,17 +536,7 @@ __device__ __forceinline__ void spectrum16k_body(const void *__restrict__ iq, fl
 template <int FMT>
 __global__ __launch_bounds__(T, 4) void spectrum16k_kernel(const void *__restrict__ iq, float *__restrict__ spectra,
                                                            const float *__restrict__ tabs, int n_frames) {
-    spectrum16k_body<FMT, false>(iq, spectra, tabs, n_frames);
-}
-
-// The spectrum-alone kernel (no SSB pipeline beside it): one workgroup per CU with the full-frame exchange buffer,
-// two barriers per frame instead of eight.  Same operations on the same values as spectrum16k_kernel: same bits.
-constexpr int LDS_ALONE_BYTES = N * 8 + P1_F2 * 8 + A2_F4 * 16;
-static_assert(LDS_ALONE_BYTES <= 160 * 1024, "one workgroup per CU");
-template <int FMT>
-__global__ __launch_bounds__(T, 2) void spectrum16k_alone_kernel(const void *__restrict__ iq, float *__restrict__ spectra,
-                                                                 const float *__restrict__ tabs, int n_frames) {
-    spectrum16k_body<FMT, true>(iq, spectra, tabs, n_frames);
+    spectrum16k_body<FMT>(iq, spectra, tabs, n_frames);
 }
 
 // the two LDS tables, laid out as the kernel reads them (exp evaluated in double, rounded once)
@@ -677,14 +566,12 @@ int device_cus() {
     return cus;
 }
 
-// wg_per_cu: persistent workgroups per CU (2 alone; 1 when the SSB pipeline shares the CUs, see launch_spectrum);
-// 0 = the spectrum-alone kernel (one workgroup per CU, full-frame exchange)
+// wg_per_cu: persistent workgroups per CU (2 alone; 1 when the SSB pipeline shares the CUs, see launch_spectrum)
 template <int FMT>
 hipError_t launch(const void *iq, int n_frames, const float *tabs, float *spectra, hipStream_t s, int wg_per_cu = 2,
                   int n_cus = 0) {
-    const bool alone = wg_per_cu == 0;
-    auto k = alone ? spectrum16k_alone_kernel<FMT> : spectrum16k_kernel<FMT>;
-    const int lds = alone ? LDS_ALONE_BYTES : LDS_BYTES;
+    auto k = spectrum16k_kernel<FMT>;
+    const int lds = LDS_BYTES;
     hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void *>(k), lds);
     if (e != hipSuccess) return e;
     static const int max_grid = [] {  // lab override (SDRG_SPECTRUM_GRID): persistent workgroups
@@ -871,22 +758,6 @@ __device__ __forceinline__ f2 convert_scaled(uint32_t v) {  // load_sample's val
     }
 }
 
-// Lab: the price of an in-launch hand-off of the intermediate Y, measured inside the persistent
-// four-step kernels without any waiting.  SDRG_FS_PUBLISH=1: every column tile publishes its Y slice the way a
-// producer must for another workgroup (plain stores, every wave's vmcnt(0), a barrier, lane 0's agent-scope release
-// fence, vmcnt(0), a relaxed agent flag store); =2: the write-through form (Y stored sc1, vmcnt(0), barrier, flag; no
-// fence).  SDRG_FS_ACQUIRE=1: every row tile begins as a consumer must (lane 0 reads the flag relaxed, agent-scope
-// acquire fence, vmcnt(0), barrier).  Results are unchanged (the flags are written and read, never waited on).
-#ifndef SDRG_FS_PUBLISH
-#define SDRG_FS_PUBLISH 0
-#endif
-#ifndef SDRG_FS_ACQUIRE
-#define SDRG_FS_ACQUIRE 0
-#endif
-#if SDRG_FS_PUBLISH || SDRG_FS_ACQUIRE
-__device__ unsigned g_fs_flags[1 << 16];
-#endif
-
 template <int LOG2N1, int LOG2N2, int FMT>
 __global__ __launch_bounds__(TILE_A) void four_step_a_p(const void *__restrict__ iq, f2 *__restrict__ Y,
                                                          const f2 *__restrict__ tw, int n_frames, int hi) {
@@ -945,23 +816,10 @@ __global__ __launch_bounds__(TILE_A) void four_step_a_p(const void *__restrict__
         auto store = [&](int cc, int k1, f2 v) {
             const int n2 = c0 + cc;
             const f2 w = cmul_v(v, tw_lds<1>(t_hi, t_lo, (n2 * k1) & (N - 1)));
-            if constexpr (SDRG_FS_PUBLISH == 2)
-                __hip_atomic_store(reinterpret_cast<unsigned long long *>(y + k1 * N2 + n2),
-                                   __builtin_bit_cast(unsigned long long, w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-                y[k1 * N2 + n2] = w;
+            y[k1 * N2 + n2] = w;
         };
         // pass 2 reads the tile, then a barrier (inside), so the next tile's pass-1 writes are safe
         tile_pass<N, N1, TP::RB, TP::RA, false, true, TILE_A>(lds, t_hi, t_lo, noload, store);
-#if SDRG_FS_PUBLISH
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            if constexpr (SDRG_FS_PUBLISH == 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&g_fs_flags[tile & 0xffff], (unsigned)tile + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#endif
     }
 }
 
@@ -987,15 +845,6 @@ __global__ __launch_bounds__(TILE_B) void four_step_b_p(const f2 *__restrict__ Y
     if (tile < total) issue(tile);
     for (; tile < total; tile += gridDim.x) {
         const int frame = tile / TPF, r0 = (tile % TPF) * C;
-#if SDRG_FS_ACQUIRE
-        if (threadIdx.x == 0) {
-            const unsigned seen = __hip_atomic_load(&g_fs_flags[tile & 0xffff], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (seen == 0xffffffffu) stage[0].x = 0.0f;  // keep the load
-        }
-        __syncthreads();
-#endif
 #pragma unroll
         for (int i = 0; i < S; ++i) {
             const int e = threadIdx.x + i * TILE_B;
@@ -1018,70 +867,10 @@ __global__ __launch_bounds__(TILE_B) void four_step_b_p(const f2 *__restrict__ Y
 // hi: the waves run at issue priority 1, above statistics that run beside them on a stream of their own (configs[4]
 // at 5 kHz: 0.3096-0.3113 vs 0.3127-0.3130 ms per step, 200 kHz unchanged, tools/gpu_r4y.sh); not beside the SSB
 // pipeline, whose helper roles at priority 0 would yield to them
-// Lab (SDRG_FS_2STREAM=1): waves of half the frames with two intermediate buffers, the column kernel of wave w + 1
-// on the caller's stream beside the row kernel of wave w on a second stream (events order each buffer's reuse), so the
-// launches' tails and boundaries overlap.  The engine sizes the scratch by spectrum_scratch_floats (the same bytes).
-#ifndef SDRG_FS_2STREAM
-#define SDRG_FS_2STREAM 0
-#endif
-template <int LOG2N1, int LOG2N2, int FMT>
-hipError_t launch_four_step_2s(const void *iq, int n_frames, const float *twf, float *spectra, float *scratch, int wave,
-                               hipStream_t s, bool persistent, int hi) {
-    constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
-    static hipStream_t sb = nullptr;
-    static hipEvent_t ev0, ev_end, ev_a[2], ev_b[2];
-    if (!sb) {
-        hipError_t e = hipStreamCreateWithFlags(&sb, hipStreamNonBlocking);
-        const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev0, fl);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev_end, fl);
-        for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&ev_a[i], fl);
-        for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&ev_b[i], fl);
-        if (e != hipSuccess) return e;
-    }
-    const f2 *tw = reinterpret_cast<const f2 *>(twf);
-    const int half = wave / 2 > 0 ? wave / 2 : 1;
-    const int cus = k16::device_cus();
-    hipError_t e = hipEventRecord(ev0, s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(sb, ev0, 0);
-    int w = 0;
-    for (int f0 = 0; f0 < n_frames && e == hipSuccess; f0 += half, ++w) {
-        const int nf = (n_frames - f0) < half ? (n_frames - f0) : half;
-        f2 *Y = reinterpret_cast<f2 *>(scratch) + (size_t)(w & 1) * half * N;
-        const char *src = reinterpret_cast<const char *>(iq) + (size_t)f0 * N * bytes_per_sample<FMT>();
-        if (w >= 2) e = hipStreamWaitEvent(s, ev_b[w & 1], 0);  // the row kernel of wave w - 2 read this buffer
-        if (e != hipSuccess) break;
-        if (persistent) {
-            const int ta = nf * (N2 / TilePlan<N1, TILE_A>::C), ga = ta < 2 * cus ? ta : 2 * cus;
-            hipLaunchKernelGGL((four_step_a_p<LOG2N1, LOG2N2, FMT>), dim3(ga), dim3(TILE_A), 0, s, src, Y, tw, nf, hi);
-        } else {
-            hipLaunchKernelGGL((four_step_a<LOG2N1, LOG2N2, FMT>), dim3(N2 / TilePlan<N1, TILE_A>::C, nf), dim3(TILE_A), 0,
-                               s, src, Y, tw, hi);
-        }
-        e = hipEventRecord(ev_a[w & 1], s);
-        if (e == hipSuccess) e = hipStreamWaitEvent(sb, ev_a[w & 1], 0);
-        if (e != hipSuccess) break;
-        if (persistent) {
-            const int tb = nf * (N1 / TilePlan<N2, TILE_B>::C), gb = tb < 4 * cus ? tb : 4 * cus;
-            hipLaunchKernelGGL((four_step_b_p<LOG2N1, LOG2N2>), dim3(gb), dim3(TILE_B), 0, sb, Y, spectra + (size_t)f0 * N,
-                               tw, nf, hi);
-        } else {
-            hipLaunchKernelGGL((four_step_b<LOG2N1, LOG2N2>), dim3(N1 / TilePlan<N2, TILE_B>::C, nf), dim3(TILE_B), 0, sb, Y,
-                               spectra + (size_t)f0 * N, tw, hi);
-        }
-        e = hipEventRecord(ev_b[w & 1], sb);
-    }
-    if (e == hipSuccess) e = hipEventRecord(ev_end, sb);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_end, 0);  // later work on the caller's stream follows every wave
-    return e != hipSuccess ? e : hipGetLastError();
-}
-
 template <int LOG2N1, int LOG2N2, int FMT>
 hipError_t launch_four_step(const void *iq, int n_frames, const float *twf, float *spectra, float *scratch,
                             int wave, hipStream_t s, bool persistent, bool hi_prio) {
     const int hi = hi_prio ? 1 : 0;
-    if (SDRG_FS_2STREAM) return launch_four_step_2s<LOG2N1, LOG2N2, FMT>(iq, n_frames, twf, spectra, scratch, wave, s,
-                                                                         persistent, hi);
     constexpr int N1 = 1 << LOG2N1, N2 = 1 << LOG2N2, N = N1 * N2;
     const f2 *tw = reinterpret_cast<const f2 *>(twf);
     f2 *Y = reinterpret_cast<f2 *>(scratch);
@@ -1197,18 +986,6 @@ size_t spectrum_scratch_floats(int n, int n_frames) {
     return (size_t)wave * n * 2;
 }
 
-// N = 16384 with no SSB pipeline beside it: the two-workgroup kernel (2).  The spectrum-alone kernel (0: one
-// workgroup per CU, two barriers per frame, the same bits) measured 187 us per 4096 CS8 frames against 111 us (DESIGN
-// §3.1, round 5) and is a lab option only: SDRG_K16_ALONE=1 (lab builds).
-static int k16_alone_mode(int fmt) {
-    static const int forced = [] {
-        const char *v = lab_getenv("SDRG_K16_ALONE");
-        return v ? atoi(v) : -1;
-    }();
-    (void)fmt;
-    return forced > 0 ? 0 : 2;
-}
-
 hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const float *twiddles, float *spectra,
                            float *scratch, hipStream_t stream, bool beside_ssb, int n_cus, bool beside_wide_stats) {
     if (n_frames <= 0) return hipSuccess;
@@ -1221,7 +998,7 @@ hipError_t launch_spectrum(const void *iq, int fmt, int n, int n_frames, const f
         return launch_four_step_fmt<8, 8>(iq, fmt, n_frames, twiddles, spectra, scratch, spectrum_wave_frames(n), stream,
                                           !beside_wide_stats, !beside_ssb);
     case 16384: return k16::launch_fmt(iq, fmt, n_frames, twiddles + spectrum_k16_tables_offset(), spectra, stream,
-                                      beside_ssb ? 1 : k16_alone_mode(fmt), n_cus);
+                                      beside_ssb ? 1 : 2, n_cus);
     case 64: return launch_n<6>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 128: return launch_n<7>(iq, fmt, n_frames, twiddles, spectra, stream);
     case 256: return launch_n<8>(iq, fmt, n_frames, twiddles, spectra, stream);

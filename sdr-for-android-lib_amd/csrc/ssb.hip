@@ -184,8 +184,7 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 //   SIMD2: AGC,  desired (1/4),     desired (1/4)
 //   SIMD3: load, FIR (slot group 0), FIR (slot group 1)
 // ================================================================================================
-// the low-pass wave's full chunks as one hand-scheduled asm block (1; 2: its VALU on all 64 lanes, the LDS
-// operations on the 16 stream lanes) or through row_pipeline (0)
+// the low-pass wave's full chunks as one hand-scheduled asm block (1) or through row_pipeline (0)
 #ifndef SDRG_LPF_ASM
 #define SDRG_LPF_ASM 1
 #endif
@@ -199,18 +198,6 @@ __global__ __launch_bounds__(WAVE) void ssb_eq_kernel(const float *__restrict__ 
 #define SDRG_AGC_ASM 2
 #endif
 constexpr int PG = 16;          // streams per workgroup
-// serial roles (bit 0 DC, 1 LPF, 2 AGC) that run on all 64 lanes (16 copies of the 16 streams) instead of the
-// first 16: a dependent VALU chain issues faster with the full EXEC mask, while the LDS reads of 16 copies cost
-// more LDS cycles (tools/microbench/valu5.hip, valu6.hip; tools/build_variant.sh for the trade per role)
-#ifndef SDRG_SERIAL_FULL_EXEC
-#define SDRG_SERIAL_FULL_EXEC 0x0
-#endif
-// lanes of the three hand-scheduled serial roles (DC, low-pass, AGC): 0 = lanes 0-15 (stream = lane), 1 = lanes
-// {0-3, 16-19, 32-35, 48-51} (EXEC 0x000f000f000f000f, stream = 4 x (lane / 16) + lane % 4): a dependent add chain
-// issues at 25.4 instead of 30.6 cycles per sample with that mask (tools/lab/lpf_exec.hip, profiles/r3b_pg32_stamps.md)
-#ifndef SDRG_SERIAL_LANES
-#define SDRG_SERIAL_LANES 0
-#endif
 constexpr int CH = 64;          // samples per chunk
 constexpr int ROW = CH + 4;     // padded stream row (floats): conflict-free ds_read_b128 by stream lanes
 constexpr int BUFF = PG * ROW;  // floats per [stream][sample] chunk buffer
@@ -249,30 +236,6 @@ constexpr int LA = SDRG_LPF_LOOKAHEAD ? 1 : 0;
 #define SDRG_LPF_INTERLEAVE 1
 #endif
 constexpr int NA = 2 + LA;  // slots of the DC -> low-pass ring
-// lab: the low-pass loop on all 64 lanes as four copies of the 16 streams (full EXEC for the dependent chain)
-#ifndef SDRG_LPF_COPIES
-#define SDRG_LPF_COPIES 0
-#endif
-// The low-pass outputs through a global ring instead of LDS (tools/lab/lpf_io.hip: a ds_write_b128 on the wave's 16
-// lanes costs it ~8 cycles per sample, a global_store_dwordx4 ~5): the wave stores each chunk to slot c mod GRING of its
-// workgroup's ring in the SSB scratch, waits at each barrier until only its current chunk's stores are in flight, and
-// the readers (desired-level waves, clamp) load a chunk one iteration later than from LDS, past L1 (sc1)
-#ifndef SDRG_LPF_GSTORE
-#define SDRG_LPF_GSTORE 0
-#endif
-constexpr int GS = SDRG_LPF_GSTORE ? 1 : 0;  // extra iterations of lag for every role after the low-pass
-// lab: the DC (bit 0) and AGC (bit 2) chunks with their VALU on all 64 lanes, their LDS operations on the 16 stream lanes
-#ifndef SDRG_SERIAL_SPLIT
-#define SDRG_SERIAL_SPLIT 0
-#endif
-// lab: the low-pass loop's VALU on all 64 lanes and its LDS operations on the 16 stream lanes
-#ifndef SDRG_LPF_SPLIT
-#define SDRG_LPF_SPLIT 0
-#endif
-// lab: the low-pass adds with the running sum as src1 (a + b == b + a: the same bits)
-#ifndef SDRG_LPF_SRC1
-#define SDRG_LPF_SRC1 0
-#endif
 #ifndef SDRG_PIPE_RAWB  // bytes of raw IQ per stream per prefetch batch
 #define SDRG_PIPE_RAWB (SDRG_LPF_LOOKAHEAD ? 256 : 512)
 #endif
@@ -300,24 +263,11 @@ constexpr int batch_chunks() {  // chunks per RAWB-per-stream prefetch batch (DM
 #define SDRG_PIPE_MINW 6
 #endif
 constexpr int NRAW = SDRG_PIPE_NRAW;  // raw-IQ batches in LDS: one being unpacked, NRAW - 1 in flight
-// Synchronisation of the roles: 0 = one LDS-only workgroup barrier per chunk iteration, every role
-// a fixed number of chunks behind the loader; 1 = no barrier in the loop: each role publishes how many chunks it has
-// finished in an LDS counter (PipeLds::prog, layout SDRG_PROG_* from tools/gen/gen_lpf_asm.py) and waits only on the
-// counters of its producers (the chunk it reads is complete) and of its consumers (the ring slot it writes is free).
-// LDS executes one wave's operations in issue order, so a count that another wave can see was stored after every
-// LDS read and write of the chunks it counts; the poll is a plain LDS read, retried after s_sleep 1, bounded.
-#ifndef SDRG_PIPE_FLAGS
-#define SDRG_PIPE_FLAGS 0
-#endif
-static_assert(!SDRG_PIPE_FLAGS || SDRG_LPF_LOOKAHEAD, "the counter conditions assume the low-pass lookahead");
-static_assert(!SDRG_LPF_COPIES || (SDRG_LPF_INTERLEAVE && !SDRG_SERIAL_LANES && !SDRG_PIPE_FLAGS), "copies: the IL loop");
-
 struct PipeLds {
-    int prog[16];             // chunk counters (SDRG_PIPE_FLAGS): SDRG_PROG_* index, SDRG_PROG_ABORT the give-up word
     uint4 raw[NRAW][RAW_U4];  // raw IQ bytes of the prefetch batches (LDS-DMA), [piece][loader lane]
     float re[2][BUFF];
     float a[NA][BUFF];
-    float y[4][BUFF];  // the low-pass outputs (SDRG_LPF_GSTORE: unused, kept so the other rings keep their offsets)
+    float y[4][BUFF];  // the low-pass outputs
     float d[2][BUFF];
     float g[2][BUFF];
     float out[2][BUFF];
@@ -334,40 +284,6 @@ constexpr int NCO_LDS_BYTES = 2 * CH * 4;
 
 __device__ __forceinline__ int ceil_div_i(int a, int b) {  // b > 0, any sign of a
     return a >= 0 ? (a + b - 1) / b : -((-a) / b);
-}
-
-// Chunk counters (SDRG_PIPE_FLAGS): plain LDS reads (volatile: re-read on every poll; through an LDS pointer, since
-// address-space inference leaves volatile accesses flat, and a flat load waits on vmcnt, i.e. on the loader's DMA too),
-// one lane stores.
-typedef int prog_v4 __attribute__((ext_vector_type(4)));
-typedef int prog_v2 __attribute__((ext_vector_type(2)));
-template <class T>
-__device__ __forceinline__ const volatile __attribute__((address_space(3))) T *prog_ptr(const PipeLds &L, int k) {
-    return (const volatile __attribute__((address_space(3))) T *)(&L.prog[k]);
-}
-__device__ __forceinline__ int prog1(const PipeLds &L, int k) { return *prog_ptr<int>(L, k); }
-__device__ __forceinline__ prog_v2 prog2(const PipeLds &L, int k) { return *prog_ptr<prog_v2>(L, k); }  // k even
-__device__ __forceinline__ prog_v4 prog4(const PipeLds &L, int k) { return *prog_ptr<prog_v4>(L, k); }  // k % 4 == 0
-__device__ __forceinline__ void prog_store(PipeLds &L, int k, int v) {
-    *(volatile __attribute__((address_space(3))) int *)(&L.prog[k]) = v;
-}
-__device__ __forceinline__ int min4(prog_v4 v) { return min(min(v.x, v.y), min(v.z, v.w)); }
-// Wait until ok() holds: poll after s_sleep 1, at most SDRG_PIPE_SPIN_LIMIT times (a wait that long means a broken
-// schedule: raise the abort word so that every other wait gives up at once, and run on with wrong results).
-template <class Ok>
-__device__ __forceinline__ void pipe_wait(PipeLds &L, int lane, Ok ok) {
-    if (ok()) return;
-    for (int n = 0; n < SDRG_PIPE_SPIN_LIMIT; ++n) {
-        __builtin_amdgcn_s_sleep(1);
-        if (prog1(L, SDRG_PROG_ABORT) != 0 || ok()) return;
-    }
-    if (lane == 0) prog_store(L, SDRG_PROG_ABORT, 1);
-}
-// Publish `count` finished chunks: after every LDS access of those chunks in program order (the asm barrier stops
-// the compiler moving them below the store; LDS keeps one wave's order)
-__device__ __forceinline__ void pipe_publish(PipeLds &L, int k, int count, int lane) {
-    asm volatile("" ::: "memory");
-    if (lane == 0) prog_store(L, k, count);
 }
 
 template <int FMT>
@@ -480,7 +396,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                                                           int nsl_mask, const int4 *__restrict__ chunk_out,
                                                           const float *__restrict__ taps,
                                                           SsbStreamState *__restrict__ state,
-                                                          int16_t *__restrict__ pcm, float *__restrict__ yring,
+                                                          int16_t *__restrict__ pcm,
                                                           unsigned long long *__restrict__ stamps, int prio_mask,
                                                           int skip_mask, unsigned long long role_map, AudioFront af) {
 #if SDRG_PIPE_DYN_LDS  // the whole LDS dynamic: the compiler's occupancy model then sees no LDS limit
@@ -500,34 +416,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     const int S = p.samp_count;
     const int nch = (S + CH - 1) / CH;
     const int D = p.decim, NT = p.n_taps, PL = p.pcm_len;
-    // the low-pass outputs of chunk c, stream row sl: the LDS ring, or (SDRG_LPF_GSTORE) slot c mod GRING of this
-    // workgroup's global ring ([slot][stream][CH] floats), read past L1 (sc1: the stores came from another wave of the CU)
-#if SDRG_LPF_GSTORE
-    // (formed where used: values live across the role branches would take VGPRs from every role)
-    auto y_wg = [&]() { return yring + (size_t)blockIdx.x * SDRG_LPF_GRING * PG * CH; };
-    auto y_row = [&](int c, int sl) { return y_wg() + ((c & (SDRG_LPF_GRING - 1)) * PG + sl) * CH; };
-    auto y_load4 = [&](int c, int sl, int i) {
-        const __amdgpu_buffer_rsrc_t y_rs =
-            __builtin_amdgcn_make_buffer_rsrc(y_wg(), (short)0, SDRG_LPF_GRING * PG * CH * 4, 0x00020000);
-        const auto u = __builtin_amdgcn_raw_buffer_load_b128(y_rs, (((c & (SDRG_LPF_GRING - 1)) * PG + sl) * CH + i) * 4, 0, 16);
-        return make_float4(__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3]));
-    };
-#else
-    (void)yring;
-    auto y_row = [&](int c, int sl) { return &L.y[c & 3][sl * ROW]; };
-#endif
+    auto y_row = [&](int c, int sl) { return &L.y[c & 3][sl * ROW]; };  // the low-pass outputs of chunk c, row sl
 
     for (int i = tid; i < TAPS_COPIES * TAPS_ROW; i += PIPE_T) {
         const int sh = i / TAPS_ROW, j = i % TAPS_ROW;
         const int k = j + sh - CH;  // copy sh holds taps_pad[j + sh] at index j
         L.taps_sh[sh][j] = (k >= 0 && k < NT) ? taps[k] : 0.0f;
     }
-    if (tid < 16) L.prog[tid] = 0;
 
     const int my_s = lane & (PG - 1);  // serial roles: lane = 16 x copy + stream (all 64 lanes run; lanes < PG store)
-    // the hand-scheduled serial roles' lanes (SDRG_SERIAL_LANES): ser_on = the lane holds stream ser_s
-    const bool ser_on = SDRG_SERIAL_LANES ? (lane & 12) == 0 : lane < PG;
-    const int ser_s = SDRG_SERIAL_LANES ? (((lane >> 4) << 2) | (lane & 3)) : my_s;
     const float demod_k = p.upper ? 2.0f : 0.0f;  // demodSSB(y, y) = y + y or y - y (:89-94) as y * k
     const bool serial_live = (wave < 3 || wave == W_EQ) && (lane < PG) && (s0 + lane < n_frames);
     // issue priority per role: a bit mask of roles at priority 2, or (bit 31 set) two bits of priority level per role
@@ -576,7 +473,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     // the register allocator sees one role per loop and the kernel's VGPR count is the largest role's,
     // not the sum of every role's loop-invariant values.
     auto chunk_loop = [&](auto &&body) {
-        for (int it = 0; it < nch + 8 + LA + GS; ++it) {
+        for (int it = 0; it < nch + 8 + LA; ++it) {
             if (stamps) st_a = __builtin_amdgcn_s_memtime();
             body(it);
             if (stamps) {
@@ -586,60 +483,28 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             lds_barrier();
         }
     };
-    // body(c) for the chunks c = 0 .. nch-1 of a role whose counter is `k`: with the barrier at iteration c + off of
-    // the common loop; with the counters (SDRG_PIPE_FLAGS) as soon as ok(c) holds, then publishing c + 1
-    auto run = [&](int off, int k, auto &&ok, auto &&body) {
-#if SDRG_PIPE_FLAGS
-        (void)off;
-        for (int c = 0; c < nch; ++c) {
-            pipe_wait(L, lane, [&] { return ok(c); });
-            if (stamps) st_a = __builtin_amdgcn_s_memtime();
-            body(c);
-            if (stamps) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                st_work += __builtin_amdgcn_s_memtime() - st_a;
-            }
-            pipe_publish(L, k, c + 1, lane);
-        }
-#else
-        (void)k;
-        (void)ok;
+    // body(c) for the chunks c = 0 .. nch-1, with the barrier at iteration c + off of the common loop
+    auto run = [&](int off, auto &&body) {
         chunk_loop([&](int it) {
             const int c = it - off;
             if (c >= 0 && c < nch) body(c);
         });
-#endif
     };
-    // this wave's counter (SDRG_PIPE_FLAGS)
-    const int my_prog = wave == W_DC ? SDRG_PROG_DC : wave == W_LPF ? SDRG_PROG_LPF : wave == W_AGC ? SDRG_PROG_AGC
-                      : wave == W_LOAD ? SDRG_PROG_LOAD : wave == W_FIR0 ? SDRG_PROG_FIR0 : wave == W_FIR1 ? SDRG_PROG_FIR1
-                      : wave == W_OUT ? SDRG_PROG_OUT : wave == W_EQ ? SDRG_PROG_EQ : SDRG_PROG_DES + (wave - W_DES0);
     if ((skip_mask >> wave) & 1) {
-#if SDRG_PIPE_FLAGS
-        pipe_publish(L, my_prog, nch, lane);
-#else
         chunk_loop([&](int) {});
-#endif
     } else if (wave == W_DC) {
         float dc = 0.0f;  // removeDC: reset per call (:50)
         // needs: the loader's chunk c; the low-pass wave done with chunk c - 3 (it reads c - 2 during c - 3)
-        run(1, my_prog, [&](int c) { const prog_v2 f = prog2(L, SDRG_PROG_LPF); return (f.y >= c + 1) & (f.x >= c - 2); },
-            [&](int c) {
+        run(1, [&](int c) {
             // ---- removeDC (:49-55) and the a0*x term of iir2Process, chunk it-1 ----
             // the frame's last chunk runs whole too: dc restarts every frame and the samples past the frame end
             // (zeros from the loader) only feed outputs nothing reads
             const float alpha = 0.9995f, one_minus = 1.0f - 0.9995f, a0 = p.lpf[0];
-            if (SDRG_DC_ASM && !(SDRG_SERIAL_FULL_EXEC & 1) && c >= 0 && c < nch && ser_on) {
+            if (SDRG_DC_ASM && c >= 0 && c < nch && lane < PG) {
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 const f2v om2 = {one_minus, one_minus}, a02 = {a0, a0};
-                const uint32_t src = lds_addr(&L.re[c & 1][ser_s * ROW]), dst = lds_addr(&L.a[c % NA][ser_s * ROW]);
-                if (SDRG_SERIAL_SPLIT & 1) {
-                    unsigned long long sv;
-                    asm volatile(SDRG_DC_CHUNK_IL_SPLIT_ASM
-                                 : [dc] "+v"(dc), [sv] "=&s"(sv)
-                                 : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
-                                 : SDRG_CHUNK_CLOBBERS, "memory");
-                } else if (SDRG_DC_ASM == 2)
+                const uint32_t src = lds_addr(&L.re[c & 1][my_s * ROW]), dst = lds_addr(&L.a[c % NA][my_s * ROW]);
+                if (SDRG_DC_ASM == 2)
                     asm volatile(SDRG_DC_CHUNK_IL_ASM
                                  : [dc] "+v"(dc)
                                  : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
@@ -649,7 +514,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                                  : [dc] "+v"(dc)
                                  : [src] "v"(src), [dst] "v"(dst), [alpha] "s"(alpha), [om2] "s"(om2), [a02] "s"(a02)
                                  : SDRG_CHUNK_CLOBBERS, "memory");
-            } else if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 1) || lane < PG)) {
+            } else if (c >= 0 && c < nch && lane < PG) {
                 row_pipeline(&L.re[c & 1][my_s * ROW], &L.a[c % NA][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                     for (int q = 0; q < SB; q++) {
@@ -661,11 +526,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         });
     } else if (wave == W_LPF) {
         float z1 = 0.0f, z2 = 0.0f;  // rfFilter state, carried across frames
-        const bool lpf_asm_loop = LA && SDRG_LPF_ASM == 1 && !(SDRG_SERIAL_FULL_EXEC & 2) && S % CH == 0;
-        const int ls = lpf_asm_loop ? ser_s : my_s;  // this lane's stream
-        if (s0 + ls < n_frames) {
-            z1 = state[s0 + ls].lpf_z1;
-            z2 = state[s0 + ls].lpf_z2;
+        const bool lpf_asm_loop = LA && SDRG_LPF_ASM && S % CH == 0;
+        if (s0 + my_s < n_frames) {
+            z1 = state[s0 + my_s].lpf_z1;
+            z2 = state[s0 + my_s].lpf_z2;
         }
         // y = ((((a0 x + a1 z1) + a2 z2) - b1 z1) - b2 z2): the four products as two packed multiplies (each
         // lane of v_pk_mul_f32 rounds like v_mul_f32), the adds in order; the subtractions are additions of
@@ -676,73 +540,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
             // the whole loop as one block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py): nch + 8 + LA iterations
             // with one s_barrier each, the same count as every other role's chunk_loop
             f2v z = {z1, z2};
-#if SDRG_LPF_GSTORE
-            const uint32_t abase = lds_addr(&L.a[0][ser_s * ROW]), ybase = (uint32_t)(ser_s * CH * 4);
-#else
-            const uint32_t abase = lds_addr(&L.a[0][ser_s * ROW]), ybase = lds_addr(&L.y[0][ser_s * ROW]);
-#endif
-            const int nit = nch + 8 + LA + GS;
+            const uint32_t abase = lds_addr(&L.a[0][my_s * ROW]), ybase = lds_addr(&L.y[0][my_s * ROW]);
+            const int nit = nch + 8 + LA;
             unsigned long long sv;
             int t_it, t_cc, t_r, t_yo;
-#if SDRG_PIPE_FLAGS
-            static_assert(SDRG_LPF_INTERLEAVE && !SDRG_SERIAL_LANES, "the counter loop is the interleaved 16-lane form");
-            (void)nit;
-            (void)t_it;
-            int t1, t2;
-            unsigned long long tm;
-            const uint32_t pbase = lds_addr(reinterpret_cast<const float *>(&L.prog[0]));
-            // no stamps inside the block: its work slot holds the loop start (see the report below)
-            asm volatile(SDRG_LPF_LOOP_FLAGS_ASM
-                         : [z] "+v"(z), [sv] "=&s"(sv), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo),
-                           [t1] "=&s"(t1), [t2] "=&s"(t2), [tm] "=&s"(tm)
-                         : [abase] "v"(abase), [ybase] "v"(ybase), [pbase] "v"(pbase), [c1] "s"(c1), [c2] "s"(c2),
-                           [nch] "s"(nch)
-                         : SDRG_CHUNK_CLOBBERS, "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "vcc",
-                           "memory");
-#elif SDRG_LPF_GSTORE
-            static_assert(SDRG_LPF_INTERLEAVE && !SDRG_SERIAL_LANES && !SDRG_LPF_COPIES && !SDRG_LPF_SRC1, "gstore: the IL loop");
-            static_assert(PG * CH * 4 == (1 << SDRG_LPF_GSLOT_LOG2), "global ring slot");
-            float *ygs = yring + (size_t)blockIdx.x * SDRG_LPF_GRING * PG * CH;
-#if SDRG_LPF_SPLIT
-            asm volatile(SDRG_LPF_LOOP_IL_SPLIT_GSTORE_ASM
-                         : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
-                         : [abase] "v"(abase), [ybase] "v"(ybase), [ygs] "s"(ygs), [c1] "s"(c1), [c2] "s"(c2),
-                           [nit] "s"(nit), [nch] "s"(nch)
-                         : SDRG_CHUNK_CLOBBERS, "v54", "memory");
-#else
-            asm volatile(SDRG_LPF_LOOP_IL_GSTORE_ASM
-                         : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
-                         : [abase] "v"(abase), [ybase] "v"(ybase), [ygs] "s"(ygs), [c1] "s"(c1), [c2] "s"(c2),
-                           [nit] "s"(nit), [nch] "s"(nch)
-                         : SDRG_CHUNK_CLOBBERS, "v54", "memory");
-#endif
-#else
-            if (SDRG_LPF_SPLIT)  // lab: VALU on all 64 lanes, the LDS operations on the 16 stream lanes
-                asm volatile(SDRG_LPF_LOOP_IL_SPLIT_ASM
-                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
-                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
-                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
-            else if (SDRG_LPF_COPIES && SDRG_LPF_SRC1)
-                asm volatile(SDRG_LPF_LOOP_IL_COPIES_SRC1_ASM
-                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
-                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
-                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
-            else if (SDRG_LPF_SRC1)
-                asm volatile(SDRG_LPF_LOOP_IL_SRC1_ASM
-                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
-                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
-                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
-            else if (SDRG_LPF_COPIES)  // lab: four copies of the 16 streams on all 64 lanes (lane l: stream l mod 16)
-                asm volatile(SDRG_LPF_LOOP_IL_COPIES_ASM
-                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
-                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
-                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
-            else if (SDRG_LPF_INTERLEAVE && SDRG_SERIAL_LANES)
-                asm volatile(SDRG_LPF_LOOP_IL_SPREAD_ASM
-                             : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
-                             : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
-                             : SDRG_CHUNK_CLOBBERS, "v54", "memory");
-            else if (SDRG_LPF_INTERLEAVE)
+            if (SDRG_LPF_INTERLEAVE)
                 asm volatile(SDRG_LPF_LOOP_IL_ASM
                              : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                              : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
@@ -752,58 +554,20 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                              : [z] "+v"(z), [sv] "=&s"(sv), [it] "=&s"(t_it), [cc] "=&s"(t_cc), [r] "=&s"(t_r), [yo] "=&s"(t_yo)
                              : [abase] "v"(abase), [ybase] "v"(ybase), [c1] "s"(c1), [c2] "s"(c2), [nit] "s"(nit), [nch] "s"(nch)
                              : SDRG_CHUNK_CLOBBERS, "v54", "memory");
-#endif
             z1 = z.x;
             z2 = z.y;
-        } else run(2 + LA, my_prog, [&](int c) {
-                // needs: the DC wave's chunk c; every reader of output slot c mod 4 done with chunk c - 4
-                const int dc = prog1(L, SDRG_PROG_DC), y = min(min4(prog4(L, SDRG_PROG_DES)), prog1(L, SDRG_PROG_OUT));
-                return (dc >= c + 1) & (y >= c - 3);
-            }, [&](int c) {
+        } else run(2 + LA, [&](int c) {
             // ---- iir2Process recurrence (:75-84), chunk it-2 ----
-            if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 2) || lane < PG)) {
+            if (c >= 0 && c < nch && lane < PG) {
                 const int lim = min(CH, S - c * CH);
-#ifdef SDRG_DIAG_LPF_NOLDS  // diagnostic build only: the recurrence on register data, no LDS traffic
-                if (true) {
-                    float v[CH];
-#pragma unroll
-                    for (int q = 0; q < CH; q++) v[q] = (float)(q + c) * 1e-3f;
-#pragma unroll
-                    for (int q = 0; q < CH; q++) {
-                        const f2v p1 = c1 * z1, p2 = c2 * z2;
-                        const float y = (((v[q] + p1.x) + p2.x) + p1.y) + p2.y;
-                        z2 = z1;
-                        z1 = y;
-                    }
-                } else
-#endif
-                if (lim == CH && SDRG_LPF_ASM && !GS && !(SDRG_SERIAL_FULL_EXEC & 2)) {
+                if (lim == CH && SDRG_LPF_ASM) {
                     // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                     f2v z = {z1, z2};
                     const uint32_t src = lds_addr(&L.a[c % NA][my_s * ROW]), dst = lds_addr(y_row(c, my_s));
-                    if (SDRG_LPF_ASM == 3) {  // lab: the chain on register data, no LDS (wrong results)
-                        asm volatile(SDRG_LPF_CHUNK_NOLDS_ASM
-                                     : [z] "+v"(z)
-                                     : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
-                                     : SDRG_CHUNK_CLOBBERS, "memory");
-                    } else if (SDRG_LPF_ASM == 4) {  // lab: as 3 on all 64 lanes
-                        unsigned long long sv;
-                        asm volatile(SDRG_LPF_CHUNK_NOLDS_SPLIT_ASM
-                                     : [z] "+v"(z), [sv] "=&s"(sv)
-                                     : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
-                                     : SDRG_CHUNK_CLOBBERS, "memory");
-                    } else if (SDRG_LPF_ASM == 2) {  // VALU on all 64 lanes, LDS on the 16 stream lanes
-                        unsigned long long sv;
-                        asm volatile(SDRG_LPF_CHUNK_SPLIT_ASM
-                                     : [z] "+v"(z), [sv] "=&s"(sv)
-                                     : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
-                                     : SDRG_LPF_CHUNK_CLOBBERS, "memory");
-                    } else {
-                        asm volatile(SDRG_LPF_CHUNK_ASM
-                                     : [z] "+v"(z)
-                                     : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
-                                     : SDRG_LPF_CHUNK_CLOBBERS, "memory");
-                    }
+                    asm volatile(SDRG_LPF_CHUNK_ASM
+                                 : [z] "+v"(z)
+                                 : [src] "v"(src), [dst] "v"(dst), [c1] "s"(c1), [c2] "s"(c2)
+                                 : SDRG_LPF_CHUNK_CLOBBERS, "memory");
                     z1 = z.x;
                     z2 = z.y;
                 } else if (lim == CH) {
@@ -829,12 +593,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                     }
                 }
             }
-            // global ring: the chunk's stores complete before the barrier (its readers load it one iteration later)
-            if constexpr (GS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         });
-        if ((lpf_asm_loop ? ser_on : lane < PG) && s0 + ls < n_frames) {
-            state[s0 + ls].lpf_z1 = z1;
-            state[s0 + ls].lpf_z2 = z2;
+        if (lane < PG && s0 + my_s < n_frames) {
+            state[s0 + my_s].lpf_z1 = z1;
+            state[s0 + my_s].lpf_z2 = z2;
         }
     } else if (wave == W_AGC) {
         float gain = 1.0f;  // adaptiveAGC: reset per call (:102)
@@ -844,23 +606,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         const f2v rates = {p.agc_fast, 0.00035f};
         const f2v keep = {1.0f - p.agc_fast, 1.0f - 0.00035f};
         // needs: the four desired-level waves' chunk c; the clamp wave done with chunk c - 2
-        run(4 + LA + GS, my_prog, [&](int c) {
-                const int d = min4(prog4(L, SDRG_PROG_DES)), o = prog1(L, SDRG_PROG_OUT);
-                return (d >= c + 1) & (o >= c - 1);
-            },
-            [&](int c) {
+        run(4 + LA, [&](int c) {
             // ---- adaptiveAGC gain recurrence (:101-115), chunk it-4 ----
-            if (SDRG_AGC_ASM && !(SDRG_SERIAL_FULL_EXEC & 4) && c >= 0 && c < nch && ser_on) {
+            if (SDRG_AGC_ASM && c >= 0 && c < nch && lane < PG) {
                 // the whole chunk as one hand-scheduled block (csrc/ssb_lpf_asm.h, tools/gen/gen_lpf_asm.py)
                 f2v g = {gain, gain};
-                const uint32_t src = lds_addr(&L.d[c & 1][ser_s * ROW]), dst = lds_addr(&L.g[c & 1][ser_s * ROW]);
-                if (SDRG_SERIAL_SPLIT & 4) {
-                    unsigned long long sv;
-                    asm volatile(SDRG_AGC_CHUNK_IL_SPLIT_ASM
-                                 : [g] "+v"(g), [sv] "=&s"(sv)
-                                 : [src] "v"(src), [dst] "v"(dst), [keep] "s"(keep), [rates] "s"(rates)
-                                 : SDRG_CHUNK_CLOBBERS, "vcc", "memory");
-                } else if (SDRG_AGC_ASM == 2)
+                const uint32_t src = lds_addr(&L.d[c & 1][my_s * ROW]), dst = lds_addr(&L.g[c & 1][my_s * ROW]);
+                if (SDRG_AGC_ASM == 2)
                     asm volatile(SDRG_AGC_CHUNK_IL_ASM
                                  : [g] "+v"(g)
                                  : [src] "v"(src), [dst] "v"(dst), [keep] "s"(keep), [rates] "s"(rates)
@@ -871,7 +623,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                                  : [src] "v"(src), [dst] "v"(dst), [keep] "s"(keep), [rates] "s"(rates)
                                  : SDRG_CHUNK_CLOBBERS, "vcc", "memory");
                 gain = g.x;
-            } else if (c >= 0 && c < nch && ((SDRG_SERIAL_FULL_EXEC & 4) || lane < PG)) {
+            } else if (c >= 0 && c < nch && lane < PG) {
                 row_pipeline(&L.d[c & 1][my_s * ROW], &L.g[c & 1][my_s * ROW], lane < PG, [&](float (&v)[SB]) {
 #pragma unroll
                     for (int q = 0; q < SB; q++) {
@@ -894,7 +646,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         };
         if (p.nco_on && nch > 0) nco_fetch(0);
         // needs: the DC wave done with chunk c - 2 (slot c mod 2)
-        run(0, my_prog, [&](int c) { return prog1(L, SDRG_PROG_DC) >= c - 1; }, [&](int it) {
+        run(0, [&](int it) {
             const float2 nco_hc = nco_h, nco_lc = nco_l;  // chunk it's entries
             if (p.nco_on && it + 1 < nch) nco_fetch(it + 1);
             if constexpr (DMA) {
@@ -985,11 +737,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
     } else if (wave == W_FIR0 || wave == W_FIR1) {
         float facc[MAX_SLOTS / 4] = {};  // FIR accumulators (slots j*4 + lane/16)
         // needs: the clamp wave's chunk c; the equaliser done with chunk c - 2
-        run(6 + LA + GS, my_prog, [&](int c) {
-                const int o = prog1(L, SDRG_PROG_OUT), e = prog1(L, SDRG_PROG_EQ);
-                return (o >= c + 1) & (e >= c - 1);
-            },
-            [&](int c) {
+        run(6 + LA, [&](int c) {
             // ---- FIR accumulation (:136-141) for chunk it-6: lane = (slot mod 4, stream); slot groups
             //      4j..4j+3 split between the two FIR waves ----
             if (c >= 0 && c < nch && PL > 0) {
@@ -1009,8 +757,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         });
     } else if (wave == W_OUT) {
         // needs: the AGC wave's chunk c (the low-pass output of chunk c is older); both FIR waves done with chunk c - 2
-        run(5 + LA + GS, my_prog, [&](int c) { const prog_v4 f = prog4(L, SDRG_PROG_AGC); return (f.x >= c + 1) & (min(f.y, f.z) >= c - 1); },
-            [&](int c) {
+        run(5 + LA, [&](int c) {
             // ---- AGC output clamp(x * gain, -1, 1) (:108), chunk it-5; zero beyond the frame end ----
             // lane = 4 x stream + part of 8 samples.  x = demodSSB(y, y) = y + y (upper) or y - y (lower)
             // is y * 2 or y * 0: equal values (the lower sideband's zero may carry y's sign, which the
@@ -1020,12 +767,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
                 for (int g8 = 0; g8 < CH / 32; ++g8) {
                     const int sl = lane >> 2, part = lane & 3, within = part * (CH / 4) + g8 * 8;
                     const float *gr = &L.g[c & 1][sl * ROW + within];
-#if SDRG_LPF_GSTORE
-                    const float4 ya = y_load4(c, sl, within), yb = y_load4(c, sl, within + 4);
-#else
                     const float *yr = &L.y[c & 3][sl * ROW + within];
                     const float4 ya = *reinterpret_cast<const float4 *>(yr), yb = *reinterpret_cast<const float4 *>(yr + 4);
-#endif
                     const float4 ga = *reinterpret_cast<const float4 *>(gr), gb = *reinterpret_cast<const float4 *>(gr + 4);
                     const f2v k2 = {demod_k, demod_k};
                     f2v o[4] = {(f2v{ya.x, ya.y} * k2) * f2v{ga.x, ga.y}, (f2v{ya.z, ya.w} * k2) * f2v{ga.z, ga.w},
@@ -1062,8 +805,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         float *my_new = front ? af.new_e + (size_t)(serial_live ? s0 + my_s : 0) * (size_t)af.max_new : nullptr;
         int np = 0;
         // needs: both FIR waves' chunk c
-        run(7 + LA + GS, my_prog, [&](int c) { const prog_v4 f = prog4(L, SDRG_PROG_AGC); return min(f.y, f.z) >= c + 1; },
-            [&](int ce) {
+        run(7 + LA, [&](int ce) {
             // ---- HP -> BP -> transientBoost -> floatToPCM on the outputs the FIR completed, chunk it-7 ----
             if (ce >= 0 && ce < nch && lane < PG && s0 + my_s < n_frames && PL > 0) {
                 const int c = ce;
@@ -1098,28 +840,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(PIPE_T, PIPE_T), amdgpu_wa
         }
     } else {
         // needs: the low-pass wave's chunk c; the AGC wave done with chunk c - 2
-        run(3 + LA + GS, my_prog, [&](int c) {
-                const int y = prog1(L, SDRG_PROG_LPF), a = prog1(L, SDRG_PROG_AGC);
-                return (y >= c + 1) & (a >= c - 1);
-            },
-            [&](int c) {
+        run(3 + LA, [&](int c) {
             // waves 8-11: lane = CH/16 consecutive samples of one stream (256 lanes = the 16 x CH chunk)
             constexpr int SPL = CH / 16;
             const int hl = (wave == W_DES0 ? 0 : wave == W_DES1 ? 1 : wave == W_DES2 ? 2 : 3) * 64 + lane;
             const int sl = hl / (CH / SPL), i0 = (hl % (CH / SPL)) * SPL;
             // ---- AGC "desired" level (:104-107), chunk it-3 ----
             if (c >= 0 && c < nch) {
-#if SDRG_LPF_GSTORE
-                static_assert(SPL == 4, "one 16-byte load per lane");
-                const float4 y4 = y_load4(c, sl, i0);
-#endif
 #pragma unroll
                 for (int h = 0; h < SPL; h += 2) {
-#if SDRG_LPF_GSTORE
-                    const float2 y2 = h == 0 ? make_float2(y4.x, y4.y) : make_float2(y4.z, y4.w);
-#else
                     const float2 y2 = *reinterpret_cast<const float2 *>(&L.y[c & 3][sl * ROW + i0 + h]);
-#endif
                     // fabsf(demodSSB(y, y)) == |y| * k exactly (k = 2 or 0)
                     const f2v a = f2v{fabsf(y2.x), fabsf(y2.y)} * f2v{demod_k, demod_k};
                     // target / (sqrtf(fabsf(a) + 1e-8f) + 1e-6f), correctly rounded, two lanes per op (ssb_math.h)
@@ -1318,17 +1048,6 @@ int ssb_pipe_chunk(void) { return CH; }
 #ifndef SDRG_EXT_STOP
 #define SDRG_EXT_STOP 1
 #endif
-#ifndef SDRG_SSB64  // 1 (lab builds only): the 64-stream front/back split where it applies (tools/lab/ssb64.hip)
-#define SDRG_SSB64 0
-#endif
-#if SDRG_SSB64
-// tools/lab/ssb64.hip: the chain with 64 streams per serial wave (a front and a back workgroup per 64 streams); launch_ssb
-// takes it when ssb64_supported (scratch: [n_frames][samp_count] floats for the front -> back hand-off)
-bool ssb64_supported(const SsbParams &p, const void *iq, int fmt, int n_frames, int nsl_mask, bool have_scratch);
-hipError_t launch_ssb64(const void *iq, int fmt, int n_frames, const SsbParams &p, int nsl_mask, const int *chunk_table,
-                        const float *taps, SsbStreamState *state, float *scratch, int16_t *pcm, const AudioFront *audio,
-                        hipStream_t stream, hipEvent_t stop, bool *stop_recorded);
-#endif
 hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p, const float *taps,
                       const int *chunk_table, SsbStreamState *state, float *scratch, int16_t *pcm,
                       const AudioFront *audio, hipStream_t stream, hipEvent_t stop, bool *stop_recorded) {
@@ -1337,23 +1056,7 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
     int nsl_mask = 3;
     const char *src = reinterpret_cast<const char *>(iq);
     const int4 *chunk_out = reinterpret_cast<const int4 *>(chunk_table);
-    // the 64-stream front/back split (ssb64.hip), where it applies (SDRG_SSB64; lab builds: the environment knob of the
-    // same name overrides)
-#if SDRG_SSB64  // lab builds only (profiles/r5_ssb64_stamps.md): not faster than this pipeline, see DESIGN.md 3.3
-    static const int use64 = [] {
-        const char *v = lab_getenv("SDRG_SSB64");
-        return v ? atoi(v) : SDRG_SSB64;
-    }();
-    if (use64 && chunk_out && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels() &&
-        ssb64_supported(p, iq, fmt, n_frames, nsl_mask, scratch != nullptr))
-        return launch_ssb64(iq, fmt, n_frames, p, nsl_mask, chunk_table, taps, state, scratch, pcm, audio, stream, stop,
-                            stop_recorded);
-#endif
-    // SDRG_LPF_GSTORE: the low-pass ring lives in the SSB scratch ([n_frames][samp_count + pcm_len] floats)
-    float *yring = scratch;
-    const bool ring_ok = !GS || (scratch && (size_t)((n_frames + PG - 1) / PG) * SDRG_LPF_GRING * PG * CH <=
-                                                (size_t)n_frames * (size_t)p.samp_count);
-    if (chunk_out && ring_ok && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels()) {
+    if (chunk_out && ssb_pipe_supported(p, &nsl_mask) && !ssb_force_reference_kernels()) {
         const dim3 grid((n_frames + PG - 1) / PG);
         size_t pad = PIPE_LDS_TARGET > (int)sizeof(PipeLds) ? PIPE_LDS_TARGET - sizeof(PipeLds) : 0;
         if (p.nco_on && pad < (size_t)NCO_LDS_BYTES) pad = NCO_LDS_BYTES;  // the dynamic part holds the chunk phasors
@@ -1410,13 +1113,13 @@ hipError_t launch_ssb(const void *iq, int fmt, int n_frames, const SsbParams &p,
     if (ext)                                                                                                     \
         hipExtLaunchKernelGGL(dma ? ssb_pipe_kernel<F, true> : ssb_pipe_kernel<F, false>, grid, dim3(PIPE_T),   \
                               (uint32_t)pad, stream, nullptr, stop, 0u, src, n_frames, p, nsl_mask, chunk_out, taps,   \
-                              state, pcm, yring, stamps, prio_mask, skip_mask, role_map, af);                    \
+                              state, pcm, stamps, prio_mask, skip_mask, role_map, af);                    \
     else if (dma)                                                                                                \
         hipLaunchKernelGGL((ssb_pipe_kernel<F, true>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
-                           chunk_out, taps, state, pcm, yring, stamps, prio_mask, skip_mask, role_map, af);                                         \
+                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map, af);                                         \
     else                                                                                                         \
         hipLaunchKernelGGL((ssb_pipe_kernel<F, false>), grid, dim3(PIPE_T), pad, stream, src, n_frames, p, nsl_mask, \
-                           chunk_out, taps, state, pcm, yring, stamps, prio_mask, skip_mask, role_map, af);
+                           chunk_out, taps, state, pcm, stamps, prio_mask, skip_mask, role_map, af);
         switch (fmt) {
         case SDRG_IQ_CS8: SDRG_PIPE_LAUNCH(SDRG_IQ_CS8); break;
         case SDRG_IQ_CU8: SDRG_PIPE_LAUNCH(SDRG_IQ_CU8); break;

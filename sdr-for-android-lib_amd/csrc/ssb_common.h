@@ -1,5 +1,5 @@
 // ssb_common.h — raw-IQ unpack, the NCO mix and LDS helpers shared by the SSB kernels (ssb.hip: the 16-stream
-// pipeline and the lane-per-stream kernels; tools/lab/ssb64.hip: the lab-only 64-stream front/back split).  Unpack conventions as
+// pipeline and the lane-per-stream kernels).  Unpack conventions as
 // include/sdrg.h: CS8 v/128, CU8 (v - 127.4)/128, CS16 v/32768, CF32 as is.
 #pragma once
 

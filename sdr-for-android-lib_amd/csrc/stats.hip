@@ -145,28 +145,6 @@ struct WideScan {
     int peak_idx;
 };
 
-// Which wave takes which role of scan_wide.  SDRG_WIDE_MAP 0: by wave index (wave 0 chains).  1: by placement -- when the
-// workgroup's four waves sit on four distinct SIMDs (HW_ID SIMD_ID), the chain role goes to the wave on SIMD
-// (TG_ID mod 4), so the four frames sharing a CU (thread-group slots 0-3) put their chain waves on four different
-// SIMDs instead of all on the SIMD of wave 0; otherwise by wave index.  SDRG_WIDE_PRIO: the chain wave's issue
-// priority during the scan.
-#ifndef SDRG_WIDE_MAP
-#define SDRG_WIDE_MAP 0
-#endif
-#ifndef SDRG_WIDE_PRIO
-#define SDRG_WIDE_PRIO 0
-#endif
-// SDRG_WIDE_SETS: register sets of 16 bins the chain wave cycles through (its LDS reads run SETS - 1 half-steps
-// ahead of the adds); SDRG_WIDE_PF: chunks the producers fetch ahead into registers (1 or 2)
-#ifndef SDRG_WIDE_SETS
-#define SDRG_WIDE_SETS 2
-#endif
-#ifndef SDRG_WIDE_PF
-#define SDRG_WIDE_PF 1
-#endif
-#ifndef SDRG_WIDE_FULLEXEC
-#define SDRG_WIDE_FULLEXEC 0
-#endif
 // SDRG_WIDE_DBPOOL: where the pooled-gap pass (one bottom window) gets the bottom window's dB values -- 0: evaluates
 // its 13107 logs again; 1 (lab): the producers also store every reference bin's dB value to the frame's pool scratch
 // (their stores then share vmcnt with the next chunk's loads: slower); 2 (product): the record wave copies the dB rows
@@ -175,39 +153,10 @@ struct WideScan {
 #ifndef SDRG_WIDE_DBPOOL
 #define SDRG_WIDE_DBPOOL 2
 #endif
-#ifndef SDRG_WIDE_FSPLIT
-#define SDRG_WIDE_FSPLIT 0
-#endif
-// SDRG_WIDE_LDSBAR: the wide scans' per-chunk barrier orders LDS only (s_waitcnt lgkmcnt(0); s_barrier), so the
-// producers' loads of the next chunk stay in flight across it; __syncthreads() would wait for them (vmcnt(0)) at every
-// chunk.  Nothing global is exchanged between the waves inside the scan (the pool copies are read after it, behind a
-// __syncthreads).
-#ifndef SDRG_WIDE_LDSBAR
-#define SDRG_WIDE_LDSBAR 1
-#endif
-__device__ __forceinline__ void wide_chunk_barrier() {
-    if (SDRG_WIDE_LDSBAR) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else __syncthreads();
-}
-__device__ __forceinline__ unsigned hw_id() {
-    unsigned v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
-    return v;
-}
-// sh_hw: the four waves' HW_ID words, written by wide_publish and read after a barrier
-__device__ __forceinline__ void wide_publish(unsigned *sh_hw) {
-    if (SDRG_WIDE_MAP && (threadIdx.x & 63) == 0) sh_hw[threadIdx.x >> 6] = hw_id();
-}
-__device__ __forceinline__ int wide_role(const unsigned *sh_hw) {
-    const int wv = threadIdx.x >> 6;
-    if (!SDRG_WIDE_MAP) return wv;
-    unsigned m = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) m |= 1u << ((sh_hw[i] >> 4) & 3);
-    if (m != 15) return wv;
-    const int tg = (sh_hw[0] >> 16) & 3;
-    return (int)(((sh_hw[wv] >> 4) & 3) - tg) & 3;
-}
+// The wide scans' per-chunk barrier orders LDS only (s_waitcnt lgkmcnt(0); s_barrier), so the producers' loads of the
+// next chunk stay in flight across it; __syncthreads() would wait for them (vmcnt(0)) at every chunk.  Nothing global is
+// exchanged between the waves inside the scan (the pool copies are read after it, behind a __syncthreads).
+__device__ __forceinline__ void wide_chunk_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // The focus peak of fft_process.cpp:142-154 (first strict maximum of the dB values, seeded at -130) from the largest
 // focus power pmax = out.peak_db (on entry), by monotonicity: dB(p) = 10 log10f(p + 1e-20) never decreases with p
@@ -269,7 +218,7 @@ __device__ __forceinline__ void focus_peak_monotone(const float *__restrict__ P,
 template <bool want_db>
 __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ring, int nwin, const int *wlo, const int *whi, int w,
                           int role, float *__restrict__ dbp, int wst, WideScan &out) {
-    // roles (0 chains, 1 records, 2-3 producers) are dealt to the waves by the caller (wide_role)
+    // roles: 0 chains, 1 records, 2-3 producers (role = wave index)
     const int lane = threadIdx.x & 63;
     const int fq = nwin - 1;
     // SC = 2^lg bins per window per chunk, the largest that fits; rows are RS = SC + 4 floats apart, so the chain
@@ -302,44 +251,31 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
     // ends chunk c, so their HBM latency overlaps the consumers' work instead of following it.
     constexpr int PTHREADS = WIDE_WG - 128;
     constexpr int PR = 9;  // >= SC / PG for every nwin <= 11 (SC from the ring size above)
-    // SDRG_WIDE_FSPLIT (one bottom window, three windows): wave 2 stages the two reference windows (32 lanes each),
-    // wave 3 the focus window alone, and wave 3 evaluates no logs -- the focus peak is found after the scan from the
-    // largest focus power (log10f is monotone, focus_peak_monotone) -- so its log instructions are not issued at all
-    const bool fsplit = SDRG_WIDE_FSPLIT && want_db && nwin == 3;
     const int pw = role >= 2 ? ((role - 2) << 6) | lane : 0;
-    const int PG = fsplit ? (role == 3 ? 64 : 32) : PTHREADS / nwin;
-    const int pq = fsplit ? (role == 3 ? fq : lane >> 5) : min(pw / PG, fq);
-    const int pk0 = fsplit ? (role == 3 ? lane : lane & 31) : pw - pq * PG;
-    const bool prod = role >= 2 && (fsplit || pw < PG * nwin);
-    float pmx = -INFINITY;  // fsplit: the largest focus power this thread staged
+    const int PG = PTHREADS / nwin;
+    const int pq = min(pw / PG, fq);
+    const int pk0 = pw - pq * PG;
+    const bool prod = role >= 2 && pw < PG * nwin;
     const int plo = wlo[pq], plen = whi[pq] - plo + 1;
     const float *Pq = P + plo;
     float va[PR], vb[PR];
-    // the chunk after next (SDRG_WIDE_PF 2), or the next chunk fetched before this chunk's stores (SDRG_WIDE_PF 3)
-    float va2[SDRG_WIDE_PF >= 2 ? PR : 1], vb2[SDRG_WIDE_PF >= 2 ? PR : 1];
-    auto fetch_into = [&](auto &xa, auto &xb, int c) __attribute__((always_inline)) {
+    auto fetch = [&](int c) {
         const int c0 = c << lg;
 #pragma unroll
         for (int k = 0; k < PR; k++) {
             const int t = pk0 + PG * k, e = c0 + t;
             const bool ok = t < SC && e < plen;
-            xa[k] = ok ? Pq[e] : 0.0f;
-            xb[k] = (ok && e >= w) ? Pq[e - w] : 0.0f;
+            va[k] = ok ? Pq[e] : 0.0f;
+            vb[k] = (ok && e >= w) ? Pq[e - w] : 0.0f;
         }
     };
-    auto fetch = [&](int c) { fetch_into(va, vb, c); };
-    auto store_from = [&](const auto &va, const auto &vb, int c) __attribute__((always_inline)) {
+    auto store = [&](int c) {
         const int c0 = c << lg;
         float *row = ring + (c & 1) * slot_floats + pq * 3 * RS;
 #pragma unroll
         for (int k = 0; k < PR; k++) {
             const int t = pk0 + PG * k, e = c0 + t;
-            if (t < SC && fsplit && role == 3) {  // the focus window: bins and running-sum terms, no dB
-                const float v = va[k];
-                row[t] = v;
-                row[RS + t] = (e >= w) ? v - vb[k] : v;
-                if (e < plen) pmx = fmaxf(pmx, v);
-            } else if (t < SC) {
+            if (t < SC) {
                 const bool in = e < plen;
                 const float v = va[k];
                 row[t] = v;
@@ -358,42 +294,19 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
             __builtin_amdgcn_sched_barrier(0);  // one bin's log10 at a time: interleaved they would hold ~70 VGPRs
         }
     };
-    auto store = [&](int c) { store_from(va, vb, c); };
     if (prod && nch > 0) fetch(0);
-    if (SDRG_WIDE_PF == 2 && prod && nch > 1) fetch_into(va2, vb2, 1);
 
     unsigned long long busy = 0;
     for (int c = 0; c <= nch + 1; c++) {
         const unsigned long long t_in = SDRG_STATS_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
         if (role >= 2) {
             if (prod && c < nch) {
-                if constexpr (SDRG_WIDE_PF == 3) {  // chunk c + 1's loads issue before chunk c's stores
-                    if ((c & 1) == 0) {
-                        if (c + 1 < nch) fetch_into(va2, vb2, c + 1);
-                        store(c);
-                    } else {
-                        if (c + 1 < nch) fetch(c + 1);
-                        store_from(va2, vb2, c);
-                    }
-                } else if constexpr (SDRG_WIDE_PF == 2) {  // chunk c + 2 into the registers chunk c came from
-                    if ((c & 1) == 0) {
-                        store(c);
-                        if (c + 2 < nch) fetch(c + 2);
-                    } else {
-                        store_from(va2, vb2, c);
-                        if (c + 2 < nch) fetch_into(va2, vb2, c + 2);
-                    }
-                } else {
-                    store(c);
-                    if (c + 1 < nch) fetch(c + 1);
-                }
+                store(c);
+                if (c + 1 < nch) fetch(c + 1);
             }
         } else if (role == 0) {
-            if (SDRG_WIDE_PRIO && c == 1) __builtin_amdgcn_s_setprio(SDRG_WIDE_PRIO);
-            if (c >= 1 && c <= nch && (SDRG_WIDE_FULLEXEC || chain)) {
-                // SDRG_WIDE_FULLEXEC: the wave's other lanes replay lane 0 (window 0's sum: same row, same values,
-                // the same bytes written back), so the chain's adds issue with a full EXEC mask
-                const int cj = (SDRG_WIDE_FULLEXEC && !chain) ? 0 : j, cg = (SDRG_WIDE_FULLEXEC && !chain) ? 0 : grp;
+            if (c >= 1 && c <= nch && chain) {
+                const int cj = j, cg = grp;
                 const float *slot = ring + ((c - 1) & 1) * slot_floats;
                 const float *src = slot + (cj * 3 + cg) * RS;  // x, rs terms, dB rows
                 // running values: the rs lanes' go to the rs ring (the record wave reads them); the window and dB
@@ -409,12 +322,8 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
 #pragma unroll
                     for (int i = 0; i < 4; i++) X[i] = *reinterpret_cast<const float4 *>(src + u + 4 * i);
                 };
-#ifndef SDRG_CHAIN_SRC1  // the running sum as the adds' second operand (a partial-EXEC dependent chain issues
-#define SDRG_CHAIN_SRC1 0  // sooner that way, tools/lab/lpf_exec.hip); a + b == b + a exactly
-#endif
                 auto add = [&](float x) {
-                    if (SDRG_CHAIN_SRC1) asm volatile("v_add_f32 %0, %1, %0" : "+v"(acc) : "v"(x));
-                    else acc += x;
+                    acc += x;
                     return acc;
                 };
                 auto sum16 = [&](const float4 (&X)[4], int u) {
@@ -429,45 +338,12 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
 #pragma unroll
                     for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];
                 };
-                if constexpr (SDRG_WIDE_SETS == 2) {
-                    rd(A, 0);
-                    for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
-                        rd(B, t + 16);
-                        sum16(A, t);
-                        if (t + 32 < SC) rd(A, t + 32);
-                        sum16(B, t + 16);
-                    }
-                } else if constexpr (SDRG_WIDE_SETS == 3) {  // reads two half-steps ahead
-                    float4 C[4];
-                    rd(A, 0);
-                    rd(B, 16);
-                    for (int t = 0; t < SC; t += 48) {
-                        if (t + 32 < SC) rd(C, t + 32);
-                        sum16(A, t);
-                        if (t + 16 < SC) {
-                            if (t + 48 < SC) rd(A, t + 48);
-                            sum16(B, t + 16);
-                        }
-                        if (t + 32 < SC) {
-                            if (t + 64 < SC) rd(B, t + 64);
-                            sum16(C, t + 32);
-                        }
-                    }
-                } else {  // four sets: reads three half-steps ahead (SC a multiple of 64)
-                    float4 C[4], D[4];
-                    rd(A, 0);
-                    rd(B, 16);
-                    rd(C, 32);
-                    for (int t = 0; t < SC; t += 64) {
-                        rd(D, t + 48);
-                        sum16(A, t);
-                        if (t + 64 < SC) rd(A, t + 64);
-                        sum16(B, t + 16);
-                        if (t + 64 < SC) rd(B, t + 80);
-                        sum16(C, t + 32);
-                        if (t + 64 < SC) rd(C, t + 96);
-                        sum16(D, t + 48);
-                    }
+                rd(A, 0);
+                for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
+                    rd(B, t + 16);
+                    sum16(A, t);
+                    if (t + 32 < SC) rd(A, t + 32);
+                    sum16(B, t + 16);
                 }
             }
         } else {
@@ -519,15 +395,9 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
         if (SDRG_STATS_STAMPS) busy += __builtin_amdgcn_s_memtime() - t_in;
         wide_chunk_barrier();
     }
-    if (SDRG_WIDE_PRIO && role == 0) __builtin_amdgcn_s_setprio(0);
     if (SDRG_STATS_STAMPS && lane == 0 && role <= 2 && blockIdx.x < 8192)
         g_stats_stamps[blockIdx.x * STAMP_PHASES + 6 + role] = busy;
-    if (fsplit) {
-        if (role == 3) {  // the largest focus power
-            for (int off = WAVE / 2; off > 0; off >>= 1) pmx = fmaxf(pmx, __shfl_xor(pmx, off));
-            if (lane == 0) out.peak_db = pmx;  // (the power here; focus_peak_monotone turns it into the peak)
-        }
-    } else if (role >= 2) {  // first maximum over the producer threads (lower bin on ties)
+    if (role >= 2) {  // first maximum over the producer threads (lower bin on ties)
         for (int off = WAVE / 2; off > 0; off >>= 1) {
             const float ob = __shfl_xor(pk, off);
             const int oi = __shfl_xor(pki, off);
@@ -562,9 +432,7 @@ __device__ __forceinline__ void scan_wide(const float *__restrict__ P, float *ri
     if (chain && grp == 0) out.sum[j] = acc;
     if (chain && grp == 2) out.dsum[j] = acc;
     __syncthreads();
-    if (fsplit) {
-        focus_peak_monotone<WIDE_WG>(P, wlo[fq], whi[fq] - wlo[fq] + 1, out);
-    } else if (role == 2 && lane == 0) {
+    if (role == 2 && lane == 0) {
         const bool other = pk > out.peak_db || (pk == out.peak_db && pki < out.peak_idx);
         if (other) {
             out.peak_db = pk;
@@ -898,9 +766,6 @@ __device__ float kth_smallest_wave(Visit visit, int k, int *hist, uint32_t *xch)
 #ifndef SDRG_NARROW_WPE  // lab: waves per SIMD the narrow kernel is compiled for
 #define SDRG_NARROW_WPE 8
 #endif
-#ifndef SDRG_STATS_ST_LDS  // lab: the stream's StatsState in LDS for the whole kernel instead of registers
-#define SDRG_STATS_ST_LDS 0
-#endif
 constexpr int NARROW_BATCH = SDRG_NARROW_BATCH;
 template <int R>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(R > 8 ? 6 : SDRG_NARROW_WPE))) void stats_narrow_kernel(
@@ -940,16 +805,7 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(R > 8 ? 6 
     __syncthreads();
     const int stage_total = sh_woff[n_ref + 1], stage_pad = (stage_total + 3) & ~3;
     const float *P = spectra + frame * (size_t)g.n;
-#if SDRG_STATS_ST_LDS
-    // one wave per workgroup: its LDS operations complete in order, so the copy lands before the writes below
-    __shared__ StatsState sh_st;
-    static_assert(sizeof(StatsState) % 4 == 0 && sizeof(StatsState) / 4 <= WAVE, "StatsState copy");
-    if (lane < (int)(sizeof(StatsState) / 4))
-        reinterpret_cast<uint32_t *>(&sh_st)[lane] = reinterpret_cast<const uint32_t *>(state + frame)[lane];
-    StatsState &st = sh_st;
-#else
     StatsState st = state[frame];
-#endif
     if (g.cf_changed) st.center_frequency_changed = 1;  // sdr_bridge_internal::isCenterFrequencyChanged
     sdrg_frame_record rec;
     __builtin_memset(&rec, 0, sizeof(rec));  // tail padding included: records compare and gather as bytes
@@ -1177,7 +1033,6 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
     __shared__ int w_lo[10], w_hi[10], order[10];
     __shared__ float sh_f[4];
     __shared__ int sh_geo_lo[11], sh_geo_hi[11];  // the reference windows, then the focus window (index n_ref)
-    __shared__ unsigned sh_hw[4];                   // wide_role
 
     const int lane = threadIdx.x;
     const size_t frame = blockIdx.x;
@@ -1197,9 +1052,8 @@ __global__ __launch_bounds__(WIDE_WG) __attribute__((amdgpu_waves_per_eu(4))) vo
         sh_geo_lo[n_ref] = g.focus_lo;
         sh_geo_hi[n_ref] = g.focus_hi;
     }
-    wide_publish(sh_hw);
     __syncthreads();
-    const int role = wide_role(sh_hw);
+    const int role = threadIdx.x >> 6;  // scan_wide's roles by wave
     const float *P = spectra + frame * (size_t)g.n;
     float *pool = gpool + frame * (size_t)gpool_stride;
     StatsState st = state[frame];
@@ -1409,40 +1263,12 @@ constexpr int MW_T = SDRG_MW_T;
             g_stats_stamps[blockIdx.x * STAMP_PHASES + (k)] = __builtin_amdgcn_s_memtime();                    \
     } while (0)
 constexpr int MW_F = 4;                     // frames per workgroup
-#ifndef SDRG_MW_RECW  // record waves: 1 (all frames) or MW_F (one per frame)
-#define SDRG_MW_RECW MW_F
-#endif
 #ifndef SDRG_MW_WREF  // producer lanes per reference-window lane per focus lane (a reference bin carries a log10)
 #define SDRG_MW_WREF 2
 #endif
 #ifndef SDRG_MW_ILP  // 1: the reference producers' log10s of several bins interleave (no scheduling barrier)
 #define SDRG_MW_ILP 1
 #endif
-#ifndef SDRG_MW_PRIO  // lab: the chain wave's issue priority during the scan
-#define SDRG_MW_PRIO 0
-#endif
-// SDRG_MW_MAP 1: the record waves are waves 4, 8, 12 and 1, so the chain wave (wave 0; wave w runs on SIMD w mod 4)
-// shares its SIMD with three record waves only and no producer (their f64 log10s would take its issue slots)
-#ifndef SDRG_MW_MAP
-#define SDRG_MW_MAP 0
-#endif
-#ifndef SDRG_MW_SETS  // register sets of 16 bins the chain wave cycles through (2: A / B, reads one block ahead)
-#define SDRG_MW_SETS 2
-#endif
-constexpr int MW_SETS = SDRG_MW_SETS;
-#ifndef SDRG_MW_ILP2  // lab: two frames' chains per chain lane (lanes 0-31), their adds interleaved
-#define SDRG_MW_ILP2 0
-#endif
-constexpr bool MW_ILP2 = SDRG_MW_ILP2;
-static_assert(!MW_ILP2 || MW_F == 4, "MW_ILP2 pairs frames f and f + 2");
-#ifndef SDRG_MW_WMASK  // lab: the chain writes back only the running-sum lanes' values (the only ones read)
-#define SDRG_MW_WMASK 0
-#endif
-#ifndef SDRG_MW_RDFIRST  // lab: scheduling barriers keep each block's LDS reads ahead of the previous block's sums
-#define SDRG_MW_RDFIRST 0
-#endif
-static_assert(MW_SETS == 2 || MW_SETS == 4, "the chain's sets");
-constexpr int MW_RECW = SDRG_MW_RECW;
 // The pooled gaps' dB values: 0 = evaluated again after the scan (13107 glibc-exact log10s per frame
 // at 65536 / 200 kHz, the "pool logs" phase); 1 = the record waves copy every reference window's dB row of the chunk the
 // chain is reading from the LDS ring to a per-frame HBM scratch during the scan (they issue no loads, so their stores
@@ -1453,7 +1279,7 @@ constexpr int MW_RECW = SDRG_MW_RECW;
 #ifndef SDRG_MW_DBPOOL
 #define SDRG_MW_DBPOOL 1
 #endif
-static_assert(!SDRG_MW_DBPOOL || MW_RECW == MW_F, "the dB copies run on the per-frame record waves");
+constexpr int MW_RECW = MW_F;  // record waves: one per frame
 constexpr int MW_P0 = 1 + MW_RECW;          // first producer wave
 constexpr int MW_PROD = MW_T - 64 * MW_P0;  // producer lanes
 constexpr int MW_PR = 12;                   // bins per producer lane per chunk at most (the host sizes SC for it)
@@ -1541,31 +1367,25 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
     auto frame_ptr = [&](int f) { return spectra + (size_t)frame_of(f) * (size_t)g.n; };
 
     // ---- chain wave: lane = LPFR x frame + j; j < nwin window sums, then running sums, then dB sums ----
-    // MW_ILP2: lanes 0-31 each carry the same chain of two frames, cf and cf + 2, so two independent adds issue per bin
-    const int cl = MW_ILP2 ? (lane & 31) : lane;
-    const int cf = cl / LPFR, cjj = cl - cf * LPFR;
+    const int cf = lane / LPFR, cjj = lane - cf * LPFR;
     int cg = 3, cj = 0;
     if (cjj < nwin) cg = 0, cj = cjj;
     else if (cjj < 2 * nwin) cg = 1, cj = cjj - nwin;
     else if (want_db && cjj < 3 * nwin - 1) cg = 2, cj = cjj - 2 * nwin;
-    if (MW_ILP2 && lane >= 32) cg = 3;
     const bool chain = wave == 0 && cg < 3;
-    float acc = 0.0f, acc2 = 0.0f;  // acc2: frame cf + 2 (MW_ILP2)
-    // ---- record waves: G lanes per (frame, window); one wave for all frames, or wave 1 + f for frame f ----
-    const int rfr = MW_RECW == 1 ? F : 1;  // frames per record wave
-    const int G = WAVE / (rfr * nwin), ritem = lane / G, rq0 = ritem % nwin, rk = lane - ritem * G;
-    const bool mapped = SDRG_MW_MAP && MW_RECW == MW_F && MW_T == 1024;
-    const int rwave = !mapped ? (wave >= 1 && wave <= MW_RECW ? wave - 1 : -1)
-                              : wave == 4 ? 0 : wave == 8 ? 1 : wave == 12 ? 2 : wave == 1 ? 3 : -1;  // record wave index
-    const int rf = MW_RECW == 1 ? ritem / nwin : rwave, rq = rq0;
-    const bool rec_lane = rwave >= 0 && ritem < rfr * nwin;
+    float acc = 0.0f;
+    // ---- record waves: wave 1 + f for frame f, G lanes per window ----
+    const int G = WAVE / nwin, ritem = lane / G, rq = ritem % nwin, rk = lane - ritem * G;
+    const int rwave = wave >= 1 && wave <= MW_RECW ? wave - 1 : -1;  // record wave index
+    const int rf = rwave;
+    const bool rec_lane = rwave >= 0 && ritem < nwin;
     float rm = -INFINITY;
     int ri = 0x7fffffff;
     // ---- producers: the F focus items first (pgf lanes each), then the F x fq reference items (pgr lanes each) ----
     int pgf, pgr;
     mw_lanes(n_ref, want_db, &pgf, &pgr);
     // producer ordinal: the waves that are neither the chain nor a record wave, in order
-    const int pwave = !mapped ? wave - MW_P0 : wave - 1 - (wave > 1) - (wave > 4) - (wave > 8) - (wave > 12);
+    const int pwave = wave - MW_P0;
     const bool is_prod_wave = wave != 0 && rwave < 0;
     const int pw = pwave * 64 + lane;
     int pf = 0, pq = 0, pk0 = 0, PGc = 1;
@@ -1647,7 +1467,6 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
     if (prod && nch > 0) fetch(0);
 
     unsigned long long busy = 0;
-    if (SDRG_MW_PRIO && wave == 0) __builtin_amdgcn_s_setprio(SDRG_MW_PRIO);
     for (int c = 0; c <= nch + 1; c++) {
         const unsigned long long t_in = SDRG_MW_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
         if (is_prod_wave) {
@@ -1681,71 +1500,15 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
                         acc += X[i].w;
                         r[i].w = acc;
                     }
-                    if (!SDRG_MW_WMASK || cg == 1) {  // WMASK: only the running sums are read back (record waves)
 #pragma unroll
-                        for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];
-                    }
+                    for (int i = 0; i < 4; i++) *reinterpret_cast<float4 *>(dst + u + 4 * i) = r[i];
                 };
-                if constexpr (MW_ILP2) {
-                    // two frames' chains per lane in 8-bin blocks (the same registers as two 16-bin sets): frame cf
-                    // in X0 / acc, frame cf + 2 in X1 / acc2, their adds interleaved
-                    const int fo = 2 * frame_floats;
-                    float4 A0[2], A1[2], B0[2], B1[2];
-                    auto rd2 = [&](float4 (&X0)[2], float4 (&X1)[2], int u) {
-#pragma unroll
-                        for (int i = 0; i < 2; i++) {
-                            X0[i] = *reinterpret_cast<const float4 *>(src + u + 4 * i);
-                            X1[i] = *reinterpret_cast<const float4 *>(src + fo + u + 4 * i);
-                        }
-                    };
-                    auto sum8x2 = [&](const float4 (&X0)[2], const float4 (&X1)[2], int u) {
-                        float4 r0[2], r1[2];
-#pragma unroll
-                        for (int i = 0; i < 2; i++) {
-                            acc += X0[i].x; r0[i].x = acc; acc2 += X1[i].x; r1[i].x = acc2;
-                            acc += X0[i].y; r0[i].y = acc; acc2 += X1[i].y; r1[i].y = acc2;
-                            acc += X0[i].z; r0[i].z = acc; acc2 += X1[i].z; r1[i].z = acc2;
-                            acc += X0[i].w; r0[i].w = acc; acc2 += X1[i].w; r1[i].w = acc2;
-                        }
-                        if (!SDRG_MW_WMASK || cg == 1) {
-#pragma unroll
-                            for (int i = 0; i < 2; i++) {
-                                *reinterpret_cast<float4 *>(dst + u + 4 * i) = r0[i];
-                                *reinterpret_cast<float4 *>(dst + fo + u + 4 * i) = r1[i];
-                            }
-                        }
-                    };
-                    rd2(A0, A1, 0);
-                    for (int t = 0; t < SC; t += 16) {  // SC >= 64, a multiple of 16
-                        rd2(B0, B1, t + 8);
-                        sum8x2(A0, A1, t);
-                        if (t + 16 < SC) rd2(A0, A1, t + 16);
-                        sum8x2(B0, B1, t + 8);
-                    }
-                } else if constexpr (MW_SETS == 2) {
-                    rd(A, 0);
-                    for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
-                        rd(B, t + 16);
-                        if (SDRG_MW_RDFIRST) __builtin_amdgcn_sched_barrier(0);  // the next block's reads before the sums
-                        sum16(A, t);
-                        if (t + 32 < SC) rd(A, t + 32);
-                        if (SDRG_MW_RDFIRST) __builtin_amdgcn_sched_barrier(0);
-                        sum16(B, t + 16);
-                    }
-                } else {
-                    // MW_SETS register sets of 16 bins: each set's reads are issued MW_SETS - 1 blocks before its sums
-                    // (the LDS latency under the producers' and record waves' traffic is longer than one block)
-                    float4 X[MW_SETS][4];
-#pragma unroll
-                    for (int k = 0; k < MW_SETS - 1; k++) rd(X[k], 16 * k);
-                    for (int t = 0; t < SC; t += 16 * MW_SETS) {  // SC >= 64, a power of two >= 16 MW_SETS
-#pragma unroll
-                        for (int k = 0; k < MW_SETS; k++) {
-                            const int ahead = t + 16 * (k + MW_SETS - 1);
-                            if (ahead < SC) rd(X[(k + MW_SETS - 1) % MW_SETS], ahead);
-                            sum16(X[k], t + 16 * k);
-                        }
-                    }
+                rd(A, 0);
+                for (int t = 0; t < SC; t += 32) {  // SC >= 64, a multiple of 32
+                    rd(B, t + 16);
+                    sum16(A, t);
+                    if (t + 32 < SC) rd(A, t + 32);
+                    sum16(B, t + 16);
                 }
             }
         } else if (rwave >= 0) {
@@ -1781,7 +1544,6 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
         }
         wide_chunk_barrier();
     }
-    if (SDRG_MW_PRIO && wave == 0) __builtin_amdgcn_s_setprio(0);
     if (SDRG_MW_STAMPS && lane == 0 && blockIdx.x < 8192) {  // chain, a record wave, a focus and a reference producer
         const int slot = wave == 0 ? 7 : rwave == 0 ? 8 : (is_prod_wave && pwave == 0) ? 9 : wave == MW_T / 64 - 1 ? 10 : -1;
         if (slot > 0) g_stats_stamps[blockIdx.x * STAMP_PHASES + slot] = busy;
@@ -1794,8 +1556,6 @@ __global__ __launch_bounds__(MW_T) __attribute__((amdgpu_waves_per_eu(MW_T / 256
     if (rec_lane) atomicMax(&s_rec[rf][rq], vi_key(rm, ri));
     if (chain && cg == 0) s_sum[cf][cj] = acc;
     if (chain && cg == 2) s_dsum[cf][cj] = acc;
-    if (MW_ILP2 && chain && cg == 0) s_sum[cf + 2][cj] = acc2;
-    if (MW_ILP2 && chain && cg == 2) s_dsum[cf + 2][cj] = acc2;
     __syncthreads();
     MW_STAMP(1);
 

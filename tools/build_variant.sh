@@ -14,14 +14,8 @@ $HIP -I$D/csrc -Iinclude -ffp-contract=off -fno-slp-vectorize -c ${STATS_SRC:-$D
 $HIP -I$D/csrc -Iinclude -ffp-contract=off -fno-slp-vectorize -c ${SSB_SRC:-$D/csrc/ssb.hip} -o $B/ssb.o
 $HIP -ffp-contract=off -c $D/csrc/pulse.hip -o $B/pulse.o
 $HIP -c $D/csrc/gather.hip -o $B/gather.o
-# the lab-only 64-stream SSB split (tools/lab/ssb64.hip) is compiled only into builds that select it
-SSB64_OBJ=""
-if [[ "$FLAGS" == *SDRG_SSB64=1* ]]; then
-  $HIP -I$D/csrc -Itools/lab -Iinclude -ffp-contract=off -fno-slp-vectorize -c ${SSB64_SRC:-tools/lab/ssb64.hip} -o $B/ssb64.o
-  SSB64_OBJ=$B/ssb64.o
-fi
 for f in design engine pulse_bank ingest compat ssb_processor dist; do $CXX -c $D/csrc/$f.cpp -o $B/$f.o; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/lib/libsdrg_$NAME.so $B/spectrum.o $B/fftany.o $B/stats.o \
-    $B/ssb.o $SSB64_OBJ $B/pulse.o $B/gather.o $B/design.o $B/engine.o $B/pulse_bank.o $B/ingest.o $B/compat.o $B/ssb_processor.o \
+    $B/ssb.o $B/pulse.o $B/gather.o $B/design.o $B/engine.o $B/pulse_bank.o $B/ingest.o $B/compat.o $B/ssb_processor.o \
     $B/dist.o -lm -lpthread -ldl
 echo built $D/lib/libsdrg_$NAME.so

@@ -21,7 +21,7 @@ through three rotating 16-register sub-block buffers (v0-15, v16-31, v32-47): su
 while sub-block k runs, and each wait names exactly the LDS operations still allowed in flight, so the only
 exposed LDS latency is the chunk's first read.
 Run: python tools/gen/gen_lpf_asm.py > sdr-for-android-lib_amd/csrc/ssb_lpf_asm.h
-     python tools/gen/gen_lpf_asm.py --lab > tools/lab/ssb64_lpf_asm.h
+     python tools/gen/gen_lpf_asm.py --lab > tools/lab/lab_lpf_asm.h   (lab-only variants, not in the product)
 """
 
 BUFS = [0, 16, 32]
@@ -35,20 +35,17 @@ def pair(reg):
     return f"v[{base}:{base + 1}]", reg & 1
 
 
-def lpf_sample(x, z1, z2, src1=False):
-    """x: input/output VGPR; z1, z2: (pair text, half) of the previous two outputs.  src1 (lab): the running sum, the
-    operand each add waits for, as src1 (a + b == b + a exactly; tools/lab/lpf_exec.hip timed a dependent add whose fresh
-    operand is src1 faster on a partial EXEC mask)"""
+def lpf_sample(x, z1, z2):
+    """x: input/output VGPR; z1, z2: (pair text, half) of the previous two outputs"""
     p1, h1 = z1
     p2, h2 = z2
-    add = (lambda a: f"v_add_f32 v{x}, v{a}, v{x}") if src1 else (lambda a: f"v_add_f32 v{x}, v{x}, v{a}")
     return [
         f"v_pk_mul_f32 v[{P1}:{P1 + 1}], %[c1], {p1} op_sel:[0,{h1}] op_sel_hi:[1,{h1}]",
         f"v_pk_mul_f32 v[{P2}:{P2 + 1}], %[c2], {p2} op_sel:[0,{h2}] op_sel_hi:[1,{h2}]",
-        add(P1),
-        add(P2),
-        add(P1 + 1),
-        add(P2 + 1),
+        f"v_add_f32 v{x}, v{x}, v{P1}",
+        f"v_add_f32 v{x}, v{x}, v{P2}",
+        f"v_add_f32 v{x}, v{x}, v{P1 + 1}",
+        f"v_add_f32 v{x}, v{x}, v{P2 + 1}",
     ]
 
 
@@ -144,7 +141,6 @@ def chunk(role, lds=True, split=False, il=False):
 
 
 SLOT = 16 * 68 * 4  # bytes per [stream][sample] chunk buffer (PG x ROW floats)
-SLOT64 = 64 * 68 * 4  # the same for ssb64.hip's 64-stream rows
 
 
 def lpf_loop():
@@ -241,35 +237,21 @@ def lpf_loop():
     return out
 
 
-GSLOT_LOG2 = 12  # SDRG_LPF_GSTORE: bytes per chunk slot of the global output ring (16 streams x 64 floats), 8 slots
-GRING = 8
-
-
-def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copies=False, src1=False, gstore=False,
-                         split=False):
+def lpf_loop_interleaved(copies=False, split=False):
     """lpf_loop() with the LDS traffic spread through the VALU stream: sub-blocks are numbered g = 4c + sb across
     chunks and live in buffer g mod 3; while sub-block g runs, after each 4-sample quad t its output quad is written
     and quad t of sub-block g + 2 is read (for sb = 2, 3 that is the next chunk's sub-block 0, 1, complete in its
     ring slot).  So at the barrier only the chunk's last write is outstanding (lgkmcnt(1)), and the first two
     sub-blocks of the next chunk are already in registers.  The last chunk's reads of a next chunk fetch a stale
     ring slot and are never used; the block drains them (lgkmcnt(0)) before it ends.
-    gstore (SDRG_LPF_GSTORE): the outputs go to a global ring of GRING chunk slots (%[ygs]: its base, SGPR pair; %[ybase]:
-    the lane's row offset in a slot) as global_store_dwordx4 -- a ds_write_b128 on 16 lanes costs the wave about 8
-    cycles per sample, a global store about 5 (tools/lab/lpf_io.hip) --; only the reads count on lgkmcnt, and before each
-    barrier the wave waits until only this chunk's 16 stores are in flight (vmcnt(16)), so the readers, one iteration
-    later, find the previous chunk's outputs in L2 (they load them past L1, sc1).
-    split (lab, SDRG_LPF_SPLIT): the chain's VALU on all 64 lanes (lanes 16-63 compute on whatever they hold and store
-    nothing), each quad's LDS write and read on the 16 stream lanes (EXEC switched by SALU around the pair)."""
+    Lab forms (--lab, not in the product): copies, all 64 lanes with lane l running stream l mod 16 (four copies: a
+    dependent chain issues faster on a full EXEC mask, and the copies write the same values to the same LDS
+    addresses); split, the chain's VALU on all 64 lanes (lanes 16-63 compute on whatever they hold and store nothing),
+    each quad's LDS write and read on the 16 stream lanes (EXEC switched by SALU around the pair)."""
+    assert not (copies and split)
     out = []
     u = "%="
-    # the 16 stream lanes: 0-15, or (spread) lanes {0-3, 16-19, 32-35, 48-51}; all_lanes: 64 streams, one per lane
-    # (ssb64.hip), with `slot` bytes per ring slot and the output ring's slot = chunk & ymask; copies (lab): all 64 lanes,
-    # lane l running stream l mod 16 (four identical copies: a dependent chain issues faster on a full EXEC mask, and
-    # the copies write the same values to the same LDS addresses)
-    if split:
-        assert not (spread or all_lanes or copies)
-    lanes = (["s_mov_b64 exec, -1"] if all_lanes or copies or split else
-             ["s_mov_b32 exec_lo, 0xf000f", "s_mov_b32 exec_hi, 0xf000f"] if spread else ["s_mov_b64 exec, 0xffff"])
+    lanes = ["s_mov_b64 exec, -1"] if copies or split else ["s_mov_b64 exec, 0xffff"]
     out += ["s_mov_b64 %[sv], exec"] + lanes + [
         "s_nop 4",
         "v_pk_mov_b32 v[46:47], %[z], %[z] op_sel:[1,0]",
@@ -282,8 +264,8 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
         f"s_cbranch_scc1 L_pre_{u}",
         "s_cmp_ge_i32 %[cc], %[nch]",
         f"s_cbranch_scc1 L_drain_{u}",
-        f"s_and_b32 %[yo], %[cc], {GRING - 1 if gstore else ymask}",
-        f"s_lshl_b32 %[yo], %[yo], {GSLOT_LOG2}" if gstore else f"s_mul_i32 %[yo], %[yo], {slot}",
+        "s_and_b32 %[yo], %[cc], 3",
+        f"s_mul_i32 %[yo], %[yo], {SLOT}",
         "v_add_u32 v54, %[yo], %[ybase]",
         "s_cmp_eq_u32 %[r], 0",
         f"s_cbranch_scc1 L_r0_{u}",
@@ -296,22 +278,19 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
         zb = BUFS[(r + 2) % 3]
         prev1, prev2 = pair(zb + 15), pair(zb + 14)
         for sb in range(4):
-            out.append(f"s_waitcnt lgkmcnt({4 if sb == 0 or gstore else 8})")
+            out.append(f"s_waitcnt lgkmcnt({4 if sb == 0 else 8})")
             b = BUFS[(r + sb) % 3]
             rb = BUFS[(r + sb + 2) % 3]                      # buffer of sub-block g + 2
             rslot, rsb = (r, sb + 2) if sb < 2 else ((r + 1) % 3, sb - 2)
             for q in range(16):
-                out += lpf_sample(b + q, prev1, prev2, src1)
+                out += lpf_sample(b + q, prev1, prev2)
                 prev2, prev1 = prev1, pair(b + q)
                 if q % 4 == 3:
                     t = q // 4
                     if split:
                         out.append("s_mov_b64 exec, 0xffff")
-                    if gstore:
-                        out.append(f"global_store_dwordx4 v54, v[{b + 4 * t}:{b + 4 * t + 3}], %[ygs] offset:{(16 * sb + 4 * t) * 4}")
-                    else:
-                        out.append(f"ds_write_b128 v54, v[{b + 4 * t}:{b + 4 * t + 3}] offset:{(16 * sb + 4 * t) * 4}")
-                    out.append(f"ds_read_b128 v[{rb + 4 * t}:{rb + 4 * t + 3}], %[abase] offset:{rslot * slot + (16 * rsb + 4 * t) * 4}")
+                    out.append(f"ds_write_b128 v54, v[{b + 4 * t}:{b + 4 * t + 3}] offset:{(16 * sb + 4 * t) * 4}")
+                    out.append(f"ds_read_b128 v[{rb + 4 * t}:{rb + 4 * t + 3}], %[abase] offset:{rslot * SLOT + (16 * rsb + 4 * t) * 4}")
                     if split:
                         out.append("s_mov_b64 exec, -1")
         last = BUFS[(r + 3) % 3] + 15
@@ -331,12 +310,10 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
     out += [
         f"s_branch L_bar_{u}",
         f"L_bar1_{u}:",
-        # this chunk's writes done (LDS), or all but this chunk's 16 stores (global); the last read of the next chunk
-        # may fly on
-        "s_waitcnt vmcnt(16)" if gstore else "s_waitcnt lgkmcnt(1)",
+        "s_waitcnt lgkmcnt(1)",             # this chunk's writes done; the last read of the next chunk may fly on
         f"s_branch L_bar_{u}",
         f"L_drain_{u}:",
-        "s_waitcnt vmcnt(0) lgkmcnt(0)" if gstore else "s_waitcnt lgkmcnt(0)",
+        "s_waitcnt lgkmcnt(0)",
         f"L_bar_{u}:",
         "s_barrier",
         "s_add_u32 %[it], %[it], 1",
@@ -349,130 +326,7 @@ def lpf_loop_interleaved(spread=False, all_lanes=False, slot=SLOT, ymask=3, copi
         f"L_next_{u}:",
         "s_cmp_lt_u32 %[it], %[nit]",
         f"s_cbranch_scc1 L_top_{u}",
-        # the last chunk's reads of a next chunk that does not exist (and, gstore, the last stores)
-        "s_waitcnt vmcnt(0) lgkmcnt(0)" if gstore else "s_waitcnt lgkmcnt(0)",
-        "s_mov_b64 exec, %[sv]",
-        "s_nop 4",
-        "v_pk_mov_b32 %[z], v[52:53], v[52:53] op_sel:[0,1]",
-    ]
-    return out
-
-
-# Chunk counters of the barrier-free pipeline (ssb.hip, SDRG_PIPE_FLAGS): byte offsets into PipeLds::prog.  Every role
-# publishes the number of chunks it has finished; a consumer waits on its producer's count, a producer on its
-# consumers' counts (ring-slot reuse).  The layout puts what the low-pass wave polls in two reads.
-PROG = {"des": 0, "out": 16, "dc": 20, "lpf": 24, "load": 28, "agc": 32, "fir0": 36, "fir1": 40, "eq": 44, "abort": 48}
-SPIN_LIMIT = 1 << 18  # polls (each after s_sleep 1) before a wait gives up and raises the abort word
-
-
-def lpf_loop_flags(slot=SLOT, ymask=3):
-    """lpf_loop_interleaved() without the workgroup barrier: the wave runs chunks 0 .. nch-1 at its own pace and
-    synchronises only with its neighbours through LDS chunk counters (%[pbase]: LDS byte address of PipeLds::prog).
-    Before chunk c it needs the DC wave's count >= min(c + 2, nch) (chunk c + 1's first sub-blocks are read during
-    chunk c) and the count of every reader of its output ring (the four desired-level waves and the clamp wave)
-    >= c - 3 (slot c mod 4 is free).  The counters for chunk c + 1 are read at the start of chunk c's third
-    sub-block, so the check costs no wait: the sub-block waits that follow retire them.  After chunk c the wave
-    adds 1 to its own count (one lane, ds_add_u32: LDS executes one wave's operations in order, so every output
-    write and input read of the chunk is done when another wave sees the count).  A wait that is not met polls
-    after s_sleep 1, at most SPIN_LIMIT times; then it raises the abort word (wrong results, but the kernel ends)."""
-    out = []
-    u = "%="
-    des, ocnt = PROG["des"], PROG["out"]
-    assert ocnt == des + 16 and PROG["dc"] == ocnt + 4
-
-    def flag_reads():
-        return [f"ds_read_b128 v[56:59], %[pbase] offset:{des}", f"ds_read_b64 v[60:61], %[pbase] offset:{ocnt}"]
-
-    def check(ok_label):
-        # chunk cc's needs: t1 = min(cc + 2, nch) from the DC count (v61), t2 = cc - 3 from min(DES0..3, OUT)
-        return [
-            "v_min3_i32 v56, v56, v57, v58",
-            "v_min3_i32 v56, v56, v59, v60",
-            "v_cmp_le_i32 vcc, %[t2], v56",
-            "v_cmp_le_i32 %[tm], %[t1], v61",
-            "s_and_b64 vcc, vcc, %[tm]",
-            f"s_cbranch_vccnz {ok_label}",
-        ]
-
-    out += ["s_mov_b64 %[sv], exec", "s_mov_b64 exec, 0xffff", "s_nop 4",
-            "v_pk_mov_b32 v[46:47], %[z], %[z] op_sel:[1,0]",
-            "v_pk_mov_b32 v[52:53], %[z], %[z] op_sel:[0,1]",
-            "v_mov_b32 v55, 1",
-            "s_mov_b32 %[cc], 0",
-            "s_mov_b32 %[r], 0",
-            "s_cmp_le_i32 %[nch], 0",
-            f"s_cbranch_scc1 L_end_{u}"]
-    out += flag_reads() + ["s_waitcnt lgkmcnt(0)"]
-    out += [
-        f"L_check_{u}:",                   # chunk cc's needs against the counters in v56-v61
-        "s_add_i32 %[t1], %[cc], 2",
-        "s_min_i32 %[t1], %[t1], %[nch]",
-        "s_sub_i32 %[t2], %[cc], 3",
-    ]
-    out += check(f"L_go_{u}")
-    out += ["s_mov_b32 %[yo], 0", f"L_spin_{u}:", "s_sleep 1",
-            f"ds_read_b32 v62, %[pbase] offset:{PROG['abort']}"] + flag_reads() + [
-            "s_waitcnt lgkmcnt(0)",
-            "v_cmp_ne_u32 vcc, 0, v62",
-            f"s_cbranch_vccnz L_go_{u}"]     # another wave gave up: run on (the results are already wrong)
-    out += check(f"L_go_{u}")
-    out += ["s_add_u32 %[yo], %[yo], 1", f"s_cmp_lt_u32 %[yo], {SPIN_LIMIT}", f"s_cbranch_scc1 L_spin_{u}",
-            "s_mov_b64 exec, 1", f"ds_write_b32 %[pbase], v55 offset:{PROG['abort']}", "s_mov_b64 exec, 0xffff"]
-    out += [
-        f"L_go_{u}:",
-        "s_cmp_lg_u32 %[cc], 0",
-        f"s_cbranch_scc1 L_disp_{u}",
-    ]
-    # chunk 0: its sub-blocks 0, 1 (buffers 0, 1 of slot 0); later chunks have them in registers already
-    out += [f"ds_read_b128 v[{BUFS[0] + 4 * i}:{BUFS[0] + 4 * i + 3}], %[abase] offset:{(4 * i) * 4}" for i in range(4)]
-    out += [f"ds_read_b128 v[{BUFS[1] + 4 * i}:{BUFS[1] + 4 * i + 3}], %[abase] offset:{(16 + 4 * i) * 4}" for i in range(4)]
-    out += [
-        f"L_disp_{u}:",
-        f"s_and_b32 %[yo], %[cc], {ymask}",
-        f"s_mul_i32 %[yo], %[yo], {slot}",
-        "v_add_u32 v54, %[yo], %[ybase]",
-        "s_cmp_eq_u32 %[r], 0",
-        f"s_cbranch_scc1 L_r0_{u}",
-        "s_cmp_eq_u32 %[r], 1",
-        f"s_cbranch_scc1 L_r1_{u}",
-        f"s_branch L_r2_{u}",
-    ]
-    for r in range(3):
-        out.append(f"L_r{r}_{u}:")
-        zb = BUFS[(r + 2) % 3]
-        prev1, prev2 = pair(zb + 15), pair(zb + 14)
-        for sb in range(4):
-            # sub-block 0: its reads were issued during the previous chunk's sub-block 2, followed by 8 operations;
-            # sub-blocks 1-3: 8 operations follow their last read (the counter add, if any, only makes it stricter)
-            out.append(f"s_waitcnt lgkmcnt({4 if sb == 0 else 8})")
-            if sb == 2:
-                out += flag_reads()            # the counters for chunk cc + 1, retired by sub-block 3's wait
-            b = BUFS[(r + sb) % 3]
-            rb = BUFS[(r + sb + 2) % 3]
-            rslot, rsb = (r, sb + 2) if sb < 2 else ((r + 1) % 3, sb - 2)
-            for q in range(16):
-                out += lpf_sample(b + q, prev1, prev2)
-                prev2, prev1 = prev1, pair(b + q)
-                if q % 4 == 3:
-                    t = q // 4
-                    out.append(f"ds_write_b128 v54, v[{b + 4 * t}:{b + 4 * t + 3}] offset:{(16 * sb + 4 * t) * 4}")
-                    out.append(f"ds_read_b128 v[{rb + 4 * t}:{rb + 4 * t + 3}], %[abase] offset:{rslot * slot + (16 * rsb + 4 * t) * 4}")
-        last = BUFS[(r + 3) % 3] + 15
-        out.append(f"v_pk_mov_b32 v[52:53], v[{last - 1}:{last}], v[{last - 1}:{last}] op_sel:[1,0]")
-        out.append(f"s_branch L_pub_{u}")
-    out += [
-        f"L_pub_{u}:",
-        "s_mov_b64 exec, 1",               # one lane adds 1 to the low-pass count
-        f"ds_add_u32 %[pbase], v55 offset:{PROG['lpf']}",
-        "s_mov_b64 exec, 0xffff",
-        "s_add_i32 %[cc], %[cc], 1",
-        "s_add_u32 %[r], %[r], 1",
-        "s_cmp_eq_u32 %[r], 3",
-        "s_cselect_b32 %[r], 0, %[r]",
-        "s_cmp_lt_i32 %[cc], %[nch]",
-        f"s_cbranch_scc1 L_check_{u}",
-        f"L_end_{u}:",
-        "s_waitcnt lgkmcnt(0)",            # the last chunk's reads of a chunk that does not exist
+        "s_waitcnt lgkmcnt(0)",             # the last chunk's reads of a next chunk that does not exist
         "s_mov_b64 exec, %[sv]",
         "s_nop 4",
         "v_pk_mov_b32 %[z], v[52:53], v[52:53] op_sel:[0,1]",
@@ -506,40 +360,6 @@ def main():
     emit("SDRG_LPF_LOOP_ASM", lpf_loop())
     print("// the same loop with the chunk's LDS reads and writes interleaved quad by quad (SDRG_LPF_INTERLEAVE)")
     emit("SDRG_LPF_LOOP_IL_ASM", lpf_loop_interleaved())
-    print("// the same loop without the workgroup barrier: LDS chunk counters (SDRG_PIPE_FLAGS; see lpf_loop_flags() in the")
-    print("// generator).  Extra operands: %[pbase] (v: LDS byte address of PipeLds::prog), temps %[t1], %[t2] (=&s), %[tm]")
-    print("// (=&s, 64-bit); clobbers v0-v62 and vcc")
-    emit("SDRG_LPF_LOOP_FLAGS_ASM", lpf_loop_flags())
-    for k, v in PROG.items():
-        print(f"#define SDRG_PROG_{k.upper()} {v // 4}")
-    print(f"#define SDRG_PIPE_SPIN_LIMIT {SPIN_LIMIT}")
-    print("// lab (SDRG_LPF_COPIES=1): the same loop on all 64 lanes, lane l running stream l mod 16 (four copies)")
-    emit("SDRG_LPF_LOOP_IL_COPIES_ASM", lpf_loop_interleaved(copies=True))
-    print("// lab (SDRG_LPF_SRC1=1, 2 with the copies): the interleaved loop with each add's running sum as src1")
-    emit("SDRG_LPF_LOOP_IL_SRC1_ASM", lpf_loop_interleaved(src1=True))
-    emit("SDRG_LPF_LOOP_IL_COPIES_SRC1_ASM", lpf_loop_interleaved(copies=True, src1=True))
-    print("// SDRG_LPF_GSTORE: the interleaved loop with its outputs stored to a global ring (see lpf_loop_interleaved); extra")
-    print("// operand %[ygs] (s, 64-bit: the ring's base), %[ybase] = the lane's row offset in a slot")
-    emit("SDRG_LPF_LOOP_IL_GSTORE_ASM", lpf_loop_interleaved(gstore=True))
-    print("// lab (SDRG_LPF_SPLIT=1): the interleaved loop's VALU on all 64 lanes, its LDS operations on the 16 stream lanes")
-    emit("SDRG_LPF_LOOP_IL_SPLIT_ASM", lpf_loop_interleaved(split=True))
-    print("// lab (SDRG_SERIAL_SPLIT): the DC and AGC interleaved chunks with their VALU on all 64 lanes and their LDS operations")
-    print("// on the caller's lanes (extra operand %[sv], =&s 64-bit)")
-    emit("SDRG_DC_CHUNK_IL_SPLIT_ASM", chunk("dc", il=True, split=True))
-    emit("SDRG_AGC_CHUNK_IL_SPLIT_ASM", chunk("agc", il=True, split=True))
-    print("// lab (SDRG_LPF_SPLIT=1 with SDRG_LPF_GSTORE=1): both")
-    emit("SDRG_LPF_LOOP_IL_SPLIT_GSTORE_ASM", lpf_loop_interleaved(split=True, gstore=True))
-    print(f"#define SDRG_LPF_GSLOT_LOG2 {GSLOT_LOG2}")
-    print(f"#define SDRG_LPF_GRING {GRING}")
-    print("// the same on the lanes {0-3, 16-19, 32-35, 48-51} (SDRG_SERIAL_LANES=1)")
-    emit("SDRG_LPF_LOOP_IL_SPREAD_ASM", lpf_loop_interleaved(spread=True))
-    print("// the low-pass chunk with its VALU on all 64 lanes and the LDS operations on the caller's lanes; extra operand")
-    print("// %[sv] (=&s, 64-bit): the caller's EXEC (lab option SDRG_LPF_ASM=2)")
-    emit("SDRG_LPF_CHUNK_SPLIT_ASM", chunk("lpf", split=True))
-    print("// lab only (tools/microbench/valu6.hip, SDRG_LPF_ASM=3 / 4): the low-pass chunk on register data, no LDS")
-    print("// operations (wrong results), on the caller's lanes / on all 64 lanes (extra operand %[sv] as above)")
-    emit("SDRG_LPF_CHUNK_NOLDS_ASM", chunk("lpf", lds=False))
-    emit("SDRG_LPF_CHUNK_NOLDS_SPLIT_ASM", chunk("lpf", lds=False, split=True))
     print("#define SDRG_CHUNK_CLOBBERS \\")
     regs = [f'"v{i}"' for i in range(T0 + 2)]
     for i in range(0, len(regs), 16):
@@ -549,13 +369,22 @@ def main():
 
 
 def main_lab():
-    """tools/lab/ssb64_lpf_asm.h: the lab-only 64-stream low-pass loop (tools/lab/ssb64.hip)"""
-    print("// Generated by tools/gen/gen_lpf_asm.py --lab -- do not edit.  Lab only (tools/lab/ssb64.hip, not in the product")
-    print("// library): the low-pass loop of lpf_loop_interleaved() on all 64 lanes, one stream each (64-stream rows, a")
-    print("// 2-slot output ring).")
+    """tools/lab/lab_lpf_asm.h: lab-only forms of the low-pass chunk and loop (tools/lab/lpf_loop_lab.hip,
+    tools/microbench/valu6.hip), included beside the product header; not in the product library"""
+    print("// Generated by tools/gen/gen_lpf_asm.py --lab -- do not edit.  Lab only (tools/lab, tools/microbench; not in the")
+    print("// product library): forms of the low-pass wave measured against the product's (DESIGN.md 3.3).  Include after")
+    print("// csrc/ssb_lpf_asm.h (operands and clobbers as there).")
     print("#pragma once")
-    emit("SDRG_LPF64_LOOP_IL_ASM", lpf_loop_interleaved(all_lanes=True, slot=SLOT64, ymask=1))
-    print(f"#define SDRG_LPF64_LOOP_SLOT_BYTES {SLOT64}")
+    print("// the interleaved loop on all 64 lanes, lane l running stream l mod 16 (four copies)")
+    emit("SDRG_LPF_LOOP_IL_COPIES_ASM", lpf_loop_interleaved(copies=True))
+    print("// the interleaved loop's VALU on all 64 lanes, its LDS operations on the 16 stream lanes")
+    emit("SDRG_LPF_LOOP_IL_SPLIT_ASM", lpf_loop_interleaved(split=True))
+    print("// the low-pass chunk with its VALU on all 64 lanes and the LDS operations on the caller's lanes; extra operand")
+    print("// %[sv] (=&s, 64-bit): the caller's EXEC")
+    emit("SDRG_LPF_CHUNK_SPLIT_ASM", chunk("lpf", split=True))
+    print("// the low-pass chunk on register data, no LDS operations (wrong results), on the caller's lanes / on all 64 lanes")
+    emit("SDRG_LPF_CHUNK_NOLDS_ASM", chunk("lpf", lds=False))
+    emit("SDRG_LPF_CHUNK_NOLDS_SPLIT_ASM", chunk("lpf", lds=False, split=True))
 
 
 if __name__ == "__main__":

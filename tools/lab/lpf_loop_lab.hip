@@ -2,12 +2,13 @@
 // workgroup that only meet its per-chunk barrier (the pipeline's other roles skipped), against the same chain with the
 // same per-quad LDS traffic at fixed addresses and a plain per-chunk barrier ("bar").  s_memtime cycles per sample,
 // the minimum of 5 launches after a warm-up.  Build: hipcc --offload-arch=gfx950 -O3 -I sdr-for-android-lib_amd/csrc
-//   -o tools/lab/lpf_loop_lab tools/lab/lpf_loop_lab.hip
+//   -I tools/lab -o tools/lab/lpf_loop_lab tools/lab/lpf_loop_lab.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 
 #include "ssb_lpf_asm.h"
+#include "lab_lpf_asm.h"  // tools/lab: the copies / split forms
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 constexpr int SLOT_F = 16 * 68;

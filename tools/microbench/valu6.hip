@@ -5,6 +5,7 @@
 #include <stdio.h>
 
 #include "../../sdr-for-android-lib_amd/csrc/ssb_lpf_asm.h"
+#include "../lab/lab_lpf_asm.h"  // the split / no-LDS lab forms
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 #pragma clang fp contract(off)
