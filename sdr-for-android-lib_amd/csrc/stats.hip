@@ -747,8 +747,8 @@ __device__ float kth_smallest_wave(Visit visit, int k, int *hist, uint32_t *xch)
 }
 
 // Narrow statistics, one wave per frame.  Every window's bins are staged compactly into LDS (window q at
-// sh_woff[q]), all of a lane's loads in flight at once; the focus peak's dB values are evaluated during that
-// copy (the other bins need no dB until the pool).  The reference's sequential sums run one lane per window
+// sh_woff[q]) by buffer loads straight into LDS, all of the frame's loads in flight at once; the focus peak's dB
+// values are evaluated from LDS right after (the other bins need no dB until the pool).  The reference's sequential sums run one lane per window
 // (the window scans) or per frame (the pooled mean, the scalar tail); the order-free work (copy, dB, pooled
 // gaps, select) runs across the lanes.  LDS per frame: the staged bins, over which the pool is laid out in
 // order once the scans are done (R > 0: pool values <= R per lane, held in registers for the select), or, for
@@ -756,17 +756,17 @@ __device__ float kth_smallest_wave(Visit visit, int k, int *hist, uint32_t *xch)
 // (84.5 KiB of LDS per CU) the frames that fit at once set the kernel's time.
 // Registers for eight waves per SIMD (<= 64 VGPRs; the 24-register pool variant six): the statistics of a pipelined
 // call then fit beside the next call's spectrum on every SIMD (its four waves hold 112 VGPRs each) instead of waiting
-// for its workgroups to retire.  The staging copy keeps NARROW_BATCH loads per lane in flight (16 needed 12 VGPRs
-// more than 64 allow and spilled).
+// for its workgroups to retire.
 // Measured (tools/gpu_r4n.sh, alternating, one box): alone 27.2 vs 26.7 us per 4096 frames; the c3 step with the
 // statistics on their own stream 0.3077-0.3088 ms against 0.3121-0.3124 (76 VGPRs) and 0.3141 on the main stream.
-#ifndef SDRG_NARROW_BATCH  // lab: loads per lane in flight in the staging copy
-#define SDRG_NARROW_BATCH 8
-#endif
+// Round 6 (tools/gpu_r6u.sh, alternating, one box): the staging copy as LDS-direct buffer loads, one instruction per
+// 64 bins of a window, instead of 8 register loads per lane in flight behind a 10-step window search per bin (50
+// VGPRs instead of 64, no second HBM round trip): alone 27.0 -> 26.6 us per 4096 x 16384 / 5 kHz and 47.0 -> 41.6 us
+// per 1024 x 65536 / 5 kHz; the configs[4] 5 kHz line 207.9 / 208.0 -> 216.6 / 216.5 G; bit-exact.
+
 #ifndef SDRG_NARROW_WPE  // lab: waves per SIMD the narrow kernel is compiled for
 #define SDRG_NARROW_WPE 8
 #endif
-constexpr int NARROW_BATCH = SDRG_NARROW_BATCH;
 template <int R>
 __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(R > 8 ? 6 : SDRG_NARROW_WPE))) void stats_narrow_kernel(
     const float *__restrict__ spectra, StatsGeometry g, int64_t now_ms, StatsState *__restrict__ state,
@@ -819,36 +819,29 @@ __global__ __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(R > 8 ? 6 
         float best = -130.0f;
         int bidx = 0x7fffffff;
         {
-            // staged bin i of window q reads P[i + dl[q]]; q = the number of window starts wo[] at or below i
-            int wo[10], dl[11];
-#pragma unroll
-            for (int k = 0; k < 11; k++) dl[k] = (k <= n_ref) ? sh_geo_lo[k] - sh_woff[k] : 0;
-#pragma unroll
-            for (int k = 0; k < 10; k++) wo[k] = (k < n_ref) ? sh_woff[k + 1] : 0x7fffffff;
+            // window q's bins straight into stage[woff[q] ..] by buffer loads to LDS (no registers, no per-bin
+            // window search): 64 bins per instruction, the window's offset in the scalar offset, every load of the
+            // frame in flight at once; then the focus bins' dB from LDS (a lane sees its focus bins in increasing
+            // order, strict > keeps each lane's first maximum; the reduction below takes the lower bin on ties, so
+            // the result does not depend on which lane holds which bin)
+            const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(P), (short)0,
+                                                                                 g.n * 4, 0x00020000);
+            for (int q = 0; q <= n_ref; q++) {
+                const int lo = __builtin_amdgcn_readfirstlane(sh_geo_lo[q]);
+                const int len = __builtin_amdgcn_readfirstlane(sh_geo_hi[q]) - lo + 1;
+                const int wo = __builtin_amdgcn_readfirstlane(sh_woff[q]);
+                for (int j0 = 0; j0 < len; j0 += WAVE)
+                    if (j0 + lane < len)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, (__attribute__((address_space(3))) void *)&stage[wo + j0],
+                                                                 4, lane * 4, (lo + j0) * 4, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS writes of this wave's loads are done
             const int foff = sh_woff[n_ref];
-            for (int base = lane; base < stage_total; base += NARROW_BATCH * WAVE) {
-                float v[NARROW_BATCH];
-#pragma unroll
-                for (int u = 0; u < NARROW_BATCH; u++) {
-                    const int i = base + WAVE * u;
-                    int d = dl[0];
-#pragma unroll
-                    for (int k = 0; k < 10; k++) d = (i >= wo[k]) ? dl[k + 1] : d;
-                    v[u] = (i < stage_total) ? P[i + d] : 0.0f;
-                }
-#pragma unroll
-                for (int u = 0; u < NARROW_BATCH; u++) {
-                    const int i = base + WAVE * u;
-                    if (i < stage_total) stage[i] = v[u];
-                    // the focus window is the last: a lane sees its bins in increasing order, strict > keeps
-                    // each lane's first maximum
-                    if (i >= foff && i < stage_total) {
-                        const float d = db_of(v[u]);
-                        if (d > best) {
-                            best = d;
-                            bidx = g.focus_lo + (i - foff);
-                        }
-                    }
+            for (int i = foff + lane; i < stage_total; i += WAVE) {
+                const float d = db_of(stage[i]);
+                if (d > best) {
+                    best = d;
+                    bidx = g.focus_lo + (i - foff);
                 }
             }
             for (int off = WAVE / 2; off > 0; off >>= 1) {  // first maximum over the lanes (lower bin on ties)
