@@ -46,6 +46,10 @@ ISO_LAUNCHES = 30  # launches of the spectrum stage alone behind roofline_isolat
 N_INPUTS = 3  # distinct input batches rotated per step: 3 x 128 MiB > the 256 MiB Infinity Cache
 SSB_ISO_CALLS = 20  # joined SSB-only calls timed for ssb_latency_floor.ssb_ms_alone
 PROFILED_STEPS = 20  # labelled lines: steps of the separate profiled pass behind their per-kernel times
+# labelled lines: timed steps at least this many (the headline times exactly --steps): a labelled line's own timed region
+# carries the same fixed fill / drain / clock cost (~0.3 ms) as the headline's, which over the driver's 20
+# steps hid their steady rate (configs[2] 9 % under it); each labelled dict records its steps
+LABELLED_MIN_STEPS = 100
 LAB_HOST_TIMES = os.environ.get("SDRG_BENCH_HOST_TIMES") == "1"
 LAB_NO_STEP_GATHER = os.environ.get("SDRG_BENCH_NO_STEP_GATHER") == "1"  # lab: the N > 1 path without its per-step gathers
 N_OUTPUTS = 3  # spectra / records buffers rotated per step (asynchronous statistics read a call's spectra late)
@@ -558,7 +562,7 @@ def main() -> int:
             eng.set_ssb_variant(NCO_HZ, 127)
         eng.set_pipelining(pipe_mode if mode is None else mode)
         eng.set_profiling(False)
-        for _ in range(3):
+        for _ in range(10):  # untimed, after the variant / schedule switch
             step(st)
         eng.synchronize()
         t1 = time.perf_counter()
@@ -575,7 +579,7 @@ def main() -> int:
         eng.set_profiling(False)
         if variant_on:
             eng.set_ssb_variant(0.0, 0)
-        r = {"value": round(k_steps * streams * n / dt / 1e6, 2), "ms_per_step": round(dt / k_steps * 1e3, 4),
+        r = {"value": round(k_steps * streams * n / dt / 1e6, 2), "ms_per_step": round(dt / k_steps * 1e3, 4), "steps": k_steps,
              "spectrum_ms": round(tm["spectrum_ms"], 4), "stats_ms": round(tm["stats_ms"], 4)}
         if st & sdrg.STAGE_SSB:
             r["ssb_ms"] = round(tm["ssb_ms"], 4)
@@ -617,7 +621,7 @@ def main() -> int:
         fft_bytes = 8.0 * s5 * n5  # CS16: 4 B in + 4 B float32 power out per sample
         step_b = fft_bytes + s5 * sdrg.RECORD_DTYPE.itemsize
         del iq5, sp5, rc5
-        return {"value": round(k_steps * s5 * n5 / dt / 1e6, 2), "ms_per_step": round(ms, 4),
+        return {"value": round(k_steps * s5 * n5 / dt / 1e6, 2), "ms_per_step": round(ms, 4), "steps": k_steps,
                 "spectrum_ms": round(tm["spectrum_ms"], 4), "stats_ms": round(tm["stats_ms"], 4),
                 "roofline_fft": {"kernel": "four_step_a + four_step_b", "achieved": round(fft_bytes / tm["spectrum_ms"]
                                                                                           / 1e6, 1),
@@ -628,11 +632,12 @@ def main() -> int:
                             f"+ fftshift + signal-strength stats over a {focus_c5} kHz focus; no SSB"}
 
     labelled = {}
+    k_lab = max(args.steps, LABELLED_MIN_STEPS)
     if not dist_on and args.config == "c3" and args.stages == "all" and not variant and not args.no_labelled:
         eng.set_profiling(False)
         # FFT + statistics alone: the statistics after the spectrum on one stream (--stats-async auto) unless forced
         c1_mode = pipelined | (sdrg.PIPELINE_STATS_ASYNC if async_ok and args.stats_async == "1" else 0)
-        labelled["configs1_fft_stats"] = dict(labelled_rate(sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS, args.steps,
+        labelled["configs1_fft_stats"] = dict(labelled_rate(sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS, k_lab,
                                                             mode=c1_mode),
                                               stats_async=bool(c1_mode & sdrg.PIPELINE_STATS_ASYNC),
                                               workload="BASELINE configs[1]: same batch, FFT + |X|^2 + fftshift + "
@@ -640,15 +645,15 @@ def main() -> int:
         if async_ok:  # the other statistics schedule of the same line, measured right after it (an A/B in the record)
             alt = pipelined | (0 if c1_mode & sdrg.PIPELINE_STATS_ASYNC else sdrg.PIPELINE_STATS_ASYNC)
             labelled["configs1_fft_stats_other_schedule"] = dict(
-                labelled_rate(sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS, args.steps, mode=alt),
+                labelled_rate(sdrg.STAGE_SPECTRUM | sdrg.STAGE_STATS, k_lab, mode=alt),
                 stats_async=bool(alt & sdrg.PIPELINE_STATS_ASYNC),
                 note="configs1_fft_stats with the statistics schedule flipped (--stats-async), not the line's choice")
-        labelled["configs2_nco127"] = dict(labelled_rate(sdrg.STAGE_ALL, args.steps, variant_on=True),
+        labelled["configs2_nco127"] = dict(labelled_rate(sdrg.STAGE_ALL, k_lab, variant_on=True),
                                            workload="BASELINE configs[2] as written (a build extension, not the "
                                                     f"reference chain): SSB with an NCO mixer at +{NCO_HZ / 1e3:g} kHz "
                                                     "+ 127-tap FIR decim 41, every other stage as the headline")
-        labelled["configs4_c5_5khz"] = c5_line(5, args.steps)
-        labelled["configs4_c5_200khz"] = c5_line(200, args.steps)
+        labelled["configs4_c5_5khz"] = c5_line(5, k_lab)
+        labelled["configs4_c5_200khz"] = c5_line(200, k_lab)
     if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
