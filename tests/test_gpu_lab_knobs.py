@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 KNOBS = {"SDRG_PIPE_SKIP": "0xfff", "SDRG_PIPE_MAP": "0", "SDRG_CU_SPLIT": "1", "SDRG_PIPE_PRIO": "0xfff",
          "SDRG_SSB_REFERENCE_KERNELS": "1", "SDRG_SPECTRUM_GRID": "3", "SDRG_STREAM_PRIO": "-1,1",
-         "SDRG_EVENT_FENCE": "1", "SDRG_PIPE_STAMPS": "1", "SDRG_K16_ALONE": "1", "SDRG_QUEUES": "31,1",
+         "SDRG_EVENT_FENCE": "1", "SDRG_PIPE_STAMPS": "1", "SDRG_QUEUES": "31,1",
          "SDRG_GATHER_STREAM": "1", "SDRG_WIDE_SINGLE": "1", "SDRG_SSB_FIRST": "1", "SDRG_STATS_CUS": "32"}
 
 
